@@ -1,0 +1,337 @@
+"""Python mirror of HundDB's ``utils/crc`` package over libhundcrc.so.
+
+Same names, argument meaning and error behaviour as
+/root/reference/utils/crc/crc_util.go:10-122, so the parity tests read like the
+reference's own Go tests:
+
+=========================  ==========================================  ====================
+Go (crc_util.go)           here                                        C ABI (hundcrc.h)
+=========================  ==========================================  ====================
+BLOCK_SIZE, CRC_SIZE :11   BLOCK_SIZE, CRC_SIZE                        HC_BLOCK_SIZE/CRC_SIZE
+GetCRC :15                 GetCRC(data) -> int                         hc_crc32_ieee
+AddCRCToBlockData :21      AddCRCToBlockData(bytearray) -> same obj    hc_add_crc_block
+AddCRCsToData :41          AddCRCsToData(data) -> bytearray            hc_add_crcs
+SizeAfterAddingCRCs :69    SizeAfterAddingCRCs(n) -> int               hc_size_after_crcs
+SizeWithoutCRCs :79        SizeWithoutCRCs(n) -> int                   hc_size_without_crcs
+CheckBlockIntegrity :88    CheckBlockIntegrity(data) -> error|None     hc_check_block
+FixLastBlockCRC :106       FixLastBlockCRC(bytearray) -> error|None    hc_fix_last_block
+=========================  ==========================================  ====================
+
+Go returns ``error`` values instead of raising, so these functions return
+``None`` or a :class:`CRCError` whose ``str()`` is the exact ``errors.New``
+text.  Library failures (no GPU for a batch entry, HIP errors) raise
+:class:`HundCRCError`: the batched GPU path never falls back to the CPU.
+
+The batched entries (``crc32_blocks``, ``verify_blocks``, ``stamp_blocks``,
+``crc32_messages`` and their ``dev_*`` forms on torch device tensors) are the
+GPU hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+BLOCK_SIZE = 4096  # crc_util.go:11
+CRC_SIZE = 4       # crc_util.go:12
+
+HC_OK = 0
+HC_ERR_INVALID_BLOCK = 1
+HC_ERR_CRC_MISMATCH = 2
+HC_ERR_TOO_SHORT = 3
+HC_F_STAMP = 1
+HC_F_MESSAGES = 2
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhundcrc.so")
+
+
+class HundCRCError(RuntimeError):
+    """A library-level failure (argument, HIP, no device)."""
+
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {_lib().hc_strerror(code).decode()} (code {code})")
+
+
+class CRCError(Exception):
+    """Mirror of the Go ``error`` values returned by utils/crc."""
+
+    def __init__(self, code: int):
+        self.code = code
+        super().__init__(_lib().hc_strerror(code).decode())
+
+    def __eq__(self, other):  # errors.New values compare by identity in Go; by text here
+        return isinstance(other, CRCError) and str(other) == str(self)
+
+    __hash__ = Exception.__hash__
+
+
+class LaunchInfo(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_char_p), ("fast_blocks", ctypes.c_uint64),
+                ("general_blocks", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("grid", ctypes.c_uint32), ("block_threads", ctypes.c_uint32),
+                ("lds_bytes", ctypes.c_uint32)]
+
+
+_LIB = None
+_u8p = ctypes.c_void_p
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(_LIB_PATH):
+            raise ImportError(f"{_LIB_PATH} is missing: run `make -C hunddb_amd` or "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(_LIB_PATH)
+        P, S, U32, U64, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        sig = {
+            "hc_strerror": (ctypes.c_char_p, [I]),
+            "hc_version": (ctypes.c_char_p, []),
+            "hc_crc32_ieee": (U32, [P, S]),
+            "hc_add_crc_block": (I, [P, S]),
+            "hc_add_crcs_size": (S, [S]),
+            "hc_add_crcs": (S, [P, S, P, S]),
+            "hc_size_after_crcs": (U64, [U64]),
+            "hc_size_without_crcs": (U64, [U64]),
+            "hc_check_block": (I, [P, S]),
+            "hc_fix_last_block": (I, [P, S]),
+            "hc_crc32_blocks": (I, [P, P, P, U64, U32, U64, P]),
+            "hc_verify_blocks": (I, [P, P, P, U64, U32, U64, P, P]),
+            "hc_stamp_blocks": (I, [P, P, P, U64, U32, U64]),
+            "hc_crc32_messages": (I, [P, P, P, U64, P]),
+            "hc_dev_crc32_blocks": (I, [I, P, P, P, U64, U32, U64, P, P, P, U32, P]),
+            "hc_dev_verify_prepare": (I, [I, P, P, U64, P]),
+            "hc_dev_fill_blocks": (I, [I, P, P, P, U64, U32, U64, U64, P]),
+            "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
+            "hc_debug_tables": (I, [P, S]),
+            "hc_device_count": (I, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        _LIB = L
+    return _LIB
+
+
+def lib():
+    """The loaded libhundcrc.so (ctypes.CDLL)."""
+    return _lib()
+
+
+# ---- buffer helpers --------------------------------------------------------
+def _ro_ptr(data):
+    """(address, length, keepalive) of a bytes-like object without copying."""
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+        return a.ctypes.data, a.nbytes, a
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        a = np.frombuffer(mv, dtype=np.uint8)
+        return a.ctypes.data, a.nbytes, a
+    a = np.frombuffer(mv, dtype=np.uint8)
+    return a.ctypes.data, a.nbytes, a
+
+
+def _rw_ptr(data):
+    if isinstance(data, np.ndarray):
+        if not data.flags.c_contiguous or not data.flags.writeable:
+            raise ValueError("need a writable contiguous array")
+        return data.ctypes.data, data.nbytes, data
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        raise TypeError("need a writable buffer (bytearray / numpy array)")
+    a = np.frombuffer(mv, dtype=np.uint8)
+    return a.ctypes.data, a.nbytes, a
+
+
+def _err(code: int) -> Optional[CRCError]:
+    if code == HC_OK:
+        return None
+    if code > 0:
+        return CRCError(code)
+    raise HundCRCError(code)
+
+
+# ---- drop-ins (crc_util.go) --------------------------------------------------
+def GetCRC(data) -> int:
+    """crc_util.go:15-17 — crc32.ChecksumIEEE(data)."""
+    p, n, _k = _ro_ptr(data)
+    return int(_lib().hc_crc32_ieee(p if n else None, n))
+
+
+def AddCRCToBlockData(data):
+    """crc_util.go:21-33 — stamps data[0:4] in place and returns the same object."""
+    p, n, _k = _rw_ptr(data)
+    rc = _lib().hc_add_crc_block(p if n else None, n)
+    if rc < 0:
+        raise HundCRCError(rc, "AddCRCToBlockData")
+    return data
+
+
+def AddCRCsToData(serialized) -> bytearray:
+    """crc_util.go:41-64 — frame into 4096-byte blocks with 4092-byte payloads."""
+    p, n, _k = _ro_ptr(serialized)
+    L = _lib()
+    out = bytearray(L.hc_add_crcs_size(n))
+    if not out:
+        return out
+    op, on, _ok = _rw_ptr(out)
+    wrote = L.hc_add_crcs(p, n, op, on)
+    if wrote == ctypes.c_size_t(-1).value:
+        raise HundCRCError(-1, "AddCRCsToData")
+    return out
+
+
+def SizeAfterAddingCRCs(n: int) -> int:
+    """crc_util.go:69-74 (float64 ceil semantics)."""
+    return int(_lib().hc_size_after_crcs(n))
+
+
+def SizeWithoutCRCs(n: int) -> int:
+    """crc_util.go:79-83 (float64 ceil, uint64 wrap)."""
+    return int(_lib().hc_size_without_crcs(n))
+
+
+def CheckBlockIntegrity(block) -> Optional[CRCError]:
+    """crc_util.go:88-100 — None, or CRCError("invalid block data" | "CRC mismatch in block")."""
+    p, n, _k = _ro_ptr(block)
+    return _err(_lib().hc_check_block(p if n else None, n))
+
+
+def FixLastBlockCRC(data) -> Optional[CRCError]:
+    """crc_util.go:106-122 — restamp the last complete 4096-byte block in place."""
+    p, n, _k = _rw_ptr(data)
+    return _err(_lib().hc_fix_last_block(p if n else None, n))
+
+
+# ---- batched, host-resident (GPU) ---------------------------------------------
+def _meta(off, lens):
+    o = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    l = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint32)
+    return o, l
+
+
+def _nblocks(buf_len, off, lens, stride, ulen, nblocks):
+    if nblocks is not None:
+        return int(nblocks)
+    if off is not None:
+        return len(off)
+    if lens is not None:
+        return len(lens)
+    if stride:
+        return buf_len // stride
+    raise ValueError("cannot infer the block count")
+
+
+def crc32_blocks(buf, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None) -> np.ndarray:
+    """CRC of block[4:len] for every block (what CheckBlockIntegrity computes), on the GPU."""
+    p, n, _k = _ro_ptr(buf)
+    o, l = _meta(off, lens)
+    nb = _nblocks(n, o, l, stride, ulen, nblocks)
+    out = np.zeros(nb, dtype=np.uint32)
+    rc = _lib().hc_crc32_blocks(p, None if o is None else o.ctypes.data,
+                                None if l is None else l.ctypes.data, stride, ulen, nb, out.ctypes.data)
+    if rc != HC_OK:
+        raise HundCRCError(rc, "crc32_blocks")
+    return out
+
+
+def verify_blocks(buf, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None):
+    """Batched CheckBlockIntegrity: (err | None, bad_bitmap uint32[], first_bad int)."""
+    p, n, _k = _ro_ptr(buf)
+    o, l = _meta(off, lens)
+    nb = _nblocks(n, o, l, stride, ulen, nblocks)
+    bm = np.zeros((nb + 31) // 32, dtype=np.uint32)
+    fb = ctypes.c_int64(-1)
+    rc = _lib().hc_verify_blocks(p, None if o is None else o.ctypes.data,
+                                 None if l is None else l.ctypes.data, stride, ulen, nb,
+                                 bm.ctypes.data if nb else None, ctypes.addressof(fb))
+    return _err(rc), bm, fb.value
+
+
+def stamp_blocks(buf, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None):
+    """Batched AddCRCToBlockData (in place)."""
+    p, n, _k = _rw_ptr(buf)
+    o, l = _meta(off, lens)
+    nb = _nblocks(n, o, l, stride, ulen, nblocks)
+    rc = _lib().hc_stamp_blocks(p, None if o is None else o.ctypes.data,
+                                None if l is None else l.ctypes.data, stride, ulen, nb)
+    if rc != HC_OK:
+        raise HundCRCError(rc, "stamp_blocks")
+    return buf
+
+
+def crc32_messages(buf, off, lens) -> np.ndarray:
+    """GetCRC of every variable-length message buf[off[i]:off[i]+lens[i]], on the GPU."""
+    p, n, _k = _ro_ptr(buf)
+    o, l = _meta(off, lens)
+    out = np.zeros(len(o), dtype=np.uint32)
+    rc = _lib().hc_crc32_messages(p, o.ctypes.data, l.ctypes.data, len(o), out.ctypes.data)
+    if rc != HC_OK:
+        raise HundCRCError(rc, "crc32_messages")
+    return out
+
+
+# ---- batched, device-resident (torch tensors as device memory only) ------------
+def _tptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def dev_crc32_blocks(buf, crc_out=None, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE,
+                     nblocks=None, bad_bitmap=None, first_bad=None, flags=0, stream=None):
+    """Enqueue the CRC kernel on device tensors (uint8 buf; uint64 off; int32/uint32 lens;
+    int32 crc_out / bad_bitmap; int64 first_bad).  Asynchronous on `stream`."""
+    nb = _nblocks(buf.numel(), off, lens, stride, ulen, nblocks)
+    dev = buf.device.index if buf.device.index is not None else 0
+    rc = _lib().hc_dev_crc32_blocks(dev, buf.data_ptr(), _tptr(off), _tptr(lens), stride, ulen, nb,
+                                    _tptr(crc_out), _tptr(bad_bitmap), _tptr(first_bad), flags,
+                                    _stream_ptr(stream))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_crc32_blocks")
+    return crc_out
+
+
+def dev_verify_prepare(bad_bitmap, first_bad, nblocks, stream=None):
+    dev = first_bad.device.index or 0
+    rc = _lib().hc_dev_verify_prepare(dev, _tptr(bad_bitmap), _tptr(first_bad), nblocks, _stream_ptr(stream))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_verify_prepare")
+
+
+def dev_fill_blocks(buf, seed, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None,
+                    stream=None):
+    nb = _nblocks(buf.numel(), off, lens, stride, ulen, nblocks)
+    dev = buf.device.index if buf.device.index is not None else 0
+    rc = _lib().hc_dev_fill_blocks(dev, buf.data_ptr(), _tptr(off), _tptr(lens), stride, ulen, nb,
+                                   seed & ((1 << 64) - 1), _stream_ptr(stream))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_fill_blocks")
+
+
+def last_launch() -> dict:
+    info = LaunchInfo()
+    _lib().hc_last_launch(ctypes.byref(info))
+    return {f: (getattr(info, f).decode() if f == "kernel" and getattr(info, f) else getattr(info, f))
+            for f, _ in LaunchInfo._fields_}
+
+
+def device_count() -> int:
+    return int(_lib().hc_device_count())
+
+
+def debug_tables() -> np.ndarray:
+    L = _lib()
+    size = L.hc_debug_tables(None, 0)
+    buf = np.zeros(size // 4, dtype=np.uint32)
+    assert L.hc_debug_tables(buf.ctypes.data, size) == 0
+    return buf

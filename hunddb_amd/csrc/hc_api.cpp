@@ -1,0 +1,548 @@
+// hc_api.cpp — C ABI of libhundcrc.so (include/hundcrc.h): the drop-in
+// utils/crc surface (/root/reference/utils/crc/crc_util.go:10-122) and the
+// batched GPU entries, plus the host runtime behind them (per-device constant
+// tables, per-thread streams, pinned staging ring with H2D/kernel/D2H overlap).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/hundcrc.h"
+#include "hc_gf2.hpp"
+#include "hc_kernels.hpp"
+
+namespace hc {
+uint32_t cpu_crc32_update(uint32_t crc, const uint8_t *p, size_t n);
+}
+
+using namespace hc;
+
+namespace {
+
+constexpr size_t kPayloadPerBlock = HC_BLOCK_SIZE - HC_CRC_SIZE;  // 4092 (crc_util.go:43)
+
+// ---------------------------------------------------------------------------
+// Devices
+struct DeviceState {
+  std::once_flag once;
+  int status = HC_E_NODEV;
+  int cus = 0;
+  DeviceTables *dtab = nullptr;  // device copy of the constant image
+};
+
+constexpr int kMaxDevices = 64;
+DeviceState g_dev[kMaxDevices];
+
+const DeviceTables &host_tables() {
+  static const DeviceTables *t = [] {
+    auto *p = new DeviceTables;
+    build_device_tables(*p);
+    return p;
+  }();
+  return *t;
+}
+
+struct DeviceGuard {  // keep the caller's current device untouched
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int device_count_raw() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int init_device(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return HC_E_ARG;
+  DeviceState &d = g_dev[dev];
+  std::call_once(d.once, [&] {
+    if (dev >= device_count_raw()) return;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return;  // kernels are gfx950-only
+    DeviceGuard g(dev);
+    void *p = nullptr;
+    if (hipMalloc(&p, sizeof(DeviceTables)) != hipSuccess) {
+      d.status = HC_E_NOMEM;
+      return;
+    }
+    if (hipMemcpy(p, &host_tables(), sizeof(DeviceTables), hipMemcpyHostToDevice) != hipSuccess) {
+      d.status = HC_E_HIP;
+      return;
+    }
+    d.dtab = static_cast<DeviceTables *>(p);
+    d.cus = prop.multiProcessorCount;
+    d.status = HC_OK;
+  });
+  return d.status;
+}
+
+int env_int(const char *name, int dflt) {
+  const char *v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+int default_device() { return env_int("HC_DEVICE", 0); }
+
+thread_local hc_launch_info t_last{"", 0, 0, 0, 0, 0, 0};
+
+// ---------------------------------------------------------------------------
+// Device batch dispatch (shared by _dev_ entries and the host pipeline)
+int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+             uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t *bitmap, int64_t *first_bad,
+             uint32_t flags, hipStream_t s, uint64_t bytes_hint) {
+  DeviceState &d = g_dev[dev];
+  Batch b{};
+  b.base = base;
+  b.off = off;
+  b.len = len;
+  b.stride = stride;
+  b.ulen = ulen;
+  b.flags = flags & (kFlagStamp | kFlagMessages);
+  b.nblocks = n;
+  b.crc_out = crc_out;
+  b.bad_bitmap = bitmap;
+  b.first_bad = reinterpret_cast<unsigned long long *>(first_bad);
+  b.tables = d.dtab;
+  if (n == 0) return HC_OK;
+  const int fast_grid = d.cus;  // one 1024-thread, 144 KiB-LDS workgroup per CU
+  int gen_grid = (int)std::min<uint64_t>((n + kGenWaves - 1) / kGenWaves, (uint64_t)d.cus * 8);
+  hc_launch_info info{"k_crc_fast", 0, 0, bytes_hint, (uint32_t)fast_grid, kFastThreads,
+                      kFastLdsBytes};
+  hipError_t e = hipSuccess;
+  if (!off && !len) {
+    const bool fast = ulen >= 1024 && (ulen & 1023u) == 0 &&
+                      (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (stride & 15u) == 0;
+    if (fast) {
+      e = launch_fast(b, true, fast_grid, s);
+      info.fast_blocks = n;
+    } else {
+      e = launch_general(b, false, gen_grid, s);
+      info.kernel = "k_crc_general";
+      info.general_blocks = n;
+      info.grid = gen_grid;
+      info.block_threads = kGenThreads;
+      info.lds_bytes = 8192;
+    }
+  } else {
+    e = launch_fast(b, false, fast_grid, s);
+    if (e == hipSuccess) e = launch_general(b, true, gen_grid, s);
+    info.kernel = "k_crc_fast+k_crc_general";
+    info.fast_blocks = n;  // routing is decided on the device per block
+  }
+  t_last = info;
+  return e == hipSuccess ? HC_OK : HC_E_HIP;
+}
+
+// ---------------------------------------------------------------------------
+// Host-resident batches: per-thread pipeline through pinned staging.
+struct Slot {
+  uint8_t *pin = nullptr;    // pinned staging (blocks, packed, 16-B aligned)
+  uint64_t *pin_off = nullptr;
+  uint32_t *pin_len = nullptr;
+  uint32_t *pin_crc = nullptr;
+  uint8_t *dbuf = nullptr;
+  uint64_t *doff = nullptr;
+  uint32_t *dlen = nullptr;
+  uint32_t *dcrc = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint64_t i0 = 0, nb = 0;  // block range of the in-flight chunk
+  bool busy = false;
+};
+
+struct HostPipe {
+  int dev = -1;
+  size_t chunk = 0;   // staging bytes per slot
+  size_t maxblk = 0;  // metadata capacity per slot
+  Slot slot[2];
+  bool ok = false;
+
+  int init(int d) {
+    if (ok && dev == d) return HC_OK;
+    release();
+    dev = d;
+    chunk = (size_t)env_int("HC_CHUNK_MB", 64) << 20;
+    maxblk = chunk / 64 + 1;
+    DeviceGuard g(dev);
+    for (auto &s : slot) {
+      if (hipHostMalloc(reinterpret_cast<void **>(&s.pin), chunk, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&s.pin_off), maxblk * 8, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&s.pin_len), maxblk * 4, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&s.pin_crc), maxblk * 4, hipHostMallocDefault) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void **>(&s.dbuf), chunk) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void **>(&s.doff), maxblk * 8) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void **>(&s.dlen), maxblk * 4) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void **>(&s.dcrc), maxblk * 4) != hipSuccess ||
+          hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+        release();
+        return HC_E_NOMEM;
+      }
+    }
+    ok = true;
+    return HC_OK;
+  }
+  void release() {
+    if (dev < 0) return;
+    DeviceGuard g(dev);
+    for (auto &s : slot) {
+      if (s.stream) (void)hipStreamSynchronize(s.stream);
+      if (s.pin) (void)hipHostFree(s.pin);
+      if (s.pin_off) (void)hipHostFree(s.pin_off);
+      if (s.pin_len) (void)hipHostFree(s.pin_len);
+      if (s.pin_crc) (void)hipHostFree(s.pin_crc);
+      if (s.dbuf) (void)hipFree(s.dbuf);
+      if (s.doff) (void)hipFree(s.doff);
+      if (s.dlen) (void)hipFree(s.dlen);
+      if (s.dcrc) (void)hipFree(s.dcrc);
+      if (s.stream) (void)hipStreamDestroy(s.stream);
+      if (s.done) (void)hipEventDestroy(s.done);
+      s = Slot{};
+    }
+    ok = false;
+  }
+  ~HostPipe() { release(); }
+};
+
+thread_local HostPipe t_pipe;
+
+inline uint64_t blk_off(const uint64_t *off, uint64_t stride, uint64_t i) { return off ? off[i] : i * stride; }
+inline uint32_t blk_len(const uint32_t *len, uint32_t ulen, uint64_t i) { return len ? len[i] : ulen; }
+
+// Runs CRCs of host blocks on the GPU; results into crc_out[0..n).  Blocks
+// larger than one staging slot are rejected (HC_E_ARG): the on-disk block
+// sizes are 4-16 KiB (utils/config/config.go:137, README.md:191,255).
+int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+               uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t flags) {
+  const int dev = default_device();
+  int st = init_device(dev);
+  if (st != HC_OK) return st;
+  HostPipe &P = t_pipe;
+  if ((st = P.init(dev)) != HC_OK) return st;
+  DeviceGuard g(dev);
+  uint64_t i = 0, chunks = 0;
+  int rc = HC_OK;
+  auto retire = [&](Slot &s) -> int {
+    if (!s.busy) return HC_OK;
+    s.busy = false;
+    if (hipEventSynchronize(s.done) != hipSuccess) return HC_E_HIP;
+    std::memcpy(crc_out + s.i0, s.pin_crc, s.nb * 4);
+    return HC_OK;
+  };
+  while (i < n && rc == HC_OK) {
+    Slot &s = P.slot[chunks & 1];
+    if ((rc = retire(s)) != HC_OK) break;
+    // gather blocks [i, j) into the slot (16-B aligned packing)
+    uint64_t j = i, pos = 0;
+    bool uniform = true;
+    const uint32_t l0 = blk_len(len, ulen, i);
+    while (j < n && j - i < P.maxblk) {
+      const uint32_t l = blk_len(len, ulen, j);
+      const uint64_t need = (pos + l + 15) & ~uint64_t(15);
+      if (need > P.chunk) break;
+      std::memcpy(s.pin + pos, base + blk_off(off, stride, j), l);
+      s.pin_off[j - i] = pos;
+      s.pin_len[j - i] = l;
+      uniform = uniform && l == l0;
+      pos = need;
+      j++;
+    }
+    if (j == i) {
+      rc = HC_E_ARG;  // a single block larger than the staging slot
+      break;
+    }
+    const uint64_t nb = j - i;
+    const bool packed_uniform = uniform && (l0 & 15u) == 0;  // then off = k*l0
+    if (hipMemcpyAsync(s.dbuf, s.pin, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+      rc = HC_E_HIP;
+      break;
+    }
+    if (!packed_uniform) {
+      if (hipMemcpyAsync(s.doff, s.pin_off, nb * 8, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+          hipMemcpyAsync(s.dlen, s.pin_len, nb * 4, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+        rc = HC_E_HIP;
+        break;
+      }
+    }
+    rc = packed_uniform
+             ? dispatch(dev, s.dbuf, nullptr, nullptr, l0, l0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos)
+             : dispatch(dev, s.dbuf, s.doff, s.dlen, 0, 0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos);
+    if (rc != HC_OK) break;
+    if (hipMemcpyAsync(s.pin_crc, s.dcrc, nb * 4, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+        hipEventRecord(s.done, s.stream) != hipSuccess) {
+      rc = HC_E_HIP;
+      break;
+    }
+    s.i0 = i;
+    s.nb = nb;
+    s.busy = true;
+    i = j;
+    chunks++;
+  }
+  for (auto &s : P.slot) {
+    int r = retire(s);
+    if (rc == HC_OK) rc = r;
+  }
+  return rc;
+}
+
+// HC_FORCE_GPU=1 routes the single-buffer drop-ins through the GPU batch path
+// too (read per call so tests can toggle it).
+int force_gpu() { return env_int("HC_FORCE_GPU", 0); }
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+extern "C" {
+
+const char *hc_strerror(int code) {
+  switch (code) {
+    case HC_OK: return "";
+    case HC_ERR_INVALID_BLOCK: return "invalid block data";
+    case HC_ERR_CRC_MISMATCH: return "CRC mismatch in block";
+    case HC_ERR_TOO_SHORT: return "data is too short to contain a complete block";
+    case HC_E_ARG: return "hundcrc: invalid argument";
+    case HC_E_HIP: return "hundcrc: HIP runtime error";
+    case HC_E_NODEV: return "hundcrc: no gfx950 device available (the GPU path never falls back to the CPU)";
+    case HC_E_NOMEM: return "hundcrc: device or pinned allocation failed";
+    case HC_E_LAYOUT: return "hundcrc: device batch violates the layout contract";
+    default: return "hundcrc: unknown error";
+  }
+}
+
+const char *hc_version(void) { return "hundcrc 0.1.0 (gfx950)"; }
+
+int hc_device_count(void) {
+  int n = device_count_raw(), good = 0;
+  for (int i = 0; i < n && i < kMaxDevices; i++) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, i) == hipSuccess &&
+        std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+      good++;
+  }
+  return good;
+}
+
+// ---- drop-ins ---------------------------------------------------------------
+uint32_t hc_crc32_ieee(const uint8_t *p, size_t n) {
+  if (n == 0) return 0;
+  if (force_gpu()) {
+    uint64_t o = 0;
+    uint32_t l = (uint32_t)n, c = 0;
+    if (n <= 0xFFFFFFFFu && host_batch(p, &o, &l, 0, 0, 1, &c, kFlagMessages) == HC_OK) return c;
+  }
+  return hc::cpu_crc32_update(0, p, n);
+}
+
+int hc_add_crc_block(uint8_t *p, size_t n) {
+  if (n < HC_CRC_SIZE) return HC_OK;  // crc_util.go:22-24
+  if (!p) return HC_E_ARG;
+  uint32_t c;
+  if (force_gpu() && n <= 0xFFFFFFFFu) {
+    uint64_t o = 0;
+    uint32_t l = (uint32_t)n;
+    int rc = host_batch(p, &o, &l, 0, 0, 1, &c, 0);
+    if (rc != HC_OK) return rc;
+  } else {
+    c = hc::cpu_crc32_update(0, p + HC_CRC_SIZE, n - HC_CRC_SIZE);
+  }
+  std::memcpy(p, &c, 4);  // binary.LittleEndian.PutUint32 (crc_util.go:30)
+  return HC_OK;
+}
+
+size_t hc_add_crcs_size(size_t n) { return (n + kPayloadPerBlock - 1) / kPayloadPerBlock * HC_BLOCK_SIZE; }
+
+size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
+  const size_t out = hc_add_crcs_size(n);
+  if (out > dst_cap || (n && (!src || !dst))) return (size_t)-1;
+  const size_t nb = out / HC_BLOCK_SIZE;
+  // framing: zeroed 4096-byte blocks, payload at [4:] (crc_util.go:48-60)
+  for (size_t b = 0; b < nb; b++) {
+    uint8_t *blk = dst + b * HC_BLOCK_SIZE;
+    const size_t s = b * kPayloadPerBlock, e = std::min(n, s + kPayloadPerBlock);
+    std::memset(blk, 0, HC_CRC_SIZE);
+    std::memcpy(blk + HC_CRC_SIZE, src + s, e - s);
+    if (e - s < kPayloadPerBlock) std::memset(blk + HC_CRC_SIZE + (e - s), 0, kPayloadPerBlock - (e - s));
+  }
+  // CRCs: one GPU batch for multi-block outputs, host for a single block
+  static const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", 256);
+  if (nb >= gpu_min || (force_gpu() && nb > 0)) {
+    std::vector<uint32_t> crc(nb);
+    int rc = host_batch(dst, nullptr, nullptr, HC_BLOCK_SIZE, HC_BLOCK_SIZE, nb, crc.data(), 0);
+    if (rc != HC_OK) return (size_t)-1;
+    for (size_t b = 0; b < nb; b++) std::memcpy(dst + b * HC_BLOCK_SIZE, &crc[b], 4);
+  } else {
+    for (size_t b = 0; b < nb; b++) {
+      uint8_t *blk = dst + b * HC_BLOCK_SIZE;
+      const uint32_t c = hc::cpu_crc32_update(0, blk + HC_CRC_SIZE, kPayloadPerBlock);
+      std::memcpy(blk, &c, 4);
+    }
+  }
+  return out;
+}
+
+uint64_t hc_size_after_crcs(uint64_t n) {
+  // int(math.Ceil(float64(n) / float64(4092))) -- crc_util.go:70-71
+  const int64_t nb = (int64_t)std::ceil((double)n / (double)kPayloadPerBlock);
+  return n + (uint64_t)nb * HC_CRC_SIZE;
+}
+
+uint64_t hc_size_without_crcs(uint64_t n) {
+  // uint64(math.Ceil(float64(n) / float64(4096))) -- crc_util.go:80; wraps for 0<n<4
+  const uint64_t nb = (uint64_t)std::ceil((double)n / (double)HC_BLOCK_SIZE);
+  return n - nb * HC_CRC_SIZE;
+}
+
+int hc_check_block(const uint8_t *p, size_t n) {
+  if (n < HC_CRC_SIZE) return HC_ERR_INVALID_BLOCK;  // crc_util.go:89-91
+  uint32_t stored;
+  std::memcpy(&stored, p, 4);
+  uint32_t c;
+  if (force_gpu() && n <= 0xFFFFFFFFu) {
+    uint64_t o = 0;
+    uint32_t l = (uint32_t)n;
+    int rc = host_batch(p, &o, &l, 0, 0, 1, &c, 0);
+    if (rc != HC_OK) return rc;
+  } else {
+    c = hc::cpu_crc32_update(0, p + HC_CRC_SIZE, n - HC_CRC_SIZE);
+  }
+  return stored == c ? HC_OK : HC_ERR_CRC_MISMATCH;
+}
+
+int hc_fix_last_block(uint8_t *p, size_t n) {
+  if (n < HC_BLOCK_SIZE) return HC_ERR_TOO_SHORT;  // crc_util.go:107-109
+  const size_t complete = n / HC_BLOCK_SIZE;
+  return hc_add_crc_block(p + (complete - 1) * HC_BLOCK_SIZE, HC_BLOCK_SIZE);
+}
+
+// ---- host-resident batches ---------------------------------------------------
+int hc_crc32_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                    uint32_t ulen, uint64_t nblocks, uint32_t *crc_out) {
+  if (nblocks == 0) return HC_OK;
+  if (!base || !crc_out) return HC_E_ARG;
+  return host_batch(base, off, len, stride, ulen, nblocks, crc_out, 0);
+}
+
+int hc_crc32_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n,
+                      uint32_t *crc_out) {
+  if (n == 0) return HC_OK;
+  if (!base || !off || !len || !crc_out) return HC_E_ARG;
+  return host_batch(base, off, len, 0, 0, n, crc_out, kFlagMessages);
+}
+
+int hc_verify_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                     uint32_t ulen, uint64_t nblocks, uint32_t *bad_bitmap, int64_t *first_bad) {
+  if (first_bad) *first_bad = -1;
+  if (bad_bitmap) std::memset(bad_bitmap, 0, ((nblocks + 31) / 32) * 4);
+  if (nblocks == 0) return HC_OK;
+  if (!base) return HC_E_ARG;
+  std::vector<uint32_t> crc(nblocks);
+  int rc = host_batch(base, off, len, stride, ulen, nblocks, crc.data(), 0);
+  if (rc != HC_OK) return rc;
+  int result = HC_OK;
+  for (uint64_t i = 0; i < nblocks; i++) {
+    const uint32_t l = blk_len(len, ulen, i);
+    int r = HC_OK;
+    if (l < HC_CRC_SIZE) {
+      r = HC_ERR_INVALID_BLOCK;
+    } else {
+      uint32_t stored;
+      std::memcpy(&stored, base + blk_off(off, stride, i), 4);
+      if (stored != crc[i]) r = HC_ERR_CRC_MISMATCH;
+    }
+    if (r != HC_OK) {
+      if (bad_bitmap) bad_bitmap[i >> 5] |= 1u << (i & 31);
+      if (result == HC_OK) {
+        result = r;
+        if (first_bad) *first_bad = (int64_t)i;
+      }
+    }
+  }
+  return result;
+}
+
+int hc_stamp_blocks(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                    uint32_t ulen, uint64_t nblocks) {
+  if (nblocks == 0) return HC_OK;
+  if (!base) return HC_E_ARG;
+  std::vector<uint32_t> crc(nblocks);
+  int rc = host_batch(base, off, len, stride, ulen, nblocks, crc.data(), 0);
+  if (rc != HC_OK) return rc;
+  for (uint64_t i = 0; i < nblocks; i++)
+    if (blk_len(len, ulen, i) >= HC_CRC_SIZE) std::memcpy(base + blk_off(off, stride, i), &crc[i], 4);
+  return HC_OK;
+}
+
+// ---- device-resident batches ---------------------------------------------------
+int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const uint32_t *len,
+                        uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out,
+                        uint32_t *bad_bitmap, int64_t *first_bad, uint32_t flags, void *stream) {
+  if (nblocks == 0) return HC_OK;
+  if (!base) return HC_E_ARG;
+  if (bad_bitmap && !first_bad) return HC_E_ARG;
+  if ((flags & HC_F_MESSAGES) && (first_bad || (flags & HC_F_STAMP))) return HC_E_ARG;
+  int st = init_device(device);
+  if (st != HC_OK) return st;
+  DeviceGuard g(device);
+  uint64_t bytes = (!off && !len) ? nblocks * (uint64_t)ulen : 0;
+  return dispatch(device, static_cast<const uint8_t *>(base), off, len, stride, ulen, nblocks, crc_out,
+                  bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes);
+}
+
+int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad, uint64_t nblocks,
+                          void *stream) {
+  int st = init_device(device);
+  if (st != HC_OK) return st;
+  DeviceGuard g(device);
+  return launch_verify_prepare(bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), nblocks,
+                               static_cast<hipStream_t>(stream)) == hipSuccess
+             ? HC_OK
+             : HC_E_HIP;
+}
+
+int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32_t *len,
+                       uint64_t stride, uint32_t ulen, uint64_t nblocks, uint64_t seed, void *stream) {
+  if (nblocks == 0) return HC_OK;
+  if (!base) return HC_E_ARG;
+  int st = init_device(device);
+  if (st != HC_OK) return st;
+  DeviceGuard g(device);
+  int grid = (int)std::min<uint64_t>((nblocks + 3) / 4, (uint64_t)g_dev[device].cus * 16);
+  return launch_fill(static_cast<uint8_t *>(base), off, len, stride, ulen, nblocks, seed, grid,
+                     static_cast<hipStream_t>(stream)) == hipSuccess
+             ? HC_OK
+             : HC_E_HIP;
+}
+
+int hc_last_launch(hc_launch_info *info) {
+  if (!info) return HC_E_ARG;
+  *info = t_last;
+  return HC_OK;
+}
+
+int hc_debug_tables(void *out, size_t cap) {
+  if (!out || cap < sizeof(DeviceTables)) return (int)sizeof(DeviceTables);
+  std::memcpy(out, &host_tables(), sizeof(DeviceTables));
+  return HC_OK;
+}
+
+}  // extern "C"

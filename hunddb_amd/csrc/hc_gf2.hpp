@@ -1,0 +1,94 @@
+// hc_gf2.hpp — GF(2) arithmetic for CRC-32/IEEE in the reflected domain and
+// the constant tables the gfx950 kernels read.
+//
+// Notation (used throughout DESIGN.md and the kernels):
+//   raw(m)        CRC register after feeding message m into a zero register
+//                 (no init, no xorout).  raw is GF(2)-linear in m and
+//                 raw(a || b) = shift(raw(a), |b|) ^ raw(b).
+//   shift(c, n)   register c after feeding n zero bytes = c * x^(8n) mod P.
+//   ChecksumIEEE(m) = raw(W0 || m) ^ 0xFFFFFFFF with shift(W0, 4) = 0xFFFFFFFF,
+//                 i.e. Go's init ^0 is a 4-byte virtual prefix W0 (any |m|).
+// The reference arithmetic is Go's crc32.ChecksumIEEE as called by
+// /root/reference/utils/crc/crc_util.go:16,94.
+#pragma once
+#include <cstdint>
+
+namespace hc {
+
+constexpr uint32_t kPolyReflected = 0xEDB88320u;
+constexpr uint32_t kRowBytes = 1024;  // one wave-instruction of 16 B/lane
+constexpr uint32_t kLanes = 64;
+
+// Byte-at-a-time Sarwate table (host side only).
+struct Gf2 {
+  uint32_t t[256];
+  Gf2() {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int b = 0; b < 8; b++) c = (c >> 1) ^ (kPolyReflected & (0u - (c & 1u)));
+      t[i] = c;
+    }
+  }
+  uint32_t shift_bytes(uint32_t c, uint64_t n) const {
+    for (uint64_t i = 0; i < n; i++) c = (c >> 8) ^ t[c & 0xFF];
+    return c;
+  }
+  // Inverse of shift(., 4) by Gaussian elimination over GF(2).
+  uint32_t unshift4(uint32_t target) const {
+    uint32_t col[32];
+    for (int i = 0; i < 32; i++) col[i] = shift_bytes(1u << i, 4);
+    // Solve sum_i x_i col[i] = target.  Rows = output bits.
+    uint64_t rows[32];  // bits 0..31: coefficient of x_i; bit 32: rhs
+    for (int r = 0; r < 32; r++) {
+      uint64_t v = 0;
+      for (int i = 0; i < 32; i++) v |= (uint64_t)((col[i] >> r) & 1u) << i;
+      v |= (uint64_t)((target >> r) & 1u) << 32;
+      rows[r] = v;
+    }
+    int rank = 0;
+    int pivcol[32];
+    for (int c = 0; c < 32 && rank < 32; c++) {
+      int p = -1;
+      for (int r = rank; r < 32; r++)
+        if ((rows[r] >> c) & 1) { p = r; break; }
+      if (p < 0) continue;
+      uint64_t tmp = rows[p]; rows[p] = rows[rank]; rows[rank] = tmp;
+      for (int r = 0; r < 32; r++)
+        if (r != rank && ((rows[r] >> c) & 1)) rows[r] ^= rows[rank];
+      pivcol[rank++] = c;
+    }
+    uint32_t x = 0;
+    for (int r = 0; r < rank; r++)
+      if ((rows[r] >> 32) & 1) x |= 1u << pivcol[r];
+    return x;
+  }
+};
+
+// Device constant image (one per device, 12 KiB), uploaded once.
+//   tg[k][b]   = shift(b << 8k, kRowBytes)        Horner step across a row
+//   s4[k][b]   = shift(b << 8k, 4)                lane stream combine
+//   lane[l][i] = shift(1 << i, kRowBytes - 12 - 16 l)   lane placement
+//   w0         = shift^-1(0xFFFFFFFF, 4)           Go's init as a prefix word
+struct DeviceTables {
+  uint32_t tg[4][256];
+  uint32_t s4[4][256];
+  uint32_t lane[kLanes][32];
+  uint32_t w0;
+  uint32_t pad[63];
+};
+static_assert(sizeof(DeviceTables) % 256 == 0, "keep the image 256-B multiple");
+
+inline void build_device_tables(DeviceTables &d) {
+  Gf2 g;
+  for (int k = 0; k < 4; k++)
+    for (uint32_t b = 0; b < 256; b++) {
+      d.tg[k][b] = g.shift_bytes(b << (8 * k), kRowBytes);
+      d.s4[k][b] = g.shift_bytes(b << (8 * k), 4);
+    }
+  for (uint32_t l = 0; l < kLanes; l++)
+    for (int i = 0; i < 32; i++) d.lane[l][i] = g.shift_bytes(1u << i, kRowBytes - 12 - 16 * l);
+  d.w0 = g.unshift4(0xFFFFFFFFu);
+  for (auto &p : d.pad) p = 0;
+}
+
+}  // namespace hc

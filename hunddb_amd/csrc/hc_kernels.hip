@@ -1,0 +1,447 @@
+// hc_kernels.hip — hand-written gfx950 (CDNA4) kernels of the batched
+// block-checksum engine.  CRC-32/IEEE exactly as Go's crc32.ChecksumIEEE,
+// applied per block the way /root/reference/utils/crc/crc_util.go:21-33 (stamp)
+// and :88-100 (verify) apply it.
+//
+// Streaming kernel (k_crc_fast), per wave = one block at a time:
+//   * A block of B bytes is B/1024 rows; row j is read by ONE coalesced
+//     global_load_dwordx4 (lane l gets bytes 1024j+16l .. +15).  No LDS
+//     staging: every byte goes HBM -> VGPR once.
+//   * Lane l keeps four Horner streams c_k (word k of its 16 B):
+//       c_k <- shift(c_k, 1024) ^ w_k
+//     shift(., 1024) is four byte-table lookups (tg) in LDS.  Each table is
+//     replicated 32x so lane l reads bank l%32: conflict-free ds_read_b32.
+//     The LDS byte address of a lookup is built by ONE v_perm_b32.
+//   * Block end: d = shift4^3(c0)^shift4^2(c1)^shift4(c2)^c3 (s4 tables), the
+//     lane's placement e = d*x^(8(1012-16l)) mod P as a 32x32 GF(2) mat-vec
+//     against 32 lane-constant VGPRs (v_bfe_i32 + v_bitop3), then a DPP/readlane
+//     XOR reduction across the 64 lanes.  CRC = xor ^ 0xFFFFFFFF.
+//   * Go's init value is the virtual prefix word W0 with shift(W0,4)=~0: in
+//     block mode it replaces the stored CRC word (bytes 0..3), which the CRC
+//     must not cover anyway.
+// General kernel (k_crc_general): any alignment and length (incl. < 4 bytes),
+// same row decomposition with the message right-aligned to rows by virtual
+// leading zeros; unaligned bytes are assembled from in-range dword loads.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "hc_kernels.hpp"
+
+namespace hc {
+
+namespace {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Scalar (s_load) reads of wave-uniform metadata.  hipcc keeps these as
+// vector loads (it cannot prove the arrays are unclobbered), and the
+// s_waitcnt vmcnt(0) such a load needs would drain the row-load ring.
+__device__ __forceinline__ uint64_t sload_u64(const uint64_t *p) {
+  uint64_t v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t sload_u32(const uint32_t *p) {
+  uint32_t v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void block_meta(const Batch &b, uint64_t i, uint64_t &o, uint32_t &l) {
+  o = b.off ? b.off[i] : i * b.stride;
+  l = b.len ? b.len[i] : b.ulen;
+}
+
+__device__ __forceinline__ bool fast_ok(const Batch &b, uint64_t o, uint32_t l) {
+  return (((uintptr_t)b.base + o) & 15u) == 0 && (l & 1023u) == 0 && l != 0;
+}
+
+// 32x32 GF(2) mat-vec: XOR of col[i] over the set bits i of d.
+__device__ __forceinline__ uint32_t matvec32(const uint32_t (&col)[32], uint32_t d) {
+  uint32_t e = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint32_t m = (uint32_t)((int32_t)(d << (31 - i)) >> 31);  // v_bfe_i32 d, i, 1
+    e = __builtin_amdgcn_bitop3_b32(m, col[i], e, 0x6A);      // (m & col) ^ e
+  }
+  return e;
+}
+
+// XOR of v over the 64 lanes (wave-uniform result).
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1032
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm 2301
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return __builtin_amdgcn_readlane(v, 0) ^ __builtin_amdgcn_readlane(v, 16) ^
+         __builtin_amdgcn_readlane(v, 32) ^ __builtin_amdgcn_readlane(v, 48);
+}
+
+// ---------------------------------------------------------------------------
+// Streaming kernel.  Pointer arguments are separate __restrict__ kernel
+// arguments so the per-block metadata reads (off/len) become scalar s_loads
+// (lgkmcnt) instead of vector loads that would drain the row ring (vmcnt(0)).
+template <bool kUniform>
+__global__ __launch_bounds__(kFastThreads) void k_crc_fast(
+    const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+    uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks,
+    uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
+    unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+
+  // Fill the replicated tables.  Main region address of (table k, byte v,
+  // replica r) = (k>>1)<<16 | v<<8 | (k&1)<<7 | r<<2; s4 region address
+  // = kLdsMainBytes + k*4096 + v*16 + (r&3)*4.
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
+  }
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+
+  const uint32_t r4 = (lane & 31u) << 2;
+  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
+  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  const bool msg = (flags & kFlagMessages) != 0;
+
+  // c <- shift(c, 1024) ^ w : four conflict-free lookups, one v_perm each.
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
+    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
+    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
+    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
+    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
+    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
+    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+
+  const uint32_t wave = uni(tid >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
+  const uint64_t b0 = uni64(nblocks * gw / W), b1 = uni64(nblocks * (gw + 1) / W);
+
+  // Advance a cursor to the first block >= from that this kernel handles.
+  auto seek = [&](uint64_t from, uint64_t &blk, const uint8_t *&ptr, uint32_t &rows) -> bool {
+    if (kUniform) {
+      if (from >= b1) return false;
+      blk = from;
+      ptr = base + from * stride;
+      rows = ulen >> 10;
+      return true;
+    }
+    for (uint64_t i = from; i < b1; i++) {
+      const uint64_t o = offs ? sload_u64(offs + i) : i * stride;
+      const uint32_t l = lens ? sload_u32(lens + i) : ulen;
+      if ((((uintptr_t)base + o) & 15u) == 0 && (l & 1023u) == 0 && l != 0) {
+        blk = i;
+        ptr = base + o;
+        rows = l >> 10;
+        return true;
+      }
+    }
+    return false;
+  };
+
+  uint64_t pb = 0, cb = 0;
+  const uint8_t *pptr = nullptr, *cptr = nullptr;
+  uint32_t prow = 0, prows = 0, crow = 0, crows = 0;
+  if (!seek(b0, cb, cptr, crows)) return;
+  pb = cb;
+  pptr = cptr;
+  prows = crows;
+
+  // Producer: issue the load of the next row, then advance (clamped at the
+  // wave's last row so every issued load is in bounds).
+  auto load_next = [&]() -> uint4 {
+    const uint4 v = *reinterpret_cast<const uint4 *>(pptr + (size_t)prow * kRowBytes + lane * 16u);
+    if (++prow == prows) {
+      uint64_t nb;
+      const uint8_t *np;
+      uint32_t nr;
+      if (seek(pb + 1, nb, np, nr)) {
+        pb = nb;
+        pptr = np;
+        prows = nr;
+        prow = 0;
+      } else {
+        prow = prows - 1;
+      }
+    }
+    return v;
+  };
+
+  constexpr int kRing = 8;
+  uint4 ring[kRing];
+#pragma unroll
+  for (int u = 0; u < kRing; u++) ring[u] = load_next();
+
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
+  for (;;) {
+#pragma unroll
+    for (int u = 0; u < kRing; u++) {
+      // consume slot u, then refill it (same registers: no copies, kRing-1
+      // rows stay in flight while this one is hashed)
+      uint4 v = ring[u];
+      if (crow == 0) {
+        if (lane == 0) {
+          stored = v.x;
+          v.x = msg ? (v.x ^ 0xFFFFFFFFu) : w0;
+        }
+        c0 = v.x;
+        c1 = v.y;
+        c2 = v.z;
+        c3 = v.w;
+      } else {
+        c0 = row_step(c0, v.x);
+        c1 = row_step(c1, v.y);
+        c2 = row_step(c2, v.z);
+        c3 = row_step(c3, v.w);
+      }
+      ring[u] = load_next();
+      if (++crow == crows) {
+        const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
+        const uint32_t crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        if (lane == 0) {
+          if (crc_out) crc_out[cb] = crc;
+          if (flags & kFlagStamp) *const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(cptr)) = crc;
+          if (first_bad && stored != crc) {
+            if (bad_bitmap)
+              __hip_atomic_fetch_or(&bad_bitmap[cb >> 5], 1u << (cb & 31), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_min(first_bad, (unsigned long long)cb, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        if (!seek(cb + 1, cb, cptr, crows)) return;
+        crow = 0;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// General kernel: one wave per block, any alignment/length.
+__device__ __forceinline__ uint32_t load_dw_if(const uint8_t *p, bool ok) {
+  return ok ? *reinterpret_cast<const uint32_t *>(p) : 0u;
+}
+
+__global__ __launch_bounds__(kGenThreads) void k_crc_general(Batch bt, int only_nonfast) {
+  __shared__ uint32_t tgl[1024];
+  __shared__ uint32_t s4l[1024];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  for (uint32_t i = tid; i < 1024; i += kGenThreads) {
+    tgl[i] = (&bt.tables->tg[0][0])[i];
+    s4l[i] = (&bt.tables->s4[0][0])[i];
+  }
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = bt.tables->lane[lane][i];
+  const uint32_t w0 = bt.tables->w0;
+  __syncthreads();
+
+  auto tshift = [&](const uint32_t *t, uint32_t c) -> uint32_t {
+    return t[c & 255u] ^ t[256 + ((c >> 8) & 255u)] ^ t[512 + ((c >> 16) & 255u)] ^
+           t[768 + (c >> 24)];
+  };
+  const bool msg = (bt.flags & kFlagMessages) != 0;
+  const uint64_t W = (uint64_t)gridDim.x * kGenWaves;
+  for (uint64_t blk = (uint64_t)blockIdx.x * kGenWaves + uni(tid >> 6); blk < bt.nblocks;
+       blk += W) {
+    uint64_t o;
+    uint32_t l;
+    block_meta(bt, blk, o, l);
+    if (only_nonfast && fast_ok(bt, o, l)) continue;
+    const uint8_t *blkp = bt.base + o;
+    if (!msg && l < 4) {  // "invalid block data": no CRC, always bad
+      if (lane == 0) {
+        if (bt.crc_out) bt.crc_out[blk] = 0;
+        if (bt.first_bad) {
+          if (bt.bad_bitmap) atomicOr(&bt.bad_bitmap[blk >> 5], 1u << (blk & 31));
+          atomicMin(bt.first_bad, (unsigned long long)blk);
+        }
+      }
+      continue;
+    }
+    const uint8_t *P = msg ? blkp : blkp + 4;  // payload
+    const int64_t Lp = msg ? (int64_t)l : (int64_t)l - 4;
+    const int64_t Lv = Lp + 4;  // W0 || payload
+    const uint32_t rows = (uint32_t)((Lv + kRowBytes - 1) / kRowBytes);
+    const int64_t z = (int64_t)rows * kRowBytes - Lv;
+    uint32_t c[4] = {0, 0, 0, 0};
+    for (uint32_t r = 0; r < rows; r++) {
+      // payload-relative offset of this lane's first byte
+      const int64_t s = (int64_t)r * kRowBytes + 16 * (int64_t)lane - z - 4;
+      const uintptr_t A = (uintptr_t)P + (uintptr_t)s;  // wraps harmlessly if s < 0
+      const uintptr_t Ab = A & ~(uintptr_t)3;
+      const uint32_t sh = (uint32_t)(A & 3u);
+      const uintptr_t lo = (uintptr_t)P, hi = (uintptr_t)P + (uintptr_t)Lp;
+      uint32_t d[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uintptr_t a = Ab + 4 * j;
+        // load only dwords overlapping [P, P+Lp); with s < 0 the wrap makes
+        // Ab huge or below lo, so test in signed payload-relative space.
+        const int64_t rel = s - (int64_t)sh + 4 * j;  // payload offset of dword start
+        const bool ok = rel + 4 > 0 && rel < Lp;
+        d[j] = load_dw_if(reinterpret_cast<const uint8_t *>(a), ok);
+        (void)lo;
+        (void)hi;
+      }
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+      if (s < 0) {  // front of the virtual message: zeros, then W0, then data
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint32_t dm = 0, wv = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int64_t ob = s + 4 * k + j;
+            if (ob >= 0) dm |= 0xFFu << (8 * j);
+            else if (ob >= -4) wv |= ((w0 >> (8 * (ob + 4))) & 0xFFu) << (8 * j);
+          }
+          w[k] = (w[k] & dm) | wv;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) c[k] = (r == 0 ? 0u : tshift(tgl, c[k])) ^ w[k];
+    }
+    const uint32_t dd = tshift(s4l, tshift(s4l, tshift(s4l, c[0]) ^ c[1]) ^ c[2]) ^ c[3];
+    const uint32_t crc = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    const uint32_t stored = (!msg && lane == 0) ? *reinterpret_cast<const uint32_t *>(blkp) : 0u;
+    // the stored word of an unaligned block is read bytewise
+    uint32_t st = stored;
+    if (!msg && lane == 0 && (((uintptr_t)blkp) & 3u)) {
+      st = (uint32_t)blkp[0] | ((uint32_t)blkp[1] << 8) | ((uint32_t)blkp[2] << 16) |
+           ((uint32_t)blkp[3] << 24);
+    }
+    if (lane == 0) {
+      if (bt.crc_out) bt.crc_out[blk] = crc;
+      if (bt.flags & kFlagStamp) {
+        uint8_t *wp = const_cast<uint8_t *>(blkp);
+        wp[0] = (uint8_t)crc;
+        wp[1] = (uint8_t)(crc >> 8);
+        wp[2] = (uint8_t)(crc >> 16);
+        wp[3] = (uint8_t)(crc >> 24);
+      }
+      if (bt.first_bad && !msg && st != crc) {
+        if (bt.bad_bitmap) atomicOr(&bt.bad_bitmap[blk >> 5], 1u << (blk & 31));
+        atomicMin(bt.first_bad, (unsigned long long)blk);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic workload fill: 64-bit word w of block i = splitmix64(seed, i, w).
+__device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t blk, uint64_t w) {
+  uint64_t z = seed + ((blk << 21) + w) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill(uint8_t *base, const uint64_t *off, const uint32_t *len,
+                                               uint64_t stride, uint32_t ulen, uint64_t n,
+                                               uint64_t seed) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t W = (uint64_t)gridDim.x * 4;
+  for (uint64_t blk = (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6); blk < n; blk += W) {
+    const uint64_t o = off ? off[blk] : blk * stride;
+    const uint32_t l = len ? len[blk] : ulen;
+    uint8_t *p = base + o;
+    if ((((uintptr_t)p) & 15u) == 0) {
+      for (uint32_t w = 2 * lane; 8 * w + 16 <= l; w += 128) {
+        ulonglong2 v;
+        v.x = splitmix(seed, blk, w);
+        v.y = splitmix(seed, blk, w + 1);
+        *reinterpret_cast<ulonglong2 *>(p + 8 * w) = v;
+      }
+      // tail (l % 16 != 0)
+      const uint32_t done = l & ~15u;
+      for (uint32_t b = done + lane; b < l; b += 64)
+        p[b] = (uint8_t)(splitmix(seed, blk, b >> 3) >> (8 * (b & 7)));
+    } else {
+      for (uint32_t b = lane; b < l; b += 64)
+        p[b] = (uint8_t)(splitmix(seed, blk, b >> 3) >> (8 * (b & 7)));
+    }
+  }
+}
+
+__global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t words) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (bitmap)
+    for (uint64_t k = i; k < words; k += (uint64_t)gridDim.x * blockDim.x) bitmap[k] = 0;
+  if (i == 0 && first_bad) *first_bad = (unsigned long long)LLONG_MAX;
+}
+
+}  // namespace
+
+hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s) {
+  if (uniform_fast)
+    hipLaunchKernelGGL(k_crc_fast<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len,
+                       b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables);
+  else
+    hipLaunchKernelGGL(k_crc_fast<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len,
+                       b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables);
+  return hipGetLastError();
+}
+
+hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_crc_general, dim3(grid), dim3(kGenThreads), 0, s, b, only_nonfast ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                       uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, s, base, off, len, stride, ulen, n, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
+                                 hipStream_t s) {
+  const uint64_t words = (n + 31) / 32;
+  int grid = (int)((words + 255) / 256);
+  if (grid < 1) grid = 1;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_verify_prepare, dim3(grid), dim3(256), 0, s, bitmap, first_bad, words);
+  return hipGetLastError();
+}
+
+}  // namespace hc

@@ -1,0 +1,53 @@
+// hc_kernels.hpp — launch interface between the host runtime (hc_api.cpp) and
+// the gfx950 kernels (hc_kernels.hip).  No torch types, plain pointers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hc_gf2.hpp"
+
+namespace hc {
+
+enum : uint32_t { kFlagStamp = 1u, kFlagMessages = 2u };
+
+// One batch of blocks (or messages) as the kernels see it.  Block i occupies
+// base[off(i) .. off(i)+len(i)) with off(i) = off ? off[i] : i*stride and
+// len(i) = len ? len[i] : ulen.
+struct Batch {
+  const uint8_t *base;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint64_t stride;
+  uint32_t ulen;
+  uint32_t flags;
+  uint64_t nblocks;
+  uint32_t *crc_out;              // optional
+  uint32_t *bad_bitmap;           // optional (verify)
+  unsigned long long *first_bad;  // optional (verify), INT64_MAX when clean
+  const DeviceTables *tables;
+};
+
+// Streaming kernel geometry (one workgroup per CU; see DESIGN.md "Kernel").
+constexpr int kFastWaves = 16;
+constexpr int kFastThreads = kFastWaves * 64;
+constexpr uint32_t kLdsMainBytes = 131072;  // 4 row-shift tables x 256 x 32 replicas x 4 B
+constexpr uint32_t kLdsS4Bytes = 16384;     // 4 x 256 x 4 replicas x 4 B
+constexpr uint32_t kFastLdsBytes = kLdsMainBytes + kLdsS4Bytes;
+
+// General kernel (any alignment / length), 4 waves per workgroup.
+constexpr int kGenWaves = 4;
+constexpr int kGenThreads = kGenWaves * 64;
+
+// Host launchers; return the hipError_t of the launch.
+// uniform_fast: the host proved every block satisfies the streaming kernel's
+// layout contract (16-B aligned start, length a positive multiple of 1024).
+hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s);
+// only_nonfast: process only blocks the streaming kernel skips.
+hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s);
+hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                       uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s);
+hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
+                                 hipStream_t s);
+
+}  // namespace hc

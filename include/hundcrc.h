@@ -1,0 +1,153 @@
+/*
+ * hundcrc.h — C ABI of libhundcrc.so, the MI355X-native batched block-checksum
+ * engine that replaces HundDB's utils/crc package.
+ *
+ * Reference interface replaced (file:line relative to mrsladoje/HundDB):
+ *   utils/crc/crc_util.go:11-12  BLOCK_SIZE / CRC_SIZE          -> HC_BLOCK_SIZE / HC_CRC_SIZE
+ *   utils/crc/crc_util.go:15-17  GetCRC                          -> hc_crc32_ieee
+ *   utils/crc/crc_util.go:21-33  AddCRCToBlockData               -> hc_add_crc_block
+ *   utils/crc/crc_util.go:41-64  AddCRCsToData                   -> hc_add_crcs (+ hc_add_crcs_size)
+ *   utils/crc/crc_util.go:69-74  SizeAfterAddingCRCs             -> hc_size_after_crcs
+ *   utils/crc/crc_util.go:79-83  SizeWithoutCRCs                 -> hc_size_without_crcs
+ *   utils/crc/crc_util.go:88-100 CheckBlockIntegrity             -> hc_check_block
+ *   utils/crc/crc_util.go:106-122 FixLastBlockCRC                -> hc_fix_last_block
+ * New batched entries (the GPU hot path) for the per-block loops of
+ *   lsm/block_manager/block_manager.go:203-235 (ReadFromDisk verify loop),
+ *   lsm/wal/wal.go:260-271,362-406 (flushBlock / recoverMemtable),
+ *   lsm/sstable/sstable.go:660-887 (serialize -> AddCRCsToData).
+ *
+ * Conventions
+ *   - A "block" is a byte range [off, off+len) whose first 4 bytes hold the
+ *     little-endian CRC-32/IEEE (Go crc32.ChecksumIEEE) of bytes [4, len).
+ *   - All pointers are borrowed for the duration of the call only (the cgo
+ *     pointer rule); the library never retains or frees caller memory.
+ *   - Host entries (no _dev_) take host pointers, copy through library-owned
+ *     pinned staging and are synchronous.  _dev_ entries take device pointers
+ *     and a hipStream_t (passed as void*; NULL = the library's per-thread
+ *     stream) and are asynchronous on that stream.
+ *   - Every function is re-entrant and thread-safe (no global mutable state on
+ *     the call path besides lazily-initialised per-device constant tables).
+ *   - Return codes: >= 0 success / Go-level result; < 0 library error.
+ *     No C++ exception ever crosses this ABI.
+ */
+#ifndef HUNDCRC_H
+#define HUNDCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HC_BLOCK_SIZE 4096u /* crc_util.go:11 (typed uint64 in Go) */
+#define HC_CRC_SIZE 4u      /* crc_util.go:12 (untyped constant in Go) */
+
+/* Go-level results (mapped by hc_strerror to the exact errors.New texts) */
+#define HC_OK 0
+#define HC_ERR_INVALID_BLOCK 1 /* "invalid block data"                            crc_util.go:90  */
+#define HC_ERR_CRC_MISMATCH 2  /* "CRC mismatch in block"                         crc_util.go:96  */
+#define HC_ERR_TOO_SHORT 3     /* "data is too short to contain a complete block" crc_util.go:108 */
+/* library errors */
+#define HC_E_ARG -1     /* invalid argument (null pointer, bad size, capacity too small) */
+#define HC_E_HIP -2     /* a HIP runtime call failed */
+#define HC_E_NODEV -3   /* no usable gfx950 device: the GPU path fails loudly, never falls back */
+#define HC_E_NOMEM -4   /* device or pinned allocation failed */
+#define HC_E_LAYOUT -5  /* device batch violated the layout contract (see hc_dev_*) */
+
+/* Exact Go error text for a Go-level result, or a description of a library error. */
+const char *hc_strerror(int code);
+/* Library version string and the offload arch the kernels were built for. */
+const char *hc_version(void);
+
+/* ---------------- drop-ins for utils/crc (crc_util.go) ---------------- */
+/* GetCRC (crc_util.go:15-17): crc32.ChecksumIEEE(p[0:n]); n==0 -> 0. */
+uint32_t hc_crc32_ieee(const uint8_t *p, size_t n);
+/* AddCRCToBlockData (crc_util.go:21-33): n < 4 -> untouched; else
+ * p[0:4] = LE32(ChecksumIEEE(p[4:n])).  In place; returns HC_OK. */
+int hc_add_crc_block(uint8_t *p, size_t n);
+/* Output length of AddCRCsToData for an n-byte input: ceil(n/4092)*4096. */
+size_t hc_add_crcs_size(size_t n);
+/* AddCRCsToData (crc_util.go:41-64): chunk src into 4092-byte payloads, each
+ * in a zeroed 4096-byte block with its CRC in bytes [0:4).  dst is caller
+ * memory of >= hc_add_crcs_size(n) bytes (Go: make([]byte, ...)).  Returns the
+ * number of bytes written, or (size_t)-1 if dst_cap is too small. */
+size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap);
+/* SizeAfterAddingCRCs (crc_util.go:69-74), float64-ceil semantics. */
+uint64_t hc_size_after_crcs(uint64_t n);
+/* SizeWithoutCRCs (crc_util.go:79-83), float64-ceil, uint64 wrap for 0<n<4. */
+uint64_t hc_size_without_crcs(uint64_t n);
+/* CheckBlockIntegrity (crc_util.go:88-100): HC_OK, HC_ERR_INVALID_BLOCK (n<4)
+ * or HC_ERR_CRC_MISMATCH. */
+int hc_check_block(const uint8_t *p, size_t n);
+/* FixLastBlockCRC (crc_util.go:106-122): n < 4096 -> HC_ERR_TOO_SHORT; else
+ * restamps the last complete 4096-byte block.  In place. */
+int hc_fix_last_block(uint8_t *p, size_t n);
+
+/* ---------------- batched, host-resident (GPU) ---------------- */
+/* Block i is base[off[i] .. off[i]+len[i]).  off==NULL -> off[i] = i*stride;
+ * len==NULL -> len[i] = ulen.  Blocks shorter than 4 bytes get crc 0 and, for
+ * verify, count as bad ("invalid block data").  Any lengths/alignments are
+ * accepted; 16-byte-aligned blocks whose length is a multiple of 1024 take the
+ * streaming kernel, all others the general kernel. */
+int hc_crc32_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                    uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out);
+/* Batched CheckBlockIntegrity.  bad_bitmap (optional, ceil(n/32) uint32 words,
+ * bit i%32 of word i/32) marks failing blocks; *first_bad = lowest failing
+ * index or -1.  Returns HC_OK if every block passes, HC_ERR_CRC_MISMATCH or
+ * HC_ERR_INVALID_BLOCK for the first failing block's reason, < 0 on error. */
+int hc_verify_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                     uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *bad_bitmap,
+                     int64_t *first_bad);
+/* Batched AddCRCToBlockData: stamps every block in place. */
+int hc_stamp_blocks(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                    uint32_t ulen, uint64_t nblocks);
+/* GetCRC over variable-length messages base[off[i] .. off[i]+len[i]) (whole
+ * message, no 4-byte header skipped), e.g. per-record CRCs. */
+int hc_crc32_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                      uint64_t nmsgs, uint32_t *crc_out);
+
+/* ---------------- batched, device-resident (GPU) ---------------- */
+/* As above with device pointers (base, off, len, outputs) on `device`,
+ * asynchronous on `stream` (hipStream_t).  crc_out, bad_bitmap and first_bad
+ * are each optional (NULL); bad_bitmap must be zeroed and *first_bad set to
+ * INT64_MAX by the caller (hc_dev_verify_prepare does both).  `flags`: see
+ * HC_F_*.  Returns HC_OK once the work is enqueued. */
+#define HC_F_STAMP 1u /* also write each block's CRC into its bytes [0:4) */
+#define HC_F_MESSAGES 2u /* whole-message CRC (no 4-byte header skipped) */
+int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const uint32_t *len,
+                        uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out,
+                        uint32_t *bad_bitmap, int64_t *first_bad, uint32_t flags,
+                        void *stream);
+/* Zero a device bitmap of ceil(n/32) words and set *first_bad = INT64_MAX. */
+int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad,
+                          uint64_t nblocks, void *stream);
+/* Fill a device buffer with the seeded synthetic workload: block i occupies
+ * [off[i], off[i]+len[i]) (or i*stride / ulen), 64-bit word w of block i =
+ * splitmix64(seed, i, w) (see oracle/hc_oracle.c oc_splitmix64). */
+int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32_t *len,
+                       uint64_t stride, uint32_t ulen, uint64_t nblocks, uint64_t seed,
+                       void *stream);
+
+/* Per-launch accounting of the last device call on this thread (for the
+ * roofline): kernel name, number of blocks routed to the streaming kernel and
+ * to the general kernel, and algorithmic bytes (sum of block lengths). */
+typedef struct {
+  const char *kernel;
+  uint64_t fast_blocks, general_blocks, bytes;
+  uint32_t grid, block_threads, lds_bytes;
+} hc_launch_info;
+int hc_last_launch(hc_launch_info *info);
+
+/* Copy the host-built constant image the kernels use (DESIGN.md "Tables")
+ * into out (returns HC_OK) or, if cap is too small, return its size. */
+int hc_debug_tables(void *out, size_t cap);
+
+/* Number of visible gfx950 devices (0 if none; never initialises a context
+ * on a machine without GPUs). */
+int hc_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HUNDCRC_H */

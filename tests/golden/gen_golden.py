@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures that pin the CPU oracle (oracle/hc_oracle.c).
+
+Run in the build container:  python3 tests/golden/gen_golden.py
+Writes tests/golden/golden.json.
+
+Source of truth: Python's zlib.crc32 (zlib 1.2.11), which computes the same
+CRC-32/ISO-HDLC function as Go's crc32.ChecksumIEEE used by
+/root/reference/utils/crc/crc_util.go:16,94.  The reference (Go) cannot be
+built or run here (no Go toolchain) and ships no CRC golden
+vectors of its own, so the expected outputs of every utils/crc function below
+are derived from zlib plus a line-by-line Python restatement of
+crc_util.go:10-122 and, for the structural fixtures, of the WAL framing in
+lsm/wal/wal.go:177-283 / wal_header.go:5-77 / model/record/record.go:85-119.
+This file reads nothing under /root/reference at run time.
+"""
+import hashlib
+import json
+import math
+import os
+import struct
+import zlib
+
+import numpy as np
+
+BLOCK_SIZE = 4096  # crc_util.go:11
+CRC_SIZE = 4       # crc_util.go:12
+M64 = (1 << 64) - 1
+
+
+# ---- utils/crc restated (Go semantics) -----------------------------------
+def get_crc(b):                      # crc_util.go:15-17
+    return zlib.crc32(bytes(b)) & 0xFFFFFFFF
+
+
+def add_crc_to_block_data(b):        # crc_util.go:21-33 (in place)
+    b = bytearray(b)
+    if len(b) < CRC_SIZE:
+        return b
+    b[0:4] = struct.pack("<I", get_crc(b[4:]))
+    return b
+
+
+def add_crcs_to_data(src):           # crc_util.go:41-64
+    per = BLOCK_SIZE - CRC_SIZE
+    out = bytearray()
+    for i in range(0, len(src), per):
+        blk = bytearray(BLOCK_SIZE)
+        chunk = src[i:i + per]
+        blk[4:4 + len(chunk)] = chunk
+        out += add_crc_to_block_data(blk)
+    return out
+
+
+def size_after_adding_crcs(n):       # crc_util.go:69-74, float64 math
+    nb = int(math.ceil(float(n) / float(BLOCK_SIZE - CRC_SIZE)))
+    return (n + nb * CRC_SIZE) & M64
+
+
+def size_without_crcs(n):            # crc_util.go:79-83, uint64 wrap
+    nb = int(math.ceil(float(n) / float(BLOCK_SIZE)))
+    return (n - nb * CRC_SIZE) & M64
+
+
+def check_block_integrity(b):        # crc_util.go:88-100
+    if len(b) < CRC_SIZE:
+        return "invalid block data"
+    if struct.unpack("<I", bytes(b[0:4]))[0] != get_crc(b[4:]):
+        return "CRC mismatch in block"
+    return None
+
+
+def fix_last_block_crc(b):           # crc_util.go:106-122
+    b = bytearray(b)
+    if len(b) < BLOCK_SIZE:
+        return "data is too short to contain a complete block", b
+    last = (len(b) // BLOCK_SIZE - 1) * BLOCK_SIZE
+    b[last:last + BLOCK_SIZE] = add_crc_to_block_data(b[last:last + BLOCK_SIZE])
+    return None, b
+
+
+# ---- synthetic inputs: splitmix64 finaliser over (seed, block, word) -----
+def splitmix64(seed, block, words):
+    w = np.asarray(words, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + ((np.uint64(block) << np.uint64(21)) + w) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def fill_block(seed, block, length):
+    return splitmix64(seed, block, np.arange(length // 8)).astype("<u8").tobytes()
+
+
+def mixed_size(seed, block):
+    r = int(splitmix64(seed ^ 0x5A5A5A5A5A5A5A5A, block, [(1 << 21) - 1])[0])
+    return 4096 << (r % 3)
+
+
+# ---- WAL framing restated (lsm/wal/wal.go:177-283) -----------------------
+WAL_HDR = 17  # wal_header.go:16
+
+
+def wal_payload_byte(seed, rec, total_len, pos):
+    if pos < 8:
+        return (rec >> (8 * pos)) & 0xFF                       # timestamp
+    if pos == 8:
+        return 0                                               # tombstone
+    ksz = min(16, total_len - 25)                              # records are >= 25 bytes
+    if pos < 17:
+        return (ksz >> (8 * (pos - 9))) & 0xFF                 # key size
+    if pos < 25:
+        return ((total_len - 25 - ksz) >> (8 * (pos - 17))) & 0xFF  # value size
+    w = int(splitmix64(seed, rec, [(pos - 25) >> 3])[0])
+    return (w >> (8 * ((pos - 25) & 7))) & 0xFF
+
+
+def wal_frame(seed, sizes, bs=4096, log_size=16):
+    blocks = []
+    st = {"cur": bytearray(bs), "off": CRC_SIZE, "in_log": 0, "log": 1}
+    refused = 0
+
+    def flush():                                   # wal.go:260-271
+        blocks.append(bytes(add_crc_to_block_data(st["cur"])))
+        st["in_log"] += 1
+
+    def new_block():                               # wal.go:273-283
+        st["cur"] = bytearray(bs)
+        st["off"] = CRC_SIZE
+        if st["in_log"] >= log_size:
+            st["log"] += 1
+            st["in_log"] = 0
+
+    def write_to_block(rec, pay_off, n, total, typ):   # wal.go:229-257
+        if st["off"] + WAL_HDR + n > bs:
+            return False
+        o = st["off"]
+        st["cur"][o:o + WAL_HDR] = struct.pack("<QBQ", n, typ, st["log"])
+        st["cur"][o + WAL_HDR:o + WAL_HDR + n] = bytes(
+            wal_payload_byte(seed, rec, total, pay_off + k) for k in range(n))
+        st["off"] += WAL_HDR + n
+        if st["off"] == bs:
+            flush()
+            new_block()
+        return True
+
+    for rec, S in enumerate(sizes):                # wal.go:177-195
+        need = WAL_HDR + S
+        if bs - st["off"] < need:
+            flush()
+            new_block()
+            if need > bs:                          # wal.go:199-225
+                maxp = bs - WAL_HDR - CRC_SIZE
+                nf = int(math.ceil(S / maxp))
+                po = 0
+                for i in range(nf):
+                    fl = min(maxp, S - po)
+                    typ = 1 if i == 0 else (3 if i == nf - 1 else 2)
+                    write_to_block(rec, po, fl, S, typ)
+                    po += fl
+                continue
+        if not write_to_block(rec, 0, S, S, 4):
+            refused += 1
+    flush()                                        # Close()
+    return blocks, refused
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def main():
+    g = {"generator": "tests/golden/gen_golden.py", "zlib_version": zlib.ZLIB_VERSION,
+         "crc": "CRC-32/ISO-HDLC (Go crc32.ChecksumIEEE)"}
+    rng = np.random.default_rng(0x48756E64)
+
+    # 1. known answers
+    g["known"] = {
+        "check_123456789": get_crc(b"123456789"),
+        "empty": get_crc(b""),
+        "zero_payload": {str(B): get_crc(bytes(B - 4)) for B in (4096, 8192, 16384)},
+        "vectors": [],
+    }
+    for n in [1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 31, 32, 63, 64, 65, 127, 128, 255, 256, 1000, 1023,
+              1024, 1025, 4092, 4095, 4096, 4097, 8188, 16380, 65536, 100003]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        g["known"]["vectors"].append({"hex": b.hex() if n <= 4096 else None,
+                                      "seed_fill": None if n <= 4096 else [0x1234, n],
+                                      "len": n, "crc": get_crc(b if n <= 4096 else
+                                                               fill_block(0x1234, n, (n + 7) // 8 * 8)[:n])})
+
+    # 2. per-function edge cases
+    fx = {}
+    fx["add_crc_to_block_data"] = []
+    for n in [0, 1, 2, 3, 4, 5, 8, 4096, 8192]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        fx["add_crc_to_block_data"].append({"in": b.hex(), "out": add_crc_to_block_data(b).hex()})
+    cbi = []
+    for n in [0, 3]:
+        cbi.append({"in": bytes(n).hex(), "err": check_block_integrity(bytes(n))})
+    cbi.append({"in": bytes(4).hex(), "err": check_block_integrity(bytes(4))})  # CRC("")==0 -> ok
+    for B in (4096, 8192, 16384):
+        blk = add_crc_to_block_data(rng.integers(0, 256, B, dtype=np.uint8).tobytes())
+        cbi.append({"in": blk.hex(), "err": check_block_integrity(blk)})
+        flipped = bytearray(blk)
+        bit = int(rng.integers(32, B * 8))
+        flipped[bit // 8] ^= 1 << (bit % 8)
+        cbi.append({"in": flipped.hex(), "err": check_block_integrity(flipped), "flipped_bit": bit})
+        hdr = bytearray(blk)
+        hdr[1] ^= 0x10  # corrupt the stored CRC itself
+        cbi.append({"in": hdr.hex(), "err": check_block_integrity(hdr)})
+    fx["check_block_integrity"] = cbi
+    fx["add_crcs_to_data"] = []
+    for n in [0, 1, 4091, 4092, 4093, 8184, 8185, 12276, 50000]:
+        src = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        out = add_crcs_to_data(src)
+        fx["add_crcs_to_data"].append({
+            "in": src.hex() if n <= 8185 else None, "seed_fill": None if n <= 8185 else [0x77, n],
+            "len_out": len(out), "sha256": sha(out),
+            "crcs": [struct.unpack("<I", out[i:i + 4])[0] for i in range(0, len(out), BLOCK_SIZE)]})
+        if n > 8185:  # regenerate deterministically from the seed instead of storing hex
+            src2 = fill_block(0x77, n, (n + 7) // 8 * 8)[:n]
+            out2 = add_crcs_to_data(src2)
+            fx["add_crcs_to_data"][-1].update({"len_out": len(out2), "sha256": sha(out2),
+                                               "crcs": [struct.unpack("<I", out2[i:i + 4])[0]
+                                                        for i in range(0, len(out2), BLOCK_SIZE)]})
+    fx["fix_last_block_crc"] = []
+    for n in [0, 4095, 4096, 8191, 8192, 12300]:
+        src = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        err, out = fix_last_block_crc(src)
+        fx["fix_last_block_crc"].append({"in": src.hex(), "err": err, "sha256": sha(out)})
+    sizes = [0, 1, 2, 3, 4, 5, 4091, 4092, 4093, 4096, 4097, 8184, 8185, 8192, 8193,
+             (1 << 53) - 1, (1 << 53) + 1, (1 << 63) + 12345, M64]
+    fx["size_after_adding_crcs"] = [[n, size_after_adding_crcs(n)] for n in sizes]
+    fx["size_without_crcs"] = [[n, size_without_crcs(n)] for n in sizes]
+    g["functions"] = fx
+
+    # 3. structural fixtures from the reference's own layouts
+    wal = {}
+    for name, recsizes in [("one_full_record", [35]),          # wal_test.go:230-279 shape
+                           ("record_1_5_blocks", [6138]),       # wal_test.go:385-449
+                           ("record_3_blocks", [12000]),        # wal_test.go:451-496
+                           ("exact_fill", [4092 - 17 - 17 - 100, 100]),   # wal_test.go:1100-1162
+                           ("refused_size", [4076, 64]),        # 4092 < 17+S <= 4096
+                           ("mixed_small", [64, 300, 1000, 4000, 70, 5000, 64])]:
+        blocks, refused = wal_frame(0xABCDEF, recsizes)
+        wal[name] = {"seed": 0xABCDEF, "record_sizes": recsizes, "blocks": len(blocks),
+                     "refused": refused, "sha256": [sha(b) for b in blocks],
+                     "crcs": [struct.unpack("<I", b[:4])[0] for b in blocks]}
+    g["wal"] = wal
+    # global_key_dict header block: [crc4 | count u64 | zero pad], recomputed CRC
+    # (utils/global_key_dict/global_key_dict_test.go:31-38 builds it by hand)
+    hdr = bytearray(4096)
+    hdr[4:12] = struct.pack("<Q", 7)
+    g["global_key_dict_header"] = {"count": 7, "crc": get_crc(hdr[4:])}
+
+    # 4. seeded synthetic batches
+    seed = 0x48756E64
+    crcs = []
+    h = hashlib.sha256()
+    for i in range(1000):                          # config 1: 1000 x 4 KiB
+        b = fill_block(seed, i, 4096)
+        h.update(b)
+        crcs.append(get_crc(b[4:]))
+    g["config1"] = {"seed": seed, "n": 1000, "block": 4096, "sha256_inputs": h.hexdigest(),
+                    "crcs": crcs}
+    mseed = 0x4D495845
+    ms, mc = [], []
+    for i in range(256):                           # config 3 shape, small
+        s = mixed_size(mseed, i)
+        b = fill_block(mseed, i, s)
+        ms.append(s)
+        mc.append(get_crc(b[4:]))
+    g["mixed"] = {"seed": mseed, "n": 256, "sizes": ms, "crcs": mc}
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
+    with open(path, "w") as f:
+        json.dump(g, f, indent=0)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    main()

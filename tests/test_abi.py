@@ -1,0 +1,191 @@
+"""C-ABI boundary and host logic, no GPU needed.
+
+- libhundcrc.so loads and exports every function include/hundcrc.h declares;
+- the drop-in utils/crc surface (hunddb_amd.crc, crc_util.go:10-122) matches the
+  golden fixtures and the oracle, including edge lengths and exact Go error texts;
+- the batched GPU entries fail loudly (HC_E_NODEV) when no gfx950 is present:
+  there is no CPU fallback on the hot path.
+"""
+import ctypes
+import hashlib
+import os
+import re
+import threading
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "hundcrc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol(hc):
+    names = header_functions()
+    assert len(names) >= 20
+    L = hc.lib()
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_version_and_strings(hc):
+    L = hc.lib()
+    assert b"gfx950" in L.hc_version()
+    assert L.hc_strerror(1) == b"invalid block data"                      # crc_util.go:90
+    assert L.hc_strerror(2) == b"CRC mismatch in block"                   # crc_util.go:96
+    assert L.hc_strerror(3) == b"data is too short to contain a complete block"  # :108
+
+
+def test_constants(hc):
+    assert hc.BLOCK_SIZE == 4096 and hc.CRC_SIZE == 4
+
+
+def test_getcrc_known(hc, golden):
+    k = golden["known"]
+    assert hc.GetCRC(b"123456789") == 0xCBF43926
+    assert hc.GetCRC(b"") == 0
+    for B, c in k["zero_payload"].items():
+        assert hc.GetCRC(bytes(int(B) - 4)) == c
+    for v in k["vectors"]:
+        if v["hex"] is not None:
+            assert hc.GetCRC(bytes.fromhex(v["hex"])) == v["crc"]
+
+
+def test_getcrc_vs_oracle_all_small_lengths(hc, oracle):
+    rng = np.random.default_rng(7)
+    for n in range(0, 600):
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert hc.GetCRC(b) == oracle.checksum(b), n
+
+
+def test_add_crc_to_block_data(hc, golden):
+    for c in golden["functions"]["add_crc_to_block_data"]:
+        b = bytearray.fromhex(c["in"])
+        r = hc.AddCRCToBlockData(b)
+        assert r is b                       # returns the same slice (crc_util.go:32)
+        assert b.hex() == c["out"]
+
+
+def test_check_block_integrity(hc, golden):
+    for c in golden["functions"]["check_block_integrity"]:
+        err = hc.CheckBlockIntegrity(bytes.fromhex(c["in"]))
+        assert (None if err is None else str(err)) == c["err"]
+
+
+def test_add_crcs_to_data(hc, golden, oracle):
+    for c in golden["functions"]["add_crcs_to_data"]:
+        if c["in"] is not None:
+            src = bytes.fromhex(c["in"])
+        else:
+            seed, n = c["seed_fill"]
+            n8 = (n + 7) // 8 * 8
+            a = np.zeros(n8, dtype=np.uint8)
+            oracle.lib().oc_fill_block(seed, n, a.ctypes.data, n8)
+            src = a.tobytes()[:n]
+        if len(src) // 4092 >= 200:
+            continue  # multi-hundred-block outputs take the GPU (tests/test_gpu_parity.py)
+        out = hc.AddCRCsToData(src)
+        assert len(out) == c["len_out"]
+        assert hashlib.sha256(bytes(out)).hexdigest() == c["sha256"]
+
+
+def test_fix_last_block_crc(hc, golden):
+    for c in golden["functions"]["fix_last_block_crc"]:
+        b = bytearray.fromhex(c["in"])
+        err = hc.FixLastBlockCRC(b)
+        assert (None if err is None else str(err)) == c["err"]
+        assert hashlib.sha256(bytes(b)).hexdigest() == c["sha256"]
+
+
+def test_size_helpers(hc, golden):
+    for n, want in golden["functions"]["size_after_adding_crcs"]:
+        assert hc.SizeAfterAddingCRCs(n) == want, n
+    for n, want in golden["functions"]["size_without_crcs"]:
+        assert hc.SizeWithoutCRCs(n) == want, n
+
+
+def test_size_roundtrip_property(hc):
+    # SizeWithoutCRCs(SizeAfterAddingCRCs(n)) == n for every n whose framed size
+    # is not a multiple of 4096 + <4 (block_manager.go:239 relies on this)
+    for n in list(range(0, 20000, 7)) + [4092 * k for k in range(1, 50)]:
+        assert hc.SizeWithoutCRCs(hc.SizeAfterAddingCRCs(n)) == n
+
+
+def test_error_values_compare_like_go(hc):
+    a = hc.CheckBlockIntegrity(b"abc")
+    b = hc.CheckBlockIntegrity(b"xy")
+    assert a == b and str(a) == "invalid block data"
+
+
+def test_corruption_is_detected_every_bit(hc):
+    """Unlike TestWAL_CorruptionDetection (wal_test.go:847-914) this asserts."""
+    blk = hc.AddCRCToBlockData(bytearray(np.random.default_rng(3).integers(0, 256, 4096, dtype=np.uint8).tobytes()))
+    assert hc.CheckBlockIntegrity(blk) is None
+    for bit in range(0, 4096 * 8, 97):
+        c = bytearray(blk)
+        c[bit // 8] ^= 1 << (bit % 8)
+        assert str(hc.CheckBlockIntegrity(c)) == "CRC mismatch in block"
+
+
+def test_concurrent_small_calls(hc, oracle):
+    """Re-entrancy: 8 threads (flush workers / readers, block_manager_test.go:259-349)."""
+    rng = np.random.default_rng(11)
+    blocks = [rng.integers(0, 256, 4096, dtype=np.uint8).tobytes() for _ in range(64)]
+    want = [oracle.checksum(b[4:]) for b in blocks]
+    errors = []
+
+    def work():
+        for _ in range(20):
+            for b, w in zip(blocks, want):
+                x = hc.AddCRCToBlockData(bytearray(b))
+                if int.from_bytes(x[:4], "little") != w or hc.CheckBlockIntegrity(x) is not None:
+                    errors.append(1)
+
+    ts = [threading.Thread(target=work) for _ in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors
+
+
+def test_debug_tables_consistent(hc):
+    """The constant image the kernels read reproduces CRC-32 through the
+    kernel's own decomposition (rows of 1024 B, 4 streams/lane, lane placement)."""
+    import zlib
+    t = hc.debug_tables()
+    tg, s4 = t[0:1024].reshape(4, 256), t[1024:2048].reshape(4, 256)
+    lane, w0 = t[2048:4096].reshape(64, 32), int(t[4096])
+
+    def tab(T, c):
+        return T[0][c & 255] ^ T[1][(c >> 8) & 255] ^ T[2][(c >> 16) & 255] ^ T[3][c >> 24]
+
+    rng = np.random.default_rng(9)
+    for B in (1024, 4096, 8192, 16384):
+        blk = rng.integers(0, 256, B, dtype=np.uint8).tobytes()
+        w = np.frombuffer(blk, dtype="<u4").reshape(B // 1024, 64, 4).copy()
+        w[0, 0, 0] = w0
+        c = w[0].copy()
+        for r in range(1, B // 1024):
+            c = tab(tg, c) ^ w[r]
+        d = tab(s4, tab(s4, tab(s4, c[:, 0]) ^ c[:, 1]) ^ c[:, 2]) ^ c[:, 3]
+        e = np.zeros(64, dtype=np.uint32)
+        for i in range(32):
+            e ^= np.where((d >> i) & 1, lane[:, i], 0).astype(np.uint32)
+        assert (int(np.bitwise_xor.reduce(e)) ^ 0xFFFFFFFF) == zlib.crc32(blk[4:])
+
+
+def test_batch_entries_fail_loudly_without_gpu(hc):
+    if hc.device_count() > 0:
+        pytest.skip("a gfx950 device is present")
+    buf = np.zeros(4096 * 4, dtype=np.uint8)
+    with pytest.raises(hc.HundCRCError) as ei:
+        hc.crc32_blocks(buf)
+    assert ei.value.code == -3
+    with pytest.raises(hc.HundCRCError):
+        hc.stamp_blocks(buf)
+    # multi-hundred-block AddCRCsToData is a GPU batch too
+    with pytest.raises(hc.HundCRCError):
+        hc.AddCRCsToData(bytes(4092 * 300))

@@ -1,0 +1,300 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle, bit-exact.
+
+Sizes: BASELINE.json configs 1-3 and the north-star 1M x 8 KiB at full size
+(the oracle checks every CRC word, threaded), plus the edge cases the
+reference path has: lengths 0..3 ("invalid block data"), unaligned blocks,
+lengths that are not multiples of the 1 KiB row, whole-message CRCs, corrupt
+blocks (verify bitmap / first bad index), in-place stamping and WAL-framed
+blocks (lsm/wal/wal.go:177-271).
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x48756E64
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def dev_uniform(torch, hc, seed, n, size):
+    buf = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    hc.dev_fill_blocks(buf, seed, stride=size, ulen=size, nblocks=n)
+    return buf
+
+
+def dev_crc(torch, hc, buf, n, **kw):
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    hc.dev_crc32_blocks(buf, out, nblocks=n, **kw)
+    torch.cuda.synchronize()
+    return u32(out)
+
+
+def test_zero_payload_known_answers(cuda, hc, golden):
+    torch = cuda
+    for B, want in golden["known"]["zero_payload"].items():
+        B = int(B)
+        buf = torch.zeros(1000 * B, dtype=torch.uint8, device="cuda")
+        got = dev_crc(torch, hc, buf, 1000, stride=B, ulen=B)
+        assert (got == want).all(), B
+        assert hc.last_launch()["kernel"] == "k_crc_fast"
+
+
+def test_config1_golden(cuda, hc, golden):
+    torch = cuda
+    c = golden["config1"]
+    buf = dev_uniform(torch, hc, c["seed"], c["n"], c["block"])
+    import hashlib
+    assert hashlib.sha256(buf.cpu().numpy().tobytes()).hexdigest() == c["sha256_inputs"]
+    got = dev_crc(torch, hc, buf, c["n"], stride=c["block"], ulen=c["block"])
+    assert got.tolist() == c["crcs"]
+
+
+@pytest.mark.parametrize("size", [4096, 8192, 16384])
+def test_full_size_uniform(cuda, hc, oracle, size):
+    """configs[1] (1M x 4 KiB) and the north star (1M x 8 KiB) at full size;
+    16 KiB at 0.5M blocks.  Every word checked against the oracle."""
+    torch = cuda
+    n = 1_000_000 if size <= 8192 else 500_000
+    buf = dev_uniform(torch, hc, SEED + size, n, size)
+    got = dev_crc(torch, hc, buf, n, stride=size, ulen=size)
+    host = buf.cpu().numpy()
+    del buf
+    want = oracle.crc32_blocks(host, stride=size, ulen=size, threads=16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}"
+
+
+def test_config3_mixed_full(cuda, hc, oracle, golden):
+    """configs[2]: 1M blocks, each 4/8/16 KiB (seeded), packed + off[]/len[]."""
+    torch = cuda
+    m = golden["mixed"]
+    n = 1_000_000
+    L = oracle.lib()
+    sizes = np.array([L.oc_mixed_size(m["seed"], i) for i in range(n)], dtype=np.uint32)
+    assert sizes[: m["n"]].tolist() == m["sizes"]
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    total = int(off[-1]) + int(sizes[-1])
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(sizes.view(np.int32)).cuda()
+    hc.dev_fill_blocks(buf, m["seed"], off=doff, lens=dlen, nblocks=n)
+    got = dev_crc(torch, hc, buf, n, off=doff, lens=dlen)
+    assert got[: m["n"]].tolist() == m["crcs"]
+    host = buf.cpu().numpy()
+    del buf
+    want = oracle.crc32_blocks(host, off=off, lens=sizes, threads=16)
+    assert (got == want).all()
+
+
+def test_general_lengths_and_alignment(cuda, hc, oracle):
+    """Any length (0..70000, incl. <4) at any byte alignment; conforming blocks
+    take the streaming kernel, the rest the general kernel, in one call."""
+    torch = cuda
+    rng = np.random.default_rng(21)
+    n = 20000
+    lens = rng.integers(0, 9000, n).astype(np.uint32)
+    lens[:50] = np.arange(50)                     # tiny, incl. 0..3
+    lens[50:2000] = 1024 * rng.integers(1, 17, 1950)  # conforming sizes ...
+    lens[3000:3010] = 70000
+    gaps = rng.integers(0, 64, n).astype(np.uint64)
+    gaps[50:1000] = 0                              # ... some of them 16-B aligned
+    off = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        if 50 <= i < 1000:
+            pos = (pos + 15) & ~15
+        off[i] = pos
+        pos += int(lens[i])
+    host = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.view(np.int32)).cuda()
+    got = dev_crc(torch, hc, buf, n, off=doff, lens=dlen)
+    want = oracle.crc32_blocks(host, off=off, lens=lens, threads=16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:10], lens[bad[:10]], off[bad[:10]] % 16)
+
+
+def test_uniform_nonconforming_goes_general(cuda, hc, oracle):
+    torch = cuda
+    for size, stride in [(4100, 4100), (4096, 4100), (1000, 1000), (3, 8), (5000, 5008)]:
+        n = 3000
+        host = np.random.default_rng(size).integers(0, 256, n * stride + 16, dtype=np.uint8)
+        buf = torch.from_numpy(host).cuda()
+        got = dev_crc(torch, hc, buf, n, stride=stride, ulen=size)
+        assert hc.last_launch()["kernel"] == "k_crc_general"
+        want = oracle.crc32_blocks(host, stride=stride, ulen=size)
+        assert (got == want).all(), (size, stride)
+
+
+def test_messages_mode(cuda, hc, oracle):
+    """GetCRC over variable-length records (WAL records 64 B..64 KiB, config 5b)."""
+    torch = cuda
+    rng = np.random.default_rng(5)
+    n = 30000
+    lens = rng.integers(0, 66000, n).astype(np.uint32)
+    lens[:40] = np.arange(40)
+    lens[40:400] = 1024 * rng.integers(1, 40, 360)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 20, n - 1).astype(np.uint64))
+    size = int(off[-1] + lens[-1]) + 32
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.view(np.int32)).cuda()
+    got = dev_crc(torch, hc, buf, n, off=doff, lens=dlen, flags=hc.HC_F_MESSAGES)
+    want = oracle.crc32_messages(host, off, lens, threads=16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:10], lens[bad[:10]])
+
+
+def test_stamp_then_verify_and_corruption(cuda, hc, oracle):
+    torch = cuda
+    n, B = 200_000, 4096
+    buf = dev_uniform(torch, hc, 99, n, B)
+    hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, flags=hc.HC_F_STAMP)
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == 2**63 - 1 and int(bm.abs().sum().item()) == 0
+    # stamped words equal the oracle's AddCRCToBlockData
+    host = buf.cpu().numpy()
+    want = oracle.crc32_blocks(host, stride=B, ulen=B, threads=16)
+    assert (host.reshape(n, B)[:, :4].copy().view("<u4").reshape(-1) == want).all()
+    # corrupt: one flipped bit in each chosen block (payload or stored word)
+    rng = np.random.default_rng(8)
+    victims = np.sort(rng.choice(n, 777, replace=False))
+    pos = victims * B + rng.integers(0, B, victims.size)
+    bits = rng.integers(0, 8, victims.size)
+    idx = torch.from_numpy(pos.astype(np.int64)).cuda()
+    flip = torch.from_numpy((1 << bits).astype(np.uint8)).cuda()
+    buf[idx] ^= flip
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == int(victims[0])
+    bits_set = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    assert np.array_equal(np.nonzero(bits_set)[0], victims)
+
+
+def test_wal_blocks_verify(cuda, hc, oracle):
+    """Blocks framed exactly as lsm/wal/wal.go:177-271, verified as recoverMemtable does (:383)."""
+    torch = cuda
+    L = oracle.lib()
+    sizes = np.array([L.oc_wal_record_size(3, i, 64, 65536) for i in range(4000)], dtype=np.uint32)
+    blocks, st, _ = oracle.wal_frame(3, sizes)
+    nb = st.blocks
+    assert nb > 4000
+    buf = torch.from_numpy(blocks).cuda()
+    bm = torch.empty((nb + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, nb)
+    hc.dev_crc32_blocks(buf, None, stride=4096, ulen=4096, nblocks=nb, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == 2**63 - 1
+    buf[4096 * 17 + 4 + 17 + 10] ^= 1          # TestWAL_CorruptionDetection's byte (wal_test.go:884)
+    hc.dev_verify_prepare(bm, fb, nb)
+    hc.dev_crc32_blocks(buf, None, stride=4096, ulen=4096, nblocks=nb, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == 17
+
+
+def test_host_entries(cuda, hc, oracle, golden):
+    rng = np.random.default_rng(4)
+    # uniform, packed
+    host = rng.integers(0, 256, 5000 * 8192, dtype=np.uint8)
+    assert (hc.crc32_blocks(host, stride=8192, ulen=8192) ==
+            oracle.crc32_blocks(host, stride=8192, ulen=8192)).all()
+    # mixed with arbitrary offsets and lengths
+    lens = rng.integers(0, 20000, 3000).astype(np.uint32)
+    off = rng.integers(0, host.size - 20000, 3000).astype(np.uint64)
+    assert (hc.crc32_blocks(host, off=off, lens=lens) == oracle.crc32_blocks(host, off=off, lens=lens)).all()
+    # messages
+    assert (hc.crc32_messages(host, off, lens) == oracle.crc32_messages(host, off, lens)).all()
+    # stamp + verify + corrupt
+    blocks = rng.integers(0, 256, 3000 * 4096, dtype=np.uint8)
+    hc.stamp_blocks(blocks)
+    err, bm, fb = hc.verify_blocks(blocks)
+    assert err is None and fb == -1 and bm.sum() == 0
+    blocks[4096 * 1234 + 99] ^= 4
+    blocks[4096 * 2000 + 7] ^= 1
+    err, bm, fb = hc.verify_blocks(blocks)
+    assert str(err) == "CRC mismatch in block" and fb == 1234
+    assert np.nonzero(np.unpackbits(bm.view(np.uint8), bitorder="little"))[0].tolist() == [1234, 2000]
+    # invalid (short) block in a batch
+    err, bm, fb = hc.verify_blocks(blocks, off=np.array([0, 4096], np.uint64), lens=np.array([4096, 3], np.uint32))
+    assert str(err) == "invalid block data" and fb == 1
+
+
+def test_add_crcs_to_data_gpu(cuda, hc, oracle):
+    """AddCRCsToData (crc_util.go:41-64) over multi-hundred-block inputs runs on the GPU."""
+    rng = np.random.default_rng(12)
+    for n in [4092 * 256, 4092 * 1000 + 17, 3_000_001]:
+        src = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        out = hc.AddCRCsToData(src)
+        want = np.zeros(hc.lib().hc_add_crcs_size(n), dtype=np.uint8)
+        m = oracle.lib().oc_add_crcs_to_data(src, n, want.ctypes.data)
+        assert m == len(out) and bytes(out) == want.tobytes()
+
+
+def test_force_gpu_dropins(cuda, hc, golden, monkeypatch):
+    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    assert hc.GetCRC(b"123456789") == 0xCBF43926
+    for v in golden["known"]["vectors"]:
+        if v["hex"] is not None:
+            assert hc.GetCRC(bytes.fromhex(v["hex"])) == v["crc"]
+    for c in golden["functions"]["add_crc_to_block_data"]:
+        b = bytearray.fromhex(c["in"])
+        hc.AddCRCToBlockData(b)
+        assert b.hex() == c["out"]
+    for c in golden["functions"]["check_block_integrity"]:
+        err = hc.CheckBlockIntegrity(bytes.fromhex(c["in"]))
+        assert (None if err is None else str(err)) == c["err"]
+    for c in golden["functions"]["fix_last_block_crc"]:
+        b = bytearray.fromhex(c["in"])
+        hc.FixLastBlockCRC(b)
+        import hashlib
+        assert hashlib.sha256(bytes(b)).hexdigest() == c["sha256"]
+
+
+def test_concurrent_host_batches(cuda, hc, oracle):
+    """Flush workers / compaction goroutines calling the batch entry at once."""
+    rng = np.random.default_rng(6)
+    datas = [rng.integers(0, 256, 2000 * 4096, dtype=np.uint8) for _ in range(6)]
+    wants = [oracle.crc32_blocks(d) for d in datas]
+    errors = []
+
+    def work(i):
+        for _ in range(3):
+            if not (hc.crc32_blocks(datas[i]) == wants[i]).all():
+                errors.append(i)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(6)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors
+
+
+def test_side_stream(cuda, hc, oracle):
+    torch = cuda
+    s = torch.cuda.Stream()
+    n, B = 50_000, 8192
+    with torch.cuda.stream(s):
+        buf = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+        hc.dev_fill_blocks(buf, 77, stride=B, ulen=B, nblocks=n, stream=s)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        hc.dev_crc32_blocks(buf, out, stride=B, ulen=B, nblocks=n, stream=s)
+    s.synchronize()
+    host = buf.cpu().numpy()
+    assert (u32(out) == oracle.crc32_blocks(host, stride=B, ulen=B, threads=16)).all()
