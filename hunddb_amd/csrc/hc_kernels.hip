@@ -96,12 +96,47 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 // Streaming kernel.  Pointer arguments are separate __restrict__ kernel
 // arguments so the per-block metadata reads (off/len) become scalar s_loads
 // (lgkmcnt) instead of vector loads that would drain the row ring (vmcnt(0)).
-template <bool kUniform>
-__global__ __launch_bounds__(kFastThreads) void k_crc_fast(
+//
+// Tunables (FastCfg): waves per workgroup (one workgroup per CU, LDS-bound),
+// ring depth (rows in flight per wave = kRing-1 while one is hashed), load
+// cache policy (0 plain, 1 nontemporal), block order (0: each wave owns a
+// contiguous run of blocks; 1: block b goes to wave b % W -- uniform layout
+// only) and kNull (timing-only build: rows are XOR-folded instead of
+// CRC'd, to measure the memory ceiling of exactly this access pattern).
+template <int W_, int R_, int P_, int O_, bool N_ = false>
+struct FastCfg {
+  static constexpr int kWaves = W_, kRing = R_, kPolicy = P_, kOrder = O_;
+  static constexpr bool kNull = N_;
+};
+using DefaultFastCfg = FastCfg<kFastWaves, 4, 1, 0>;  // kbench r1: nt loads +17%, ring 4 best
+
+// Row load, 16 B per lane.  Policy 0: plain global_load_dwordx4; 1: the same
+// with the nontemporal (nt) bit; 2..5: buffer_load_dwordx4 with cache-policy
+// bits (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16) nt, sc0|nt, sc1|nt, sc0|sc1|nt.
+template <int kPolicy>
+__device__ __forceinline__ uint4 load_row(const uint8_t *row, uint32_t lane) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 v;
+  if constexpr (kPolicy == 0) {
+    v = *reinterpret_cast<const u32x4 *>(row + lane * 16u);
+  } else if constexpr (kPolicy == 1) {
+    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(row + lane * 16u));
+  } else {
+    constexpr int aux = kPolicy == 2 ? 2 : kPolicy == 3 ? 3 : kPolicy == 4 ? 18 : 19;
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(row), 0, kRowBytes, 0x00020000);
+    v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16u, 0, aux));
+  }
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <bool kUniform, class Cfg>
+__global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
+  constexpr int kWaves = Cfg::kWaves, kThreads = kWaves * 64, kRing = Cfg::kRing;
+  constexpr bool kInterleave = kUniform && Cfg::kOrder == 1;
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
@@ -110,14 +145,14 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
   // replica r) = (k>>1)<<16 | v<<8 | (k&1)<<7 | r<<2; s4 region address
   // = kLdsMainBytes + k*4096 + v*16 + (r&3)*4.
   const uint32_t *tg = &tables->tg[0][0];
-  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kThreads) {
     const uint32_t a = q * 16;
     const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
     const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
     *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
   }
   const uint32_t *s4 = &tables->s4[0][0];
-  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kThreads) {
     const uint32_t v = s4[q];
     *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
         make_uint4(v, v, v, v);
@@ -135,6 +170,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
 
   // c <- shift(c, 1024) ^ w : four conflict-free lookups, one v_perm each.
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (Cfg::kNull) return c ^ w;
     const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
     const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
     const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
@@ -150,9 +186,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
   };
 
   const uint32_t wave = uni(tid >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
-  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
-  const uint64_t b0 = uni64(nblocks * gw / W), b1 = uni64(nblocks * (gw + 1) / W);
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kWaves;
+  const uint64_t b0 = kInterleave ? gw : uni64(nblocks * gw / W);
+  const uint64_t b1 = kInterleave ? nblocks : uni64(nblocks * (gw + 1) / W);
 
   // Advance a cursor to the first block >= from that this kernel handles.
   auto seek = [&](uint64_t from, uint64_t &blk, const uint8_t *&ptr, uint32_t &rows) -> bool {
@@ -175,6 +212,8 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
     }
     return false;
   };
+  constexpr uint64_t kStep = 1;
+  const uint64_t step = kInterleave ? W : kStep;
 
   uint64_t pb = 0, cb = 0;
   const uint8_t *pptr = nullptr, *cptr = nullptr;
@@ -187,12 +226,12 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
   // Producer: issue the load of the next row, then advance (clamped at the
   // wave's last row so every issued load is in bounds).
   auto load_next = [&]() -> uint4 {
-    const uint4 v = *reinterpret_cast<const uint4 *>(pptr + (size_t)prow * kRowBytes + lane * 16u);
+    const uint4 v = load_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, lane);
     if (++prow == prows) {
       uint64_t nb;
       const uint8_t *np;
       uint32_t nr;
-      if (seek(pb + 1, nb, np, nr)) {
+      if (seek(pb + step, nb, np, nr)) {
         pb = nb;
         pptr = np;
         prows = nr;
@@ -204,7 +243,6 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
     return v;
   };
 
-  constexpr int kRing = 8;
   uint4 ring[kRing];
 #pragma unroll
   for (int u = 0; u < kRing; u++) ring[u] = load_next();
@@ -233,8 +271,13 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
       }
       ring[u] = load_next();
       if (++crow == crows) {
-        const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
-        const uint32_t crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        uint32_t crc;
+        if constexpr (Cfg::kNull) {
+          crc = wave_xor(c0 ^ c1 ^ c2 ^ c3);
+        } else {
+          const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
+          crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        }
         if (lane == 0) {
           if (crc_out) crc_out[cb] = crc;
           if (flags & kFlagStamp) *const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(cptr)) = crc;
@@ -246,7 +289,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(
                                    __HIP_MEMORY_SCOPE_AGENT);
           }
         }
-        if (!seek(cb + 1, cb, cptr, crows)) return;
+        if (!seek(cb + step, cb, cptr, crows)) return;
         crow = 0;
       }
     }
@@ -412,14 +455,15 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 }  // namespace
 
 hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s) {
+  using C = DefaultFastCfg;
   if (uniform_fast)
-    hipLaunchKernelGGL(k_crc_fast<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len,
-                       b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap, b.first_bad,
-                       b.tables);
+    hipLaunchKernelGGL((k_crc_fast<true, C>), dim3(grid), dim3(C::kWaves * 64), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap,
+                       b.first_bad, b.tables);
   else
-    hipLaunchKernelGGL(k_crc_fast<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len,
-                       b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap, b.first_bad,
-                       b.tables);
+    hipLaunchKernelGGL((k_crc_fast<false, C>), dim3(grid), dim3(C::kWaves * 64), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap,
+                       b.first_bad, b.tables);
   return hipGetLastError();
 }
 
