@@ -155,7 +155,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from hunddb_amd import crc
+    from hunddb_amd import crc, shard
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -165,10 +165,10 @@ def main():
     nblk, bsize, scaling = WORKLOADS[args.workload]
     if args.blocks:
         nblk = args.blocks
-    if scaling == "strong":
-        lo, hi = nblk * rank // world, nblk * (rank + 1) // world
+    if scaling == "strong":  # one global batch, partitioned by block index
+        lo, hi = shard.index_range(nblk, world, rank)
         my = hi - lo
-    else:
+    else:  # every rank owns its own full-size shard (blocks rank*n .. rank*n+n-1)
         lo, my = nblk * rank, nblk
     stream = torch.cuda.current_stream()
     seed = 0x48756E64
@@ -219,15 +219,9 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     mean_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
 
-    if world > 1:
-        t = torch.tensor([dt, mean_kern_s], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, mean_kern_s = float(t[0]), float(t[1])
-        tb = torch.tensor([step_bytes], dtype=torch.float64, device=dev)
-        dist.all_reduce(tb, op=dist.ReduceOp.SUM)
-        job_bytes = float(tb[0]) * args.steps
-    else:
-        job_bytes = float(step_bytes) * args.steps
+    # max-over-ranks clock, summed bytes (RCCL all-reduce of 3 scalars, after the timed region)
+    dt, mean_kern_s, all_bytes = shard.job_timing(dt, mean_kern_s, float(step_bytes), device=dev)
+    job_bytes = all_bytes * args.steps
 
     if args.child:
         if world > 1:

@@ -1,0 +1,68 @@
+"""Multi-GPU partition of a block batch: one process per GPU, shard by block index.
+
+CRCs of independent blocks are independent, so nothing is exchanged while
+computing.  The only collectives are outside the data path:
+gathering the 4-byte CRC words to a root (``gather_crcs``) and reducing the
+benchmark clock (``job_timing``).  With the "nccl" backend these are RCCL
+collectives over xGMI; the same code runs on "gloo" for the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def index_range(nblocks: int, world: int, rank: int):
+    """Contiguous block-index range [lo, hi) of `rank` (sizes differ by <= 1)."""
+    return nblocks * rank // world, nblocks * (rank + 1) // world
+
+
+def byte_balanced_bounds(lens, world: int) -> np.ndarray:
+    """Split boundaries (world+1 indices) balancing the sum of block bytes per
+    rank for mixed 4/8/16 KiB batches, using prefix sums."""
+    lens = np.asarray(lens, dtype=np.uint64)
+    csum = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)])
+    total = int(csum[-1])
+    targets = [total * r // world for r in range(world + 1)]
+    b = np.searchsorted(csum, targets, side="left").astype(np.int64)
+    b[0], b[-1] = 0, len(lens)
+    return np.maximum.accumulate(b)
+
+
+def gather_crcs(local, counts, dst: int = 0, group=None):
+    """Gather every rank's CRC words (torch int32 tensor) to `dst`, in rank order.
+
+    `counts[r]` = number of blocks of rank r.  Returns the concatenated tensor on
+    `dst` and None elsewhere.  Variable sizes are padded to max(counts).
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    m = max(counts)
+    pad = torch.zeros(m, dtype=local.dtype, device=local.device)
+    pad[: local.numel()] = local
+    if dist.get_backend(group) == "nccl":
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+    else:
+        bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+        dist.gather(pad, bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+
+def job_timing(wall_s: float, kernel_s: float, local_bytes: float, device=None, group=None):
+    """Whole-job numbers for the benchmark: (max wall over ranks, max mean
+    kernel time over ranks, sum of bytes over ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return wall_s, kernel_s, local_bytes
+    t = torch.tensor([wall_s, kernel_s], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    b = torch.tensor([local_bytes], dtype=torch.float64, device=device)
+    dist.all_reduce(b, op=dist.ReduceOp.SUM, group=group)
+    return float(t[0]), float(t[1]), float(b[0])

@@ -1,0 +1,99 @@
+"""N>1 path on CPU: world_size-2 (and 3) gloo process groups.
+
+Each rank owns a contiguous block-index shard (hunddb_amd.shard), computes
+its CRC words (here with the oracle, standing in for the per-GPU kernel),
+gathers them to rank 0 and the job clock is max-reduced -- exactly the
+bench.py --gpus N flow minus the device.  Rank 0 checks against the
+single-process result.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, B, mixed, q):
+    import torch
+    import torch.distributed as dist
+
+    from hunddb_amd import shard
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if mixed:
+            sizes = O.mixed_sizes(0x4D495845, n)
+            bounds = shard.byte_balanced_bounds(sizes, world)
+            lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+            counts = [int(bounds[r + 1] - bounds[r]) for r in range(world)]
+        else:
+            sizes = np.full(n, B, dtype=np.uint32)
+            lo, hi = shard.index_range(n, world, rank)
+            counts = [shard.index_range(n, world, r)[1] - shard.index_range(n, world, r)[0] for r in range(world)]
+        # the rank's resident shard: blocks lo..hi of the global batch
+        buf = np.zeros(int(sizes[lo:hi].sum()), dtype=np.uint8)
+        off = np.zeros(hi - lo, dtype=np.uint64)
+        off[1:] = np.cumsum(sizes[lo:hi - 1], dtype=np.uint64) if hi - lo > 1 else off[1:]
+        for j, i in enumerate(range(lo, hi)):
+            O.lib().oc_fill_block(0x77, i, buf.ctypes.data + int(off[j]), int(sizes[i]))
+        local = O.crc32_blocks(buf, off=off, lens=sizes[lo:hi])
+        got = shard.gather_crcs(torch.from_numpy(local.view(np.int32)), counts)
+        wall, kern, tot = shard.job_timing(0.5 + rank, 0.1 * (rank + 1), float(buf.size))
+        if rank == 0:
+            q.put((got.numpy().view(np.uint32).copy(), wall, kern, tot, counts))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mixed", [(2, False), (2, True), (3, True)])
+def test_sharded_crcs_match_single_process(world, mixed, oracle):
+    n, B = 3001, 4096
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, B, mixed, q)) for r in range(world)]
+    [p.start() for p in procs]
+    got, wall, kern, tot, counts = q.get(timeout=120)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    sizes = oracle.mixed_sizes(0x4D495845, n) if mixed else np.full(n, B, dtype=np.uint32)
+    full = np.zeros(int(sizes.sum()), dtype=np.uint8)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    for i in range(n):
+        oracle.lib().oc_fill_block(0x77, i, full.ctypes.data + int(off[i]), int(sizes[i]))
+    want = oracle.crc32_blocks(full, off=off, lens=sizes)
+    assert np.array_equal(got, want)
+    assert wall == 0.5 + (world - 1) and abs(kern - 0.1 * world) < 1e-12
+    assert tot == float(sizes.sum())
+    assert sum(counts) == n
+
+
+def test_byte_balance():
+    from hunddb_amd import shard
+    rng = np.random.default_rng(0)
+    lens = (4096 << rng.integers(0, 3, 100000)).astype(np.uint32)
+    for world in (2, 4, 8):
+        b = shard.byte_balanced_bounds(lens, world)
+        sums = [int(lens[b[r]:b[r + 1]].sum()) for r in range(world)]
+        assert b[0] == 0 and b[-1] == len(lens) and sum(sums) == int(lens.sum())
+        assert max(sums) - min(sums) <= 2 * 16384
+
+
+def test_index_range_covers():
+    from hunddb_amd import shard
+    for n in (0, 1, 7, 16_000_000):
+        for w in (1, 2, 3, 8):
+            r = [shard.index_range(n, w, k) for k in range(w)]
+            assert r[0][0] == 0 and r[-1][1] == n and all(r[k][1] == r[k + 1][0] for k in range(w - 1))
