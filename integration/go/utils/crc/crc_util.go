@@ -1,0 +1,111 @@
+// Package crc is the cgo binding of HundDB's utils/crc onto libhundcrc.so
+// (include/hundcrc.h): a drop-in for /root/reference/utils/crc/crc_util.go
+// with the identical exported surface (names, types, constant kinds, error
+// texts), so lsm/wal, lsm/block_manager, lsm/sstable, lsm and probabilistic/*
+// compile and behave unchanged.  Not compiled in this repository (no Go
+// toolchain here or on the GPU box); see INTEGRATION.md.
+package crc
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../../hunddb_amd -lhundcrc -Wl,-rpath,${SRCDIR}/../../../../hunddb_amd
+#include <stdint.h>
+#include "hundcrc.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"unsafe"
+)
+
+// BLOCK_SIZE keeps the typed-uint64 form and CRC_SIZE the untyped form of
+// crc_util.go:11-12 (CRC_SIZE is used in both int and uint64 contexts).
+const BLOCK_SIZE = 1024 * uint64(4)
+const CRC_SIZE = 4
+
+func ptr(b []byte) *C.uint8_t {
+	if len(b) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&b[0]))
+}
+
+func goErr(rc C.int) error {
+	if rc == C.HC_OK {
+		return nil
+	}
+	if rc < 0 { // library failure (no GPU for a batch, HIP error): never silent
+		panic("hundcrc: " + C.GoString(C.hc_strerror(rc)))
+	}
+	return errors.New(C.GoString(C.hc_strerror(rc))) // exact crc_util.go texts
+}
+
+// GetCRC calculates CRC32 checksum over a byte array (crc_util.go:15).
+func GetCRC(data []byte) uint32 {
+	return uint32(C.hc_crc32_ieee(ptr(data), C.size_t(len(data))))
+}
+
+// AddCRCToBlockData stamps data[0:4] in place and returns data (crc_util.go:21).
+func AddCRCToBlockData(data []byte) []byte {
+	if len(data) < CRC_SIZE {
+		return data
+	}
+	_ = goErr(C.hc_add_crc_block(ptr(data), C.size_t(len(data))))
+	return data
+}
+
+// AddCRCsToData frames data into BLOCK_SIZE blocks with a CRC each (crc_util.go:41).
+// Multi-hundred-block inputs are CRC'd in one GPU batch.
+func AddCRCsToData(serializedData []byte) []byte {
+	out := make([]byte, int(C.hc_add_crcs_size(C.size_t(len(serializedData)))))
+	if len(out) == 0 {
+		return out
+	}
+	w := C.hc_add_crcs(ptr(serializedData), C.size_t(len(serializedData)), ptr(out), C.size_t(len(out)))
+	if w == ^C.size_t(0) {
+		panic("hundcrc: AddCRCsToData failed")
+	}
+	return out
+}
+
+// SizeAfterAddingCRCs (crc_util.go:69).
+func SizeAfterAddingCRCs(originalSize uint64) uint64 {
+	return uint64(C.hc_size_after_crcs(C.uint64_t(originalSize)))
+}
+
+// SizeWithoutCRCs (crc_util.go:79).
+func SizeWithoutCRCs(originalSize uint64) uint64 {
+	return uint64(C.hc_size_without_crcs(C.uint64_t(originalSize)))
+}
+
+// CheckBlockIntegrity (crc_util.go:88): nil, "invalid block data" or "CRC mismatch in block".
+func CheckBlockIntegrity(blockData []byte) error {
+	return goErr(C.hc_check_block(ptr(blockData), C.size_t(len(blockData))))
+}
+
+// FixLastBlockCRC (crc_util.go:106): restamps the last complete block in place.
+func FixLastBlockCRC(data []byte) error {
+	return goErr(C.hc_fix_last_block(ptr(data), C.size_t(len(data))))
+}
+
+// ---- batched entries (new; the GPU hot path) ------------------------------
+
+// CheckBlocksIntegrity verifies every blockSize-byte block of data in one GPU
+// batch (the per-block loop of BlockManager.ReadFromDisk,
+// block_manager.go:203-235, and WAL recovery, wal.go:366-403).  It returns
+// the index of the first failing block (-1 if none) and that block's error.
+func CheckBlocksIntegrity(data []byte, blockSize int) (int, error) {
+	n := len(data) / blockSize
+	var first C.int64_t = -1
+	rc := C.hc_verify_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize),
+		C.uint64_t(n), nil, &first)
+	return int(first), goErr(rc)
+}
+
+// AddCRCToBlocks stamps every blockSize-byte block of data in one GPU batch
+// (flushBlock over a run of WAL blocks, wal.go:260-271).
+func AddCRCToBlocks(data []byte, blockSize int) {
+	n := len(data) / blockSize
+	_ = goErr(C.hc_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize), C.uint64_t(n)))
+}
