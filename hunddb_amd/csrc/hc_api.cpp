@@ -152,7 +152,13 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
 }
 
 // ---------------------------------------------------------------------------
-// Host-resident batches: per-thread pipeline through pinned staging.
+// Host-resident batches: per-thread pipeline of kSlots slots.  Each slot owns
+// pinned staging, device buffers, a non-blocking stream and an event, so the
+// CPU gather of chunk k+1 overlaps the H2D copy / kernel / D2H copy of the
+// chunks before it.  A caller buffer that is already pinned (hipHostMalloc /
+// hipHostRegister) is DMA'd directly, without the staging copy.
+constexpr int kSlots = 3;
+
 struct Slot {
   uint8_t *pin = nullptr;    // pinned staging (blocks, packed, 16-B aligned)
   uint64_t *pin_off = nullptr;
@@ -172,7 +178,7 @@ struct HostPipe {
   int dev = -1;
   size_t chunk = 0;   // staging bytes per slot
   size_t maxblk = 0;  // metadata capacity per slot
-  Slot slot[2];
+  Slot slot[kSlots];
   bool ok = false;
 
   int init(int d) {
@@ -227,6 +233,31 @@ thread_local HostPipe t_pipe;
 inline uint64_t blk_off(const uint64_t *off, uint64_t stride, uint64_t i) { return off ? off[i] : i * stride; }
 inline uint32_t blk_len(const uint32_t *len, uint32_t ulen, uint64_t i) { return len ? len[i] : ulen; }
 
+// fn(t) on `threads` threads (the caller runs t = 0)
+template <class F>
+void parallel_for(int threads, F &&fn) {
+  if (threads <= 1) {
+    fn(0);
+    return;
+  }
+  std::vector<std::thread> ts;
+  ts.reserve(threads - 1);
+  for (int t = 1; t < threads; t++) ts.emplace_back([&fn, t] { fn(t); });
+  fn(0);
+  for (auto &t : ts) t.join();
+}
+
+bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky "invalid value" of pageable memory
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+thread_local uint64_t t_host_bytes = 0;  // bytes moved by the last host batch (stats)
+
 // Runs CRCs of host blocks on the GPU; results into crc_out[0..n).  Blocks
 // larger than one staging slot are rejected (HC_E_ARG): the on-disk block
 // sizes are 4-16 KiB (utils/config/config.go:137, README.md:191,255).
@@ -238,7 +269,11 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
   HostPipe &P = t_pipe;
   if ((st = P.init(dev)) != HC_OK) return st;
   DeviceGuard g(dev);
-  uint64_t i = 0, chunks = 0;
+  const int copy_threads = std::max(1, env_int("HC_COPY_THREADS", 8));
+  // direct DMA: uniform, densely packed (stride == ulen, 16-B multiple) and already pinned
+  const bool direct = !off && !len && stride == ulen && ulen > 0 && (ulen & 15u) == 0 &&
+                      (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && is_pinned(base);
+  uint64_t i = 0, chunks = 0, moved = 0;
   int rc = HC_OK;
   auto retire = [&](Slot &s) -> int {
     if (!s.busy) return HC_OK;
@@ -248,40 +283,66 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     return HC_OK;
   };
   while (i < n && rc == HC_OK) {
-    Slot &s = P.slot[chunks & 1];
+    Slot &s = P.slot[chunks % kSlots];
     if ((rc = retire(s)) != HC_OK) break;
-    // gather blocks [i, j) into the slot (16-B aligned packing)
     uint64_t j = i, pos = 0;
-    bool uniform = true;
-    const uint32_t l0 = blk_len(len, ulen, i);
-    while (j < n && j - i < P.maxblk) {
-      const uint32_t l = blk_len(len, ulen, j);
-      const uint64_t need = (pos + l + 15) & ~uint64_t(15);
-      if (need > P.chunk) break;
-      std::memcpy(s.pin + pos, base + blk_off(off, stride, j), l);
-      s.pin_off[j - i] = pos;
-      s.pin_len[j - i] = l;
-      uniform = uniform && l == l0;
-      pos = need;
-      j++;
-    }
-    if (j == i) {
-      rc = HC_E_ARG;  // a single block larger than the staging slot
-      break;
-    }
-    const uint64_t nb = j - i;
-    const bool packed_uniform = uniform && (l0 & 15u) == 0;  // then off = k*l0
-    if (hipMemcpyAsync(s.dbuf, s.pin, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
-      rc = HC_E_HIP;
-      break;
-    }
-    if (!packed_uniform) {
-      if (hipMemcpyAsync(s.doff, s.pin_off, nb * 8, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
-          hipMemcpyAsync(s.dlen, s.pin_len, nb * 4, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+    bool packed_uniform;
+    uint32_t l0 = blk_len(len, ulen, i);
+    if (direct) {
+      j = std::min<uint64_t>(n, i + std::max<uint64_t>(1, P.chunk / ulen));
+      j = std::min<uint64_t>(j, i + P.maxblk);
+      pos = (j - i) * (uint64_t)ulen;
+      if (pos > P.chunk) {
+        rc = HC_E_ARG;
+        break;
+      }
+      if (hipMemcpyAsync(s.dbuf, base + i * stride, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+        rc = HC_E_HIP;
+        break;
+      }
+      packed_uniform = true;
+    } else {
+      // plan the chunk: blocks [i, j) packed at 16-B aligned offsets
+      bool uniform = true;
+      while (j < n && j - i < P.maxblk) {
+        const uint32_t l = blk_len(len, ulen, j);
+        const uint64_t need = (pos + l + 15) & ~uint64_t(15);
+        if (need > P.chunk) break;
+        s.pin_off[j - i] = pos;
+        s.pin_len[j - i] = l;
+        uniform = uniform && l == l0;
+        pos = need;
+        j++;
+      }
+      if (j == i) {
+        rc = HC_E_ARG;  // a single block larger than the staging slot
+        break;
+      }
+      const uint64_t nb = j - i;
+      // gather into pinned staging on copy_threads threads
+      const int th = (int)std::min<uint64_t>((uint64_t)copy_threads, std::max<uint64_t>(1, pos >> 22));
+      parallel_for(th, [&](int t) {
+        const uint64_t a = nb * t / th, b = nb * (t + 1) / th;
+        if (!off && !len && stride == ulen) {  // contiguous source: one memcpy per thread
+          if (b > a) std::memcpy(s.pin + s.pin_off[a], base + (i + a) * stride, (b - a) * (uint64_t)ulen);
+        } else {
+          for (uint64_t k = a; k < b; k++)
+            std::memcpy(s.pin + s.pin_off[k], base + blk_off(off, stride, i + k), s.pin_len[k]);
+        }
+      });
+      packed_uniform = uniform && (l0 & 15u) == 0;  // then off = k*l0
+      if (hipMemcpyAsync(s.dbuf, s.pin, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+        rc = HC_E_HIP;
+        break;
+      }
+      if (!packed_uniform &&
+          (hipMemcpyAsync(s.doff, s.pin_off, nb * 8, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+           hipMemcpyAsync(s.dlen, s.pin_len, nb * 4, hipMemcpyHostToDevice, s.stream) != hipSuccess)) {
         rc = HC_E_HIP;
         break;
       }
     }
+    const uint64_t nb = j - i;
     rc = packed_uniform
              ? dispatch(dev, s.dbuf, nullptr, nullptr, l0, l0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos)
              : dispatch(dev, s.dbuf, s.doff, s.dlen, 0, 0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos);
@@ -294,6 +355,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     s.i0 = i;
     s.nb = nb;
     s.busy = true;
+    moved += pos;
     i = j;
     chunks++;
   }
@@ -301,6 +363,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     int r = retire(s);
     if (rc == HC_OK) rc = r;
   }
+  t_host_bytes = moved;
   return rc;
 }
 

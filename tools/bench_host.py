@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Secondary benchmarks (DESIGN.md numbers; bench.py is the headline):
+
+  --mode host8k   1M x 8 KiB blocks resident in HOST memory, CRC'd through
+                  hc_crc32_blocks: pinned staging / direct DMA, H2D + kernel +
+                  D2H of the CRC words overlapped on side streams.  The
+                  PCIe-inclusive rate BASELINE.json asks for.
+  --mode config5  WAL replay (BASELINE config 5): 10M records 64 B..64 KiB
+                  (log-uniform), framed into 4 KiB WAL blocks exactly as
+                  lsm/wal/wal.go:177-283 (tools/walgen.c), image in host memory,
+                  every block verified (hc_verify_blocks = recoverMemtable's
+                  CheckBlockIntegrity, wal.go:383) through the streamed pipeline.
+  --mode config5b GetCRC over each variable-length record, device-resident
+                  (hc_dev_crc32_blocks with HC_F_MESSAGES).
+
+--mem pinned|pageable chooses where the host image lives (pinned = as if the
+segment files were read into hipHostMalloc'd buffers).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import numpy as np  # noqa: E402
+
+
+def host_array(nbytes, mem):
+    import torch
+    if mem == "pinned":
+        t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        return t.numpy(), t
+    a = np.empty(nbytes, dtype=np.uint8)
+    return a, a
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["host8k", "config5", "config5b"], default="host8k")
+    ap.add_argument("--mem", choices=["pinned", "pageable"], default="pinned")
+    ap.add_argument("--records", type=int, default=10_000_000)
+    ap.add_argument("--blocks", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--check", type=int, default=1, help="spot-check results against a CPU CRC")
+    args = ap.parse_args()
+
+    import torch
+    from hunddb_amd import crc
+    torch.cuda.set_device(0)
+    res = {"mode": args.mode, "mem": args.mem}
+
+    if args.mode == "host8k":
+        B, n = 8192, args.blocks
+        host, keep = host_array(n * B, args.mem)
+        dev = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+        crc.dev_fill_blocks(dev, 0x48756E64, stride=B, ulen=B, nblocks=n)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        host[:] = dev.cpu().numpy()
+        res["fill_s"] = time.perf_counter() - t
+        want = torch.empty(n, dtype=torch.int32, device="cuda")
+        crc.dev_crc32_blocks(dev, want, stride=B, ulen=B, nblocks=n)
+        torch.cuda.synchronize()
+        want = want.cpu().numpy().view(np.uint32)
+        del dev
+        crc.crc32_blocks(host, stride=B, ulen=B, nblocks=min(n, 1000))  # warm the pipeline
+        times = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            got = crc.crc32_blocks(host, stride=B, ulen=B, nblocks=n)
+            times.append(time.perf_counter() - t)
+        assert np.array_equal(got, want), "host-path CRCs differ from the device-resident path"
+        bytes_ = n * B
+    elif args.mode == "config5":
+        import walgen
+        t = time.perf_counter()
+        plan = walgen.WalPlan(0x57414C, nrec=args.records)
+        res["plan_s"] = time.perf_counter() - t
+        nb = plan.nblocks
+        host, keep = host_array(nb * 4096, args.mem)
+        t = time.perf_counter()
+        step = 1 << 18
+        for b0 in range(0, nb, step):
+            plan.render(b0, min(nb, b0 + step), out=host[b0 * 4096:min(nb, b0 + step) * 4096], threads=args.threads)
+        res["render_s"] = time.perf_counter() - t
+        res.update(records=args.records, blocks=nb, refused=plan.refused,
+                   blocks_per_record=round(nb / args.records, 3), image_gib=round(nb * 4096 / 2**30, 2))
+        if args.check:  # every rendered block carries a valid CRC (host CPU, sampled)
+            idx = np.random.default_rng(1).choice(nb, 2000, replace=False)
+            for b in idx:
+                assert crc.CheckBlockIntegrity(host[b * 4096:(b + 1) * 4096]) is None
+        crc.verify_blocks(host, stride=4096, ulen=4096, nblocks=min(nb, 1000))  # warm
+        times = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            err, bm, fb = crc.verify_blocks(host, stride=4096, ulen=4096, nblocks=nb)
+            times.append(time.perf_counter() - t)
+            assert err is None and fb == -1, (err, fb)
+        # a corrupted fragment is found (TestWAL_CorruptionDetection, asserted)
+        victim = nb // 2
+        host[victim * 4096 + 4 + 17 + 10] ^= 1
+        err, bm, fb = crc.verify_blocks(host, stride=4096, ulen=4096, nblocks=nb)
+        host[victim * 4096 + 4 + 17 + 10] ^= 1
+        assert str(err) == "CRC mismatch in block" and fb == victim
+        bytes_ = nb * 4096
+    else:  # config5b: per-record GetCRC, device-resident
+        import walgen
+        sizes = walgen.WalPlan(0x57414C, nrec=1).sizes  # noqa: F841 (lib init)
+        sizes = np.zeros(args.records, dtype=np.uint32)
+        walgen.lib().wg_record_sizes(0x57414C, args.records, 64, 65536, sizes.ctypes.data)
+        off = np.zeros(args.records, dtype=np.uint64)
+        off[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+        total = int(off[-1]) + int(sizes[-1])
+        buf = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        doff = torch.from_numpy(off.view(np.int64)).cuda()
+        dlen = torch.from_numpy(sizes.view(np.int32)).cuda()
+        crc.dev_fill_blocks(buf, 0x57414C, off=doff, lens=dlen, nblocks=args.records)
+        out = torch.empty(args.records, dtype=torch.int32, device="cuda")
+        kw = dict(off=doff, lens=dlen, nblocks=args.records, flags=crc.HC_F_MESSAGES)
+        crc.dev_crc32_blocks(buf, out, **kw)
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(args.steps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            crc.dev_crc32_blocks(buf, out, **kw)
+            e.record()
+            torch.cuda.synchronize()
+            times.append(s.elapsed_time(e) / 1e3)
+        if args.check:
+            got = out.cpu().numpy().view(np.uint32)
+            idx = np.random.default_rng(2).choice(args.records, 2000, replace=False)
+            hb = buf.cpu().numpy()
+            for i in idx:
+                assert got[i] == crc.GetCRC(hb[int(off[i]):int(off[i]) + int(sizes[i])])
+        res.update(records=args.records, mean_record_bytes=round(total / args.records, 1))
+        res["launch"] = crc.last_launch()
+        bytes_ = total
+    best = min(times)
+    res.update(bytes=bytes_, seconds=[round(x, 4) for x in times], gib_s=round(bytes_ / best / 2**30, 2),
+               gb_s=round(bytes_ / best / 1e9, 2), pcie_gen5_x16_frac=round(bytes_ / best / 63e9, 3)
+               if args.mode != "config5b" else None)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
