@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc", choices=["auto", "on", "off"], default="auto",
                     help="collect FETCH_SIZE/WRITE_SIZE in rocprofv3 child runs (N=1 only)")
+    ap.add_argument("--settle", type=float, default=0.5, help="untimed clock-settle seconds before warmup")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--json-out", default="")
     return ap.parse_args()
@@ -197,6 +198,14 @@ def main():
     def step():
         crc.dev_crc32_blocks(buf, out, stream=stream, **kw)
 
+    # Clock settle (untimed): memory-bound launches of ~1 ms right after the fill
+    # run below the sustained clock; issue launches for >= args.settle seconds
+    # before the W warmup steps (MI355X_MICROARCH.md "DVFS give-back").
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

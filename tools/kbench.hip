@@ -56,6 +56,19 @@ struct Variant {
 };
 
 template <class Cfg>
+Variant arrays_variant(const char *name, const uint64_t *doff, const uint32_t *dlen) {
+  Variant v;
+  v.name = name;
+  v.check = !Cfg::kNull;
+  v.run = [doff, dlen](const hc::Batch &b, int cus, hipStream_t s) {
+    hipLaunchKernelGGL((hc::k_crc_fast<false, Cfg>), dim3(cus), dim3(Cfg::kWaves * 64), 0, s, b.base, doff,
+                       dlen, b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables);
+  };
+  return v;
+}
+
+template <class Cfg>
 Variant fast_variant(const char *name, int grid_mult = 1) {
   Variant v;
   v.name = name;
@@ -98,6 +111,17 @@ int main(int argc, char **argv) {
   CK(hipStreamCreate(&s));
   CK(hc::launch_fill(buf, nullptr, nullptr, B, B, N, 0x48756E64, cus * 16, s));
 
+  uint64_t *doff;
+  uint32_t *dlen;
+  CK(hipMalloc(&doff, N * 8));
+  CK(hipMalloc(&dlen, N * 4));
+  {
+    std::vector<uint64_t> ho(N);
+    std::vector<uint32_t> hl(N, B);
+    for (uint64_t i = 0; i < N; i++) ho[i] = i * B;
+    CK(hipMemcpy(doff, ho.data(), N * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dlen, hl.data(), N * 4, hipMemcpyHostToDevice));
+  }
   hc::Batch b{};
   b.base = buf;
   b.stride = B;
@@ -107,21 +131,14 @@ int main(int argc, char **argv) {
 
   using namespace hc;
   std::vector<Variant> vs;
-  vs.push_back(fast_variant<FastCfg<16, 8, 1, 0>>("w16 r8 nt contig (ref)"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 0, 0>>("w16 r8 plain contig"));
-  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 6, 1, 0>>("w16 r6 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 10, 1, 0>>("w16 r10 nt"));
-  vs.push_back(fast_variant<FastCfg<12, 8, 1, 0>>("w12 r8 nt"));
-  vs.push_back(fast_variant<FastCfg<8, 8, 1, 0>>("w8 r8 nt"));
-  vs.push_back(fast_variant<FastCfg<8, 16, 1, 0>>("w8 r16 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 2, 0>>("w16 r8 buf nt"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 3, 0>>("w16 r8 buf sc0|nt"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 4, 0>>("w16 r8 buf sc1|nt"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 5, 0>>("w16 r8 buf sc0|sc1|nt"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt (prod)"));
+  vs.push_back(arrays_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt, off/len arrays path", doff, dlen));
+  vs.push_back(fast_variant<FastCfg<16, 3, 1, 0>>("w16 r3 nt"));
+  vs.push_back(fast_variant<FastCfg<16, 5, 1, 0>>("w16 r5 nt"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1>>("w16 r4 nt inter"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 4, 0>>("w16 r4 buf sc1|nt"));
+  vs.push_back(fast_variant<FastCfg<12, 4, 1, 0>>("w12 r4 nt"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 0, true>>("NULL w16 r4 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 1, 0, true>>("NULL w16 r8 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 8, 4, 0, true>>("NULL w16 r8 buf sc1|nt"));
   for (int pol = 0; pol < 2; pol++) {
     Variant v;
     v.name = pol ? "REF grid-stride read nt, 8x256/CU" : "REF grid-stride read, 8x256/CU";
