@@ -191,70 +191,119 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
   const uint64_t b0 = kInterleave ? gw : uni64(nblocks * gw / W);
   const uint64_t b1 = kInterleave ? nblocks : uni64(nblocks * (gw + 1) / W);
 
-  // Advance a cursor to the first block >= from that this kernel handles.
-  auto seek = [&](uint64_t from, uint64_t &blk, const uint8_t *&ptr, uint32_t &rows) -> bool {
-    if (kUniform) {
-      if (from >= b1) return false;
-      blk = from;
-      ptr = base + from * stride;
-      rows = ulen >> 10;
-      return true;
-    }
-    for (uint64_t i = from; i < b1; i++) {
-      const uint64_t o = offs ? sload_u64(offs + i) : i * stride;
-      const uint32_t l = lens ? sload_u32(lens + i) : ulen;
-      if ((((uintptr_t)base + o) & 15u) == 0 && (l & 1023u) == 0 && l != 0) {
-        blk = i;
-        ptr = base + o;
-        rows = l >> 10;
-        return true;
+  const uint64_t step = kInterleave ? W : 1;
+  auto conform = [&](uint64_t o, uint32_t l) {
+    return kUniform || ((((uintptr_t)base + o) & 15u) == 0 && (l & 1023u) == 0 && l != 0);
+  };
+
+  // ---- producer ------------------------------------------------------------
+  // Cursor over this wave's blocks (b0, b0+step, ... < b1) and the rows of the
+  // current one.  With off/len arrays the NEXT block's metadata is fetched by
+  // vector loads while the current block's rows stream, so the wait for it
+  // (a counted vmcnt) finds it long arrived; only skipping a non-conforming
+  // block falls back to blocking scalar loads.
+  uint64_t pb = 0;
+  const uint8_t *pptr = nullptr;
+  uint32_t prow = 0, prows = 0;
+  bool pvalid = false;
+  uint64_t qb = ~0ull;  // block whose metadata is in flight
+  uint64_t qo = 0;      // (vector-load results)
+  uint32_t ql = 0;
+  auto meta_issue = [&](uint64_t i) {
+    qb = i;
+    if constexpr (!kUniform) {
+      if (i < b1) {
+        qo = offs ? offs[i] : i * stride;
+        ql = lens ? lens[i] : ulen;
       }
     }
-    return false;
   };
-  constexpr uint64_t kStep = 1;
-  const uint64_t step = kInterleave ? W : kStep;
-
-  uint64_t pb = 0, cb = 0;
-  const uint8_t *pptr = nullptr, *cptr = nullptr;
-  uint32_t prow = 0, prows = 0, crow = 0, crows = 0;
-  if (!seek(b0, cb, cptr, crows)) return;
-  pb = cb;
-  pptr = cptr;
-  prows = crows;
-
-  // Producer: issue the load of the next row, then advance (clamped at the
-  // wave's last row so every issued load is in bounds).
-  auto load_next = [&]() -> uint4 {
-    const uint4 v = load_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, lane);
-    if (++prow == prows) {
-      uint64_t nb;
-      const uint8_t *np;
-      uint32_t nr;
-      if (seek(pb + step, nb, np, nr)) {
-        pb = nb;
-        pptr = np;
-        prows = nr;
+  auto start_from = [&](uint64_t i) {
+    if constexpr (kUniform) {  // loop-free: keeps hipcc's vmcnt counting exact
+      pvalid = i < b1;
+      if (pvalid) {
+        pb = i;
+        pptr = base + i * stride;
+        prows = ulen >> 10;
         prow = 0;
+      }
+      return;
+    }
+    for (; i < b1; i += step) {
+      uint64_t o;
+      uint32_t l;
+      if (kUniform) {
+        o = i * stride;
+        l = ulen;
+      } else if (i == qb) {
+        o = uni64(qo);
+        l = uni(ql);
       } else {
-        prow = prows - 1;
+        o = offs ? sload_u64(offs + i) : i * stride;
+        l = lens ? sload_u32(lens + i) : ulen;
+      }
+      if (conform(o, l)) {
+        pb = i;
+        pptr = base + o;
+        prows = l >> 10;
+        prow = 0;
+        pvalid = true;
+        meta_issue(i + step);
+        return;
+      }
+    }
+    pvalid = false;
+  };
+
+  // Each ring slot carries the wave-uniform tag of the row it holds, so the
+  // consumer never touches block metadata.
+  struct Tag {
+    uint64_t blk;
+    const uint8_t *ptr;
+    uint32_t row, rows;
+    bool valid;
+  };
+  // The load is unconditional (past the wave's last row it re-reads that row,
+  // tagged invalid) so hipcc's wait counting stays exact: vmcnt(kRing-1).
+  auto load_next = [&](Tag &t) -> uint4 {
+    const uint4 v = load_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, lane);
+    t.valid = pvalid;
+    t.blk = pb;
+    t.ptr = pptr;
+    t.row = prow;
+    t.rows = prows;
+    if (pvalid && ++prow == prows) {
+      const uint64_t lb = pb;
+      const uint8_t *lp = pptr;
+      const uint32_t lr = prows;
+      start_from(pb + step);
+      if (!pvalid) {  // park on the last row
+        pb = lb;
+        pptr = lp;
+        prows = lr;
+        prow = lr - 1;
       }
     }
     return v;
   };
 
+  start_from(b0);
+  if (!pvalid) return;
   uint4 ring[kRing];
+  Tag tag[kRing];
 #pragma unroll
-  for (int u = 0; u < kRing; u++) ring[u] = load_next();
+  for (int u = 0; u < kRing; u++) ring[u] = load_next(tag[u]);
 
+  // ---- consumer --------------------------------------------------------------
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
   for (;;) {
 #pragma unroll
     for (int u = 0; u < kRing; u++) {
       // consume slot u, then refill it (same registers: no copies, kRing-1
       // rows stay in flight while this one is hashed)
+      const Tag t = tag[u];
       uint4 v = ring[u];
-      if (crow == 0) {
+      if (t.row == 0) {
         if (lane == 0) {
           stored = v.x;
           v.x = msg ? (v.x ^ 0xFFFFFFFFu) : w0;
@@ -269,8 +318,8 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
         c2 = row_step(c2, v.z);
         c3 = row_step(c3, v.w);
       }
-      ring[u] = load_next();
-      if (++crow == crows) {
+      ring[u] = load_next(tag[u]);
+      if (t.row + 1 == t.rows) {
         uint32_t crc;
         if constexpr (Cfg::kNull) {
           crc = wave_xor(c0 ^ c1 ^ c2 ^ c3);
@@ -279,8 +328,9 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
           crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
         }
         if (lane == 0) {
+          const uint64_t cb = t.blk;
           if (crc_out) crc_out[cb] = crc;
-          if (flags & kFlagStamp) *const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(cptr)) = crc;
+          if (flags & kFlagStamp) *const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(t.ptr)) = crc;
           if (first_bad && stored != crc) {
             if (bad_bitmap)
               __hip_atomic_fetch_or(&bad_bitmap[cb >> 5], 1u << (cb & 31), __ATOMIC_RELAXED,
@@ -289,8 +339,7 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
                                    __HIP_MEMORY_SCOPE_AGENT);
           }
         }
-        if (!seek(cb + step, cb, cptr, crows)) return;
-        crow = 0;
+        if (!tag[(u + 1) % kRing].valid) return;  // the wave's last block is done
       }
     }
   }
