@@ -48,20 +48,6 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Scalar (s_load) reads of wave-uniform metadata.  hipcc keeps these as
-// vector loads (it cannot prove the arrays are unclobbered), and the
-// s_waitcnt vmcnt(0) such a load needs would drain the row-load ring.
-__device__ __forceinline__ uint64_t sload_u64(const uint64_t *p) {
-  uint64_t v;
-  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ uint32_t sload_u32(const uint32_t *p) {
-  uint32_t v;
-  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
-  return v;
-}
-
 __device__ __forceinline__ void block_meta(const Batch &b, uint64_t i, uint64_t &o, uint32_t &l) {
   o = b.off ? b.off[i] : i * b.stride;
   l = b.len ? b.len[i] : b.ulen;
@@ -198,25 +184,24 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 
   // ---- producer ------------------------------------------------------------
   // Cursor over this wave's blocks (b0, b0+step, ... < b1) and the rows of the
-  // current one.  With off/len arrays the NEXT block's metadata is fetched by
-  // vector loads while the current block's rows stream, so the wait for it
-  // (a counted vmcnt) finds it long arrived; only skipping a non-conforming
-  // block falls back to blocking scalar loads.
+  // current one.
   uint64_t pb = 0;
   const uint8_t *pptr = nullptr;
   uint32_t prow = 0, prows = 0;
   bool pvalid = false;
-  uint64_t qb = ~0ull;  // block whose metadata is in flight
-  uint64_t qo = 0;      // (vector-load results)
+  // Metadata (off/len arrays only) is read through the constant address
+  // space so hipcc emits scalar s_loads, counted by lgkmcnt -- never by the
+  // vmcnt of the row ring.  The next block's entry is fetched when the
+  // current one starts, so its latency hides behind the current block's rows.
+  typedef const __attribute__((address_space(4))) uint64_t *c64p;
+  typedef const __attribute__((address_space(4))) uint32_t *c32p;
+  const c64p coffs = (c64p)offs;
+  const c32p clens = (c32p)lens;
+  uint64_t qb = ~0ull, qo = 0;  // prefetched entry (block qb)
   uint32_t ql = 0;
-  auto meta_issue = [&](uint64_t i) {
-    qb = i;
-    if constexpr (!kUniform) {
-      if (i < b1) {
-        qo = offs ? offs[i] : i * stride;
-        ql = lens ? lens[i] : ulen;
-      }
-    }
+  auto meta = [&](uint64_t i, uint64_t &o, uint32_t &l) {
+    o = coffs ? coffs[i] : i * stride;
+    l = clens ? clens[i] : ulen;
   };
   auto start_from = [&](uint64_t i) {
     if constexpr (kUniform) {  // loop-free: keeps hipcc's vmcnt counting exact
@@ -232,15 +217,11 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     for (; i < b1; i += step) {
       uint64_t o;
       uint32_t l;
-      if (kUniform) {
-        o = i * stride;
-        l = ulen;
-      } else if (i == qb) {
-        o = uni64(qo);
-        l = uni(ql);
+      if (i == qb) {
+        o = qo;
+        l = ql;
       } else {
-        o = offs ? sload_u64(offs + i) : i * stride;
-        l = lens ? sload_u32(lens + i) : ulen;
+        meta(i, o, l);
       }
       if (conform(o, l)) {
         pb = i;
@@ -248,7 +229,8 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
         prows = l >> 10;
         prow = 0;
         pvalid = true;
-        meta_issue(i + step);
+        qb = i + step;
+        if (qb < b1) meta(qb, qo, ql);
         return;
       }
     }
