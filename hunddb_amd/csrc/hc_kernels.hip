@@ -200,7 +200,11 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
   auto meta = [&](uint64_t i, uint64_t &o, uint32_t &l) {
     if (wbase == ~0ull || (i - wbase) / step >= 64) {
       wbase = i;
-      const uint64_t j = i + (uint64_t)lane * step;
+      // opaque copy of i: the window address is computed afresh, never
+      // strength-reduced across the inlined call sites
+      uint64_t iw = i;
+      asm volatile("" : "+s"(iw));
+      const uint64_t j = iw + (uint64_t)lane * step;
       const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
       wo_lo = (uint32_t)oj;
       wo_hi = (uint32_t)(oj >> 32);
