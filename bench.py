@@ -158,10 +158,18 @@ def main():
 
     from hunddb_amd import crc, shard
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(1, ndev)  # (rehearsal: ranks may share a GPU)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        # RCCL (backend "nccl") over xGMI; HC_DIST_BACKEND=gloo rehearses the
+        # N>1 path with several ranks sharing one GPU.
+        backend = os.environ.get("HC_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     nblk, bsize, scaling = WORKLOADS[args.workload]
     if args.blocks:

@@ -123,7 +123,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
   b.tables = d.dtab;
   if (n == 0) return HC_OK;
   const int fast_grid = d.cus;  // one 1024-thread, 144 KiB-LDS workgroup per CU
-  int gen_grid = (int)std::min<uint64_t>((n + kGenWaves - 1) / kGenWaves, (uint64_t)d.cus * 8);
+  const int gen_grid = d.cus;  // k_crc_any: same geometry as the streaming kernel
   hc_launch_info info{"k_crc_fast", 0, 0, bytes_hint, (uint32_t)fast_grid, kFastThreads,
                       kFastLdsBytes};
   hipError_t e = hipSuccess;
@@ -135,16 +135,13 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       info.fast_blocks = n;
     } else {
       e = launch_general(b, false, gen_grid, s);
-      info.kernel = "k_crc_general";
+      info.kernel = "k_crc_any";
       info.general_blocks = n;
-      info.grid = gen_grid;
-      info.block_threads = kGenThreads;
-      info.lds_bytes = 8192;
     }
   } else {
     e = launch_fast(b, false, fast_grid, s);
     if (e == hipSuccess) e = launch_general(b, true, gen_grid, s);
-    info.kernel = "k_crc_fast+k_crc_general";
+    info.kernel = "k_crc_fast+k_crc_any";
     info.fast_blocks = n;  // routing is decided on the device per block
   }
   t_last = info;

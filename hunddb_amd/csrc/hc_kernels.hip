@@ -19,9 +19,9 @@
 //   * Go's init value is the virtual prefix word W0 with shift(W0,4)=~0: in
 //     block mode it replaces the stored CRC word (bytes 0..3), which the CRC
 //     must not cover anyway.
-// General kernel (k_crc_general): any alignment and length (incl. < 4 bytes),
+// General kernel (k_crc_any): any alignment and length (incl. < 4 bytes),
 // same row decomposition with the message right-aligned to rows by virtual
-// leading zeros; unaligned bytes are assembled from in-range dword loads.
+// leading zeros; each lane funnel-shifts two aligned 16-B chunks.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -46,15 +46,6 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ void block_meta(const Batch &b, uint64_t i, uint64_t &o, uint32_t &l) {
-  o = b.off ? b.off[i] : i * b.stride;
-  l = b.len ? b.len[i] : b.ulen;
-}
-
-__device__ __forceinline__ bool fast_ok(const Batch &b, uint64_t o, uint32_t l) {
-  return (((uintptr_t)b.base + o) & 15u) == 0 && (l & 1023u) == 0 && l != 0;
 }
 
 // 32x32 GF(2) mat-vec: XOR of col[i] over the set bits i of d.
@@ -328,113 +319,187 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 }
 
 // ---------------------------------------------------------------------------
-// General kernel: one wave per block, any alignment/length.
-__device__ __forceinline__ uint32_t load_dw_if(const uint8_t *p, bool ok) {
-  return ok ? *reinterpret_cast<const uint32_t *>(p) : 0u;
+// General kernel (k_crc_any): any alignment, any length (incl. < 4 bytes),
+// block or whole-message mode.  One wave per block, 16 waves per CU, the same
+// replicated LDS tables and per-lane Horner streams as the streaming kernel.
+//
+// The message M = payload (block mode: bytes [4, len); message mode: all) is
+// processed as the virtual message  zeros(z) || W0 || M  of `rows` 1 KiB
+// rows (raw() ignores leading zeros; W0 is Go's init).  Row r, lane l covers
+// payload offsets s_r + 16l .. +15 with s_r = 1024r - z - 4.  Every row has
+// the same misalignment m = (P - z - 4) mod 16, so each lane loads the two
+// aligned 16-B chunks around its window (the second one is the neighbour's
+// first: an L1 hit) and funnel-shifts them by m.  Chunks that do not overlap
+// [P, P+Lp) are not loaded (no byte outside the block is touched); bytes at
+// negative offsets are replaced by zeros / W0.
+//
+// only_nonfast: the wave fetches the metadata of 64 blocks with one
+// coalesced load, ballots which of them the streaming kernel skipped, and
+// processes only those (so a batch the streaming kernel fully covered costs
+// one metadata sweep, not a per-block scan).
+__device__ __forceinline__ uint32_t byte_window(const uint32_t (&d)[8], uint32_t q, uint32_t rb, int k) {
+  // bytes [4(q+k)+rb, +4) of the 32-byte concatenation d[0..7]
+  switch (q) {
+    case 0: return __builtin_amdgcn_alignbyte(d[k + 1], d[k], rb);
+    case 1: return __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], rb);
+    case 2: return __builtin_amdgcn_alignbyte(d[k + 3], d[k + 2], rb);
+    default: return __builtin_amdgcn_alignbyte(d[k + 4], d[k + 3], rb);
+  }
 }
 
-__global__ __launch_bounds__(kGenThreads) void k_crc_general(Batch bt, int only_nonfast) {
-  __shared__ uint32_t tgl[1024];
-  __shared__ uint32_t s4l[1024];
+template <int kBatch>
+__global__ __launch_bounds__(kFastThreads) void k_crc_any(
+    const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+    uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, int only_nonfast,
+    uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
+    unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  for (uint32_t i = tid; i < 1024; i += kGenThreads) {
-    tgl[i] = (&bt.tables->tg[0][0])[i];
-    s4l[i] = (&bt.tables->s4[0][0])[i];
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
   }
   uint32_t col[32];
 #pragma unroll
-  for (int i = 0; i < 32; i++) col[i] = bt.tables->lane[lane][i];
-  const uint32_t w0 = bt.tables->w0;
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  const uint32_t w0 = tables->w0;
   __syncthreads();
 
-  auto tshift = [&](const uint32_t *t, uint32_t c) -> uint32_t {
-    return t[c & 255u] ^ t[256 + ((c >> 8) & 255u)] ^ t[512 + ((c >> 16) & 255u)] ^
-           t[768 + (c >> 24)];
+  const uint32_t r4 = (lane & 31u) << 2;
+  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
+  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  const bool msg = (flags & kFlagMessages) != 0;
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
+    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
+    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
+    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
+    return xor3(xor3(t0, t1, t2), t3, w);
   };
-  const bool msg = (bt.flags & kFlagMessages) != 0;
-  const uint64_t W = (uint64_t)gridDim.x * kGenWaves;
-  for (uint64_t blk = (uint64_t)blockIdx.x * kGenWaves + uni(tid >> 6); blk < bt.nblocks;
-       blk += W) {
-    uint64_t o;
-    uint32_t l;
-    block_meta(bt, blk, o, l);
-    if (only_nonfast && fast_ok(bt, o, l)) continue;
-    const uint8_t *blkp = bt.base + o;
-    if (!msg && l < 4) {  // "invalid block data": no CRC, always bad
-      if (lane == 0) {
-        if (bt.crc_out) bt.crc_out[blk] = 0;
-        if (bt.first_bad) {
-          if (bt.bad_bitmap) atomicOr(&bt.bad_bitmap[blk >> 5], 1u << (blk & 31));
-          atomicMin(bt.first_bad, (unsigned long long)blk);
-        }
-      }
-      continue;
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
+    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
+    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
+    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+
+  const uint32_t wave = uni(tid >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
+  const uint64_t b0 = uni64(nblocks * gw / W), b1 = uni64(nblocks * (gw + 1) / W);
+
+  for (uint64_t g = b0; g < b1; g += 64) {
+    // metadata of blocks g .. g+63, one per lane (coalesced)
+    const uint64_t j = g + lane;
+    uint64_t oj = 0;
+    uint32_t lj = 0;
+    if (j < b1) {
+      oj = offs ? offs[j] : j * stride;
+      lj = lens ? lens[j] : ulen;
     }
-    const uint8_t *P = msg ? blkp : blkp + 4;  // payload
-    const int64_t Lp = msg ? (int64_t)l : (int64_t)l - 4;
-    const int64_t Lv = Lp + 4;  // W0 || payload
-    const uint32_t rows = (uint32_t)((Lv + kRowBytes - 1) / kRowBytes);
-    const int64_t z = (int64_t)rows * kRowBytes - Lv;
-    uint32_t c[4] = {0, 0, 0, 0};
-    for (uint32_t r = 0; r < rows; r++) {
-      // payload-relative offset of this lane's first byte
-      const int64_t s = (int64_t)r * kRowBytes + 16 * (int64_t)lane - z - 4;
-      const uintptr_t A = (uintptr_t)P + (uintptr_t)s;  // wraps harmlessly if s < 0
-      const uintptr_t Ab = A & ~(uintptr_t)3;
-      const uint32_t sh = (uint32_t)(A & 3u);
-      const uintptr_t lo = (uintptr_t)P, hi = (uintptr_t)P + (uintptr_t)Lp;
-      uint32_t d[5];
-#pragma unroll
-      for (int j = 0; j < 5; j++) {
-        const uintptr_t a = Ab + 4 * j;
-        // load only dwords overlapping [P, P+Lp); with s < 0 the wrap makes
-        // Ab huge or below lo, so test in signed payload-relative space.
-        const int64_t rel = s - (int64_t)sh + 4 * j;  // payload offset of dword start
-        const bool ok = rel + 4 > 0 && rel < Lp;
-        d[j] = load_dw_if(reinterpret_cast<const uint8_t *>(a), ok);
-        (void)lo;
-        (void)hi;
-      }
-      uint32_t w[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-      if (s < 0) {  // front of the virtual message: zeros, then W0, then data
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          uint32_t dm = 0, wv = 0;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int64_t ob = s + 4 * k + j;
-            if (ob >= 0) dm |= 0xFFu << (8 * j);
-            else if (ob >= -4) wv |= ((w0 >> (8 * (ob + 4))) & 0xFFu) << (8 * j);
+    const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & 1023u) == 0 && lj != 0;
+    uint64_t todo = __ballot(j < b1 && !(only_nonfast && fast));
+    while (todo) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint64_t blk = g + k;
+      // scalar re-read of the selected block's entry (no ring here to protect)
+      typedef const __attribute__((address_space(4))) uint64_t *c64p;
+      typedef const __attribute__((address_space(4))) uint32_t *c32p;
+      const uint64_t o = offs ? ((c64p)offs)[blk] : blk * stride;
+      const uint32_t l = lens ? ((c32p)lens)[blk] : ulen;
+      const uint8_t *blkp = base + o;
+      if (!msg && l < 4) {  // "invalid block data": no CRC, always bad
+        if (lane == 0) {
+          if (crc_out) crc_out[blk] = 0;
+          if (first_bad) {
+            if (bad_bitmap) atomicOr(&bad_bitmap[blk >> 5], 1u << (blk & 31));
+            atomicMin(first_bad, (unsigned long long)blk);
           }
-          w[k] = (w[k] & dm) | wv;
+        }
+        continue;
+      }
+      const uintptr_t P = (uintptr_t)(msg ? blkp : blkp + 4);
+      const uint64_t Lp = msg ? l : l - 4;
+      const uint64_t Lv = Lp + 4;
+      const uint32_t rows = (uint32_t)((Lv + kRowBytes - 1) / kRowBytes);
+      const uint64_t z = (uint64_t)rows * kRowBytes - Lv;
+      const uintptr_t A0 = P - z - 4;
+      const uint32_t m = (uint32_t)(A0 & 15u), q = m >> 2, rb = m & 3u;
+      const uintptr_t Abase = A0 - m;
+      uint32_t c[4] = {0, 0, 0, 0};
+      for (uint32_t r0 = 0; r0 < rows; r0 += kBatch) {
+        uint4 ch0[kBatch], ch1[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; b++) {
+          ch0[b] = ch1[b] = make_uint4(0, 0, 0, 0);
+          if (r0 + b < rows) {
+            const uintptr_t X0 = Abase + (uintptr_t)(r0 + b) * kRowBytes + 16u * lane, X1 = X0 + 16;
+            if (X0 + 16 > P && X0 < P + Lp) ch0[b] = load_row<1>(reinterpret_cast<const uint8_t *>(X0), 0);
+            if (X1 + 16 > P && X1 < P + Lp) ch1[b] = load_row<1>(reinterpret_cast<const uint8_t *>(X1), 0);
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < kBatch; b++) {
+          if (r0 + b < rows) {
+            const uint32_t d[8] = {ch0[b].x, ch0[b].y, ch0[b].z, ch0[b].w,
+                                   ch1[b].x, ch1[b].y, ch1[b].z, ch1[b].w};
+            uint32_t w[4];
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) w[k2] = byte_window(d, q, rb, k2);
+            const int64_t srow = (int64_t)(r0 + b) * kRowBytes - (int64_t)z - 4;
+            if (srow < 0) {  // zeros, then W0, then data
+#pragma unroll
+              for (int k2 = 0; k2 < 4; k2++) {
+                uint32_t dm = 0, wv = 0;
+#pragma unroll
+                for (int jb = 0; jb < 4; jb++) {
+                  const int64_t ob = srow + 16 * (int64_t)lane + 4 * k2 + jb;
+                  if (ob >= 0) dm |= 0xFFu << (8 * jb);
+                  else if (ob >= -4) wv |= ((w0 >> (8 * (ob + 4))) & 0xFFu) << (8 * jb);
+                }
+                w[k2] = (w[k2] & dm) | wv;
+              }
+            }
+            if (r0 + b == 0) {
+#pragma unroll
+              for (int k2 = 0; k2 < 4; k2++) c[k2] = w[k2];
+            } else {
+#pragma unroll
+              for (int k2 = 0; k2 < 4; k2++) c[k2] = row_step(c[k2], w[k2]);
+            }
+          }
         }
       }
-#pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = (r == 0 ? 0u : tshift(tgl, c[k])) ^ w[k];
-    }
-    const uint32_t dd = tshift(s4l, tshift(s4l, tshift(s4l, c[0]) ^ c[1]) ^ c[2]) ^ c[3];
-    const uint32_t crc = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
-    const uint32_t stored = (!msg && lane == 0) ? *reinterpret_cast<const uint32_t *>(blkp) : 0u;
-    // the stored word of an unaligned block is read bytewise
-    uint32_t st = stored;
-    if (!msg && lane == 0 && (((uintptr_t)blkp) & 3u)) {
-      st = (uint32_t)blkp[0] | ((uint32_t)blkp[1] << 8) | ((uint32_t)blkp[2] << 16) |
-           ((uint32_t)blkp[3] << 24);
-    }
-    if (lane == 0) {
-      if (bt.crc_out) bt.crc_out[blk] = crc;
-      if (bt.flags & kFlagStamp) {
-        uint8_t *wp = const_cast<uint8_t *>(blkp);
-        wp[0] = (uint8_t)crc;
-        wp[1] = (uint8_t)(crc >> 8);
-        wp[2] = (uint8_t)(crc >> 16);
-        wp[3] = (uint8_t)(crc >> 24);
-      }
-      if (bt.first_bad && !msg && st != crc) {
-        if (bt.bad_bitmap) atomicOr(&bt.bad_bitmap[blk >> 5], 1u << (blk & 31));
-        atomicMin(bt.first_bad, (unsigned long long)blk);
+      const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+      const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      if (lane == 0) {
+        if (crc_out) crc_out[blk] = crcv;
+        if (!msg) {
+          uint32_t st = (uint32_t)blkp[0] | ((uint32_t)blkp[1] << 8) | ((uint32_t)blkp[2] << 16) |
+                        ((uint32_t)blkp[3] << 24);
+          if (flags & kFlagStamp) {
+            uint8_t *wp = const_cast<uint8_t *>(blkp);
+            wp[0] = (uint8_t)crcv;
+            wp[1] = (uint8_t)(crcv >> 8);
+            wp[2] = (uint8_t)(crcv >> 16);
+            wp[3] = (uint8_t)(crcv >> 24);
+          }
+          if (first_bad && st != crcv) {
+            if (bad_bitmap) atomicOr(&bad_bitmap[blk >> 5], 1u << (blk & 31));
+            atomicMin(first_bad, (unsigned long long)blk);
+          }
+        }
       }
     }
   }
@@ -499,7 +564,9 @@ hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t 
 }
 
 hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_crc_general, dim3(grid), dim3(kGenThreads), 0, s, b, only_nonfast ? 1 : 0);
+  hipLaunchKernelGGL((k_crc_any<4>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+                     b.ulen, b.flags, b.nblocks, only_nonfast ? 1 : 0, b.crc_out, b.bad_bitmap, b.first_bad,
+                     b.tables);
   return hipGetLastError();
 }
 

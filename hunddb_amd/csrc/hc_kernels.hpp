@@ -35,9 +35,6 @@ constexpr uint32_t kLdsMainBytes = 131072;  // 4 row-shift tables x 256 x 32 rep
 constexpr uint32_t kLdsS4Bytes = 16384;     // 4 x 256 x 4 replicas x 4 B
 constexpr uint32_t kFastLdsBytes = kLdsMainBytes + kLdsS4Bytes;
 
-// General kernel (any alignment / length), 4 waves per workgroup.
-constexpr int kGenWaves = 4;
-constexpr int kGenThreads = kGenWaves * 64;
 
 // Host launchers; return the hipError_t of the launch.
 // uniform_fast: the host proved every block satisfies the streaming kernel's

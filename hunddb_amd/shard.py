@@ -61,6 +61,8 @@ def job_timing(wall_s: float, kernel_s: float, local_bytes: float, device=None, 
 
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return wall_s, kernel_s, local_bytes
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"
     t = torch.tensor([wall_s, kernel_s], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     b = torch.tensor([local_bytes], dtype=torch.float64, device=device)
