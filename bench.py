@@ -38,6 +38,9 @@ WORKLOADS = {
     "config3": (1_000_000, "mixed", "weak"),
     "config4": (16_000_000, 8192, "strong"),
     "16k": (500_000, 16384, "weak"),
+    # f2: fused AddCRCsToData (k_frame): 1M output blocks = 4092 MB payload read
+    # from an unaligned address, 4096 MB framed blocks written
+    "frame": (1_000_000, "frame", "weak"),
 }
 
 
@@ -66,6 +69,7 @@ def pmc_traffic(args):
     if not exe:
         return None, "rocprofv3 not found"
     out = {}
+    kern = "k_frame" if WORKLOADS[args.workload][1] == "frame" else "k_crc_fast"
     tmp = tempfile.mkdtemp(prefix="hc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
              "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off"]
@@ -73,7 +77,7 @@ def pmc_traffic(args):
         child += ["--blocks", str(args.blocks)]
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(tmp, ctr)
-        cmd = [exe, "--pmc", ctr, "--kernel-include-regex", "k_crc_fast", "--output-format", "csv",
+        cmd = [exe, "--pmc", ctr, "--kernel-include-regex", kern, "--output-format", "csv",
                "-d", d, "-o", "run", "--"] + child
         try:
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=300,
@@ -87,7 +91,7 @@ def pmc_traffic(args):
         for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if "k_crc_fast" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    if kern in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
                         vals.append(float(row["Counter_Value"]))
         if not vals:
             return None, f"no {ctr} rows"
@@ -194,6 +198,15 @@ def main():
         kw = dict(off=doff, lens=dlen, nblocks=my)
         step_bytes = total
         block_desc = "mixed 4/8/16 KiB"
+    elif bsize == "frame":
+        npay = my * 4092 - 1000  # ragged last block
+        raw = torch.empty(npay + 1, dtype=torch.uint8, device=dev)
+        crc.dev_fill_blocks(raw, seed ^ rank, stride=npay + 1, ulen=npay + 1, nblocks=1)
+        buf = raw[1:]  # payload at an odd address
+        dst = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
+        kw = None
+        step_bytes = npay + my * 4096  # one read of the payload + one write of the blocks
+        block_desc = "AddCRCsToData: 4092-B payload slices -> 4096-B stamped blocks"
     else:
         buf = torch.empty(my * bsize, dtype=torch.uint8, device=dev)
         crc.dev_fill_blocks(buf, seed ^ rank, stride=bsize, ulen=bsize, nblocks=my)
@@ -204,7 +217,10 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        crc.dev_crc32_blocks(buf, out, stream=stream, **kw)
+        if kw is None:
+            crc.dev_add_crcs(buf, dst, crc_out=out, stream=stream)
+        else:
+            crc.dev_crc32_blocks(buf, out, stream=stream, **kw)
 
     # Clock settle (untimed): memory-bound launches of ~1 ms right after the fill
     # run below the sustained clock; issue launches for >= args.settle seconds
@@ -257,7 +273,7 @@ def main():
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and bsize != "mixed":
+        if world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "frame"):
             sample_blocks = min(my, (512 << 20) // bsize)
             host = buf[: sample_blocks * bsize].cpu().numpy()
             cpu = cpu_baseline(host, bsize, args.cpu_threads, args.cpu_seconds)

@@ -105,6 +105,7 @@ def _lib():
             "hc_dev_crc32_blocks": (I, [I, P, P, P, U64, U32, U64, P, P, P, U32, P]),
             "hc_dev_verify_prepare": (I, [I, P, P, U64, P]),
             "hc_dev_fill_blocks": (I, [I, P, P, P, U64, U32, U64, U64, P]),
+            "hc_dev_add_crcs": (I, [I, P, U64, P, P, P]),
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_device_count": (I, []),
@@ -316,6 +317,29 @@ def dev_fill_blocks(buf, seed, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOC
                                    seed & ((1 << 64) - 1), _stream_ptr(stream))
     if rc != HC_OK:
         raise HundCRCError(rc, "dev_fill_blocks")
+
+
+def dev_add_crcs(src, dst=None, crc_out=None, n=None, stream=None):
+    """Fused AddCRCsToData (crc_util.go:41-64) on device tensors: frame the first
+    `n` bytes of uint8 `src` (default: all) into stamped 4096-byte blocks at `dst`
+    (allocated when None).  Returns dst.  Asynchronous on `stream`."""
+    import torch
+    n = src.numel() if n is None else int(n)
+    out = hc_add_crcs_size_py(n)
+    if dst is None:
+        dst = torch.empty(out, dtype=torch.uint8, device=src.device)
+    if dst.numel() < out:
+        raise HundCRCError(HC_E_ARG, "dev_add_crcs: dst too small")
+    dev = src.device.index if src.device.index is not None else 0
+    rc = _lib().hc_dev_add_crcs(dev, src.data_ptr(), n, dst.data_ptr(), _tptr(crc_out), _stream_ptr(stream))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_add_crcs")
+    return dst
+
+
+def hc_add_crcs_size_py(n: int) -> int:
+    """Output size of AddCRCsToData: ceil(n/4092) * 4096 (crc_util.go:43-46)."""
+    return (n + BLOCK_SIZE - CRC_SIZE - 1) // (BLOCK_SIZE - CRC_SIZE) * BLOCK_SIZE
 
 
 def last_launch() -> dict:

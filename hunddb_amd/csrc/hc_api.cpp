@@ -568,6 +568,24 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
                   bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes);
 }
 
+int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t *crc_out, void *stream) {
+  if (n == 0) return HC_OK;  // Go returns an empty slice
+  if (!src || !dst) return HC_E_ARG;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15u) != 0) return HC_E_LAYOUT;
+  int st = init_device(device);
+  if (st != HC_OK) return st;
+  DeviceGuard g(device);
+  DeviceState &d = g_dev[device];
+  const uint64_t nblk = (n + kPayloadPerBlock - 1) / kPayloadPerBlock;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.cus, (nblk + kFastWaves - 1) / kFastWaves));
+  hc_launch_info info{"k_frame", nblk, 0, n + nblk * HC_BLOCK_SIZE, (uint32_t)grid, kFastThreads, kFastLdsBytes};
+  t_last = info;
+  return launch_frame(static_cast<const uint8_t *>(src), n, static_cast<uint8_t *>(dst), crc_out, d.dtab, grid,
+                      static_cast<hipStream_t>(stream)) == hipSuccess
+             ? HC_OK
+             : HC_E_HIP;
+}
+
 int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad, uint64_t nblocks,
                           void *stream) {
   int st = init_device(device);

@@ -337,13 +337,22 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 // coalesced load, ballots which of them the streaming kernel skipped, and
 // processes only those (so a batch the streaming kernel fully covered costs
 // one metadata sweep, not a per-block scan).
-__device__ __forceinline__ uint32_t byte_window(const uint32_t (&d)[8], uint32_t q, uint32_t rb, int k) {
-  // bytes [4(q+k)+rb, +4) of the 32-byte concatenation d[0..7]
+// 16 bytes starting at byte m = 4q + rb of the 32-byte pair (a, b): one
+// uniform switch per row, named registers only (no array -> no scratch).
+__device__ __forceinline__ uint4 funnel16(const uint4 a, const uint4 b, uint32_t q, uint32_t rb) {
   switch (q) {
-    case 0: return __builtin_amdgcn_alignbyte(d[k + 1], d[k], rb);
-    case 1: return __builtin_amdgcn_alignbyte(d[k + 2], d[k + 1], rb);
-    case 2: return __builtin_amdgcn_alignbyte(d[k + 3], d[k + 2], rb);
-    default: return __builtin_amdgcn_alignbyte(d[k + 4], d[k + 3], rb);
+    case 0:
+      return make_uint4(__builtin_amdgcn_alignbyte(a.y, a.x, rb), __builtin_amdgcn_alignbyte(a.z, a.y, rb),
+                        __builtin_amdgcn_alignbyte(a.w, a.z, rb), __builtin_amdgcn_alignbyte(b.x, a.w, rb));
+    case 1:
+      return make_uint4(__builtin_amdgcn_alignbyte(a.z, a.y, rb), __builtin_amdgcn_alignbyte(a.w, a.z, rb),
+                        __builtin_amdgcn_alignbyte(b.x, a.w, rb), __builtin_amdgcn_alignbyte(b.y, b.x, rb));
+    case 2:
+      return make_uint4(__builtin_amdgcn_alignbyte(a.w, a.z, rb), __builtin_amdgcn_alignbyte(b.x, a.w, rb),
+                        __builtin_amdgcn_alignbyte(b.y, b.x, rb), __builtin_amdgcn_alignbyte(b.z, b.y, rb));
+    default:
+      return make_uint4(__builtin_amdgcn_alignbyte(b.x, a.w, rb), __builtin_amdgcn_alignbyte(b.y, b.x, rb),
+                        __builtin_amdgcn_alignbyte(b.z, b.y, rb), __builtin_amdgcn_alignbyte(b.w, b.z, rb));
   }
 }
 
@@ -452,11 +461,8 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 #pragma unroll
         for (int b = 0; b < kBatch; b++) {
           if (r0 + b < rows) {
-            const uint32_t d[8] = {ch0[b].x, ch0[b].y, ch0[b].z, ch0[b].w,
-                                   ch1[b].x, ch1[b].y, ch1[b].z, ch1[b].w};
-            uint32_t w[4];
-#pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) w[k2] = byte_window(d, q, rb, k2);
+            const uint4 fw = funnel16(ch0[b], ch1[b], q, rb);
+            uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
             const int64_t srow = (int64_t)(r0 + b) * kRowBytes - (int64_t)z - 4;
             if (srow < 0) {  // zeros, then W0, then data
 #pragma unroll
@@ -501,6 +507,114 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
           }
         }
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused AddCRCsToData (/root/reference/utils/crc/crc_util.go:41-64): frame the
+// n-byte payload src into ceil(n/4092) zero-padded 4096-byte blocks at dst and
+// stamp each block's CRC -- one read of src, one write of dst.  One wave per
+// output block (4 rows of 1 KiB): lane l of row r owns output bytes
+// 1024r+16l..+15 = payload bytes b*4092 - 4 + (1024r+16l) ..; they are
+// funnel-shifted out of two aligned source chunks (the block's source
+// misalignment is the same for its 4 rows), masked to the block's payload,
+// stored with one coalesced 16-B store per lane and hashed exactly like a
+// block of the streaming kernel (W0 in place of bytes 0..3).  Lane 0 keeps
+// its row-0 chunk and stores it last, with the CRC in bytes 0..3.
+__global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
+                                                         uint8_t *__restrict__ dst, uint64_t nblk,
+                                                         uint32_t *__restrict__ crc_out,
+                                                         const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
+  }
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+  const uint32_t r4 = (lane & 31u) << 2;
+  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
+  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
+    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
+    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
+    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
+    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
+    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
+    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
+  const uint32_t wave = uni(tid >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
+  const uint64_t b0 = uni64(nblk * gw / W), b1 = uni64(nblk * (gw + 1) / W);
+  for (uint64_t b = b0; b < b1; b++) {
+    const uintptr_t P = (uintptr_t)src + b * kPay;                         // payload start
+    const uint64_t len = (n - b * kPay) < kPay ? (n - b * kPay) : kPay;     // payload bytes
+    const uintptr_t S0 = P - 4;                                             // source of output byte 0
+    const uint32_t m = (uint32_t)(S0 & 15u), q = m >> 2, rb = m & 3u;
+    const uintptr_t Ab = S0 - m;
+    uint4 ch0[4], ch1[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uintptr_t X0 = Ab + (uintptr_t)r * kRowBytes + 16u * lane, X1 = X0 + 16;
+      ch0[r] = ch1[r] = make_uint4(0, 0, 0, 0);
+      if (X0 + 16 > P && X0 < P + len) ch0[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X0), 0);
+      if (X1 + 16 > P && X1 < P + len) ch1[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X1), 0);
+    }
+    uint32_t c[4] = {0, 0, 0, 0};
+    uint4 keep = make_uint4(0, 0, 0, 0);
+    uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint4 fw = funnel16(ch0[r], ch1[r], q, rb);
+      uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
+      // keep output bytes t (= 1024r + 16l + 4k + j) with 4 <= t < 4 + len
+      const int32_t hi = 4 + (int32_t)len - (r * (int32_t)kRowBytes + 16 * (int32_t)lane);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t nb = hi - 4 * k;  // bytes of this word still inside the payload
+        uint32_t dm = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
+        if (r == 0 && k == 0) dm &= lane == 0 ? 0u : 0xFFFFFFFFu;  // bytes 0..3: the CRC field
+        w[k] &= dm;
+      }
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 outv = {w[0], w[1], w[2], w[3]};
+      if (r == 0 && lane == 0) {
+        keep = make_uint4(w[0], w[1], w[2], w[3]);  // stored last, with the CRC
+        w[0] = w0;                                  // Go's init in place of the CRC field
+      } else {
+        __builtin_nontemporal_store(outv, reinterpret_cast<u32x4 *>(ob + r * kRowBytes + 16 * lane));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : row_step(c[k], w[k]);
+    }
+    const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    if (lane == 0) {
+      keep.x = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
+      *reinterpret_cast<uint4 *>(ob) = keep;
+      if (crc_out) crc_out[b] = crcv;
     }
   }
 }
@@ -567,6 +681,14 @@ hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream
   hipLaunchKernelGGL((k_crc_any<4>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
                      b.ulen, b.flags, b.nblocks, only_nonfast ? 1 : 0, b.crc_out, b.bad_bitmap, b.first_bad,
                      b.tables);
+  return hipGetLastError();
+}
+
+hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
+                        const DeviceTables *tables, int grid, hipStream_t s) {
+  const uint64_t nblk = (n + 4091) / 4092;
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_frame, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, crc_out, tables);
   return hipGetLastError();
 }
 

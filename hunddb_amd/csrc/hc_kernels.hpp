@@ -42,6 +42,10 @@ constexpr uint32_t kFastLdsBytes = kLdsMainBytes + kLdsS4Bytes;
 hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s);
 // only_nonfast: process only blocks the streaming kernel skips.
 hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s);
+// Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B blocks.
+constexpr uint32_t HC_FRAME_BLOCK = 4096;
+hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
+                        const DeviceTables *tables, int grid, hipStream_t s);
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                        uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,

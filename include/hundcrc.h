@@ -119,6 +119,14 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
                         uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out,
                         uint32_t *bad_bitmap, int64_t *first_bad, uint32_t flags,
                         void *stream);
+/* Fused AddCRCsToData on device memory (utils/crc/crc_util.go:41-64): frame the
+ * n-byte payload src (any alignment) into ceil(n/4092) zero-padded 4096-byte
+ * blocks at dst (16-byte aligned, >= hc_add_crcs_size(n) bytes) and stamp each
+ * block's CRC in bytes 0..3; crc_out (optional) receives the per-block CRCs.
+ * One read of src and one write of dst (kernel k_frame).  HC_E_LAYOUT if dst
+ * is not 16-byte aligned.  n == 0 writes nothing (Go returns an empty slice). */
+int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t *crc_out,
+                    void *stream);
 /* Zero a device bitmap of ceil(n/32) words and set *first_bad = INT64_MAX. */
 int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad,
                           uint64_t nblocks, void *stream);

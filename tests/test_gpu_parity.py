@@ -298,3 +298,57 @@ def test_side_stream(cuda, hc, oracle):
     s.synchronize()
     host = buf.cpu().numpy()
     assert (u32(out) == oracle.crc32_blocks(host, stride=B, ulen=B, threads=16)).all()
+
+
+@pytest.mark.parametrize("shift", [0, 1, 3, 4, 7, 13])
+def test_dev_add_crcs_fused(cuda, hc, oracle, shift):
+    """Fused framing + CRC (k_frame) vs the oracle's AddCRCsToData (crc_util.go:41-64),
+    byte-exact, for ragged payload sizes around the 4092-byte boundary and
+    unaligned payload starts."""
+    torch = cuda
+    rng = np.random.default_rng(100 + shift)
+    for n in [1, 3, 4, 1019, 1020, 4091, 4092, 4093, 8184, 8185, 100_003, 4092 * 777 + 4090]:
+        host = rng.integers(0, 256, n + shift, dtype=np.uint8)
+        dsrc = torch.from_numpy(host).to("cuda")[shift:]
+        assert dsrc.data_ptr() % 16 == shift % 16
+        out_n = hc.lib().hc_add_crcs_size(n)
+        dst = torch.full((out_n + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        crcs = torch.empty(out_n // 4096, dtype=torch.int32, device="cuda")
+        hc.dev_add_crcs(dsrc, dst, crc_out=crcs, n=n)
+        torch.cuda.synchronize()
+        assert hc.last_launch()["kernel"] == "k_frame"
+        got = dst.cpu().numpy()
+        want = np.zeros(out_n, dtype=np.uint8)
+        src = host[shift:].tobytes()
+        assert oracle.lib().oc_add_crcs_to_data(src, n, want.ctypes.data) == out_n
+        assert got[:out_n].tobytes() == want.tobytes(), n
+        assert (got[out_n:] == 0xA5).all(), "wrote past the framed output"
+        assert (u32(crcs) == want.view(np.uint32)[::1024]).all()
+
+
+def test_dev_add_crcs_large_properties(cuda, hc, oracle):
+    """256 MiB payload: the framed output's blocks verify clean, the payload
+    round-trips (SizeWithoutCRCs direction), and the CRC words match the
+    streaming kernel's CRCs of the same blocks."""
+    torch = cuda
+    n = 256 * 2**20 + 12345
+    src = torch.empty(n + 3, dtype=torch.uint8, device="cuda")
+    hc.dev_fill_blocks(src, 9, stride=n + 3, ulen=n + 3, nblocks=1)
+    src = src[3:]
+    dst = hc.dev_add_crcs(src)
+    nb = dst.numel() // 4096
+    crc_frame = torch.empty(nb, dtype=torch.int32, device="cuda")
+    hc.dev_add_crcs(src, dst, crc_out=crc_frame)
+    crc_stream = dev_crc(torch, hc, dst, nb, stride=4096, ulen=4096)
+    assert (u32(crc_frame) == crc_stream).all()
+    assert (dst.view(nb, 4096)[:, :4].contiguous().view(torch.int32).view(-1).cpu().numpy().view(np.uint32)
+            == crc_stream).all()
+    payload = dst.view(nb, 4096)[:, 4:].reshape(-1)
+    assert torch.equal(payload[:n], src)
+    assert int(payload[n:].count_nonzero()) == 0
+    # spot-check a few blocks against the oracle's CRC
+    idx = [0, 1, nb // 2, nb - 1]
+    blocks = dst.view(nb, 4096)[idx].cpu().numpy()
+    assert (oracle.crc32_blocks(blocks) == crc_stream[idx]).all()
+    with pytest.raises(hc.HundCRCError):
+        hc.dev_add_crcs(src[:5000], torch.empty(8192 + 16, dtype=torch.uint8, device="cuda")[1:])
