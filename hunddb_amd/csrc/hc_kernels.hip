@@ -564,14 +564,32 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
     return xor3(xor3(t0, t1, t2), t3, w);
   };
   constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
   const uint32_t wave = uni(tid >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
   const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
   const uint64_t b0 = uni64(nblk * gw / W), b1 = uni64(nblk * (gw + 1) / W);
-  for (uint64_t b = b0; b < b1; b++) {
-    const uintptr_t P = (uintptr_t)src + b * kPay;                         // payload start
-    const uint64_t len = (n - b * kPay) < kPay ? (n - b * kPay) : kPay;     // payload bytes
-    const uintptr_t S0 = P - 4;                                             // source of output byte 0
+
+  // CRC of one framed block from its 4 rows (lane 0's row-0 word 0 = W0) and the
+  // store of lane 0's first 16 bytes with the CRC in front.
+  auto finish = [&](uint64_t b, const uint32_t (&c)[4], uint4 keep) {
+    const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    if (lane == 0) {
+      keep.x = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
+      *reinterpret_cast<uint4 *>(dst + b * (uint64_t)HC_FRAME_BLOCK) = keep;
+      if (crc_out) crc_out[b] = crcv;
+    }
+  };
+
+  // Edge blocks (the first, whose row 0 would start 4 bytes before src, and the
+  // last, whose payload may end mid-row): aligned loads predicated on the
+  // payload range + funnel shift + byte masks -- never touches a byte outside src.
+  auto edge_block = [&](uint64_t b) {
+    const uintptr_t P = (uintptr_t)src + b * kPay;                      // payload start
+    const uint64_t len = (n - b * kPay) < kPay ? (n - b * kPay) : kPay;  // payload bytes
+    const uintptr_t S0 = P - 4;                                          // source of output byte 0
     const uint32_t m = (uint32_t)(S0 & 15u), q = m >> 2, rb = m & 3u;
     const uintptr_t Ab = S0 - m;
     uint4 ch0[4], ch1[4];
@@ -598,24 +616,66 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
         if (r == 0 && k == 0) dm &= lane == 0 ? 0u : 0xFFFFFFFFu;  // bytes 0..3: the CRC field
         w[k] &= dm;
       }
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       const u32x4 outv = {w[0], w[1], w[2], w[3]};
       if (r == 0 && lane == 0) {
-        keep = make_uint4(w[0], w[1], w[2], w[3]);  // stored last, with the CRC
-        w[0] = w0;                                  // Go's init in place of the CRC field
+        keep = make_uint4(w[0], w[1], w[2], w[3]);
+        w[0] = w0;  // Go's init in place of the CRC field
       } else {
         __builtin_nontemporal_store(outv, reinterpret_cast<u32x4 *>(ob + r * kRowBytes + 16 * lane));
       }
 #pragma unroll
       for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : row_step(c[k], w[k]);
     }
+    finish(b, c, keep);
+  };
+
+  if (b0 == 0 && b1 > 0) edge_block(0);
+  if (nblk > 1 && b0 < nblk && b1 == nblk) edge_block(nblk - 1);
+
+  // Interior blocks 1 .. nblk-2: every row window [S0 + 1024r + 16l, +16) lies
+  // inside src, so each lane reads its 16 output bytes with ONE unaligned
+  // 16-byte load (gfx950 runs in unaligned-access mode) -- no funnel, no
+  // masks -- and the next block's 4 rows are in flight while this one is hashed.
+  const uint64_t i0 = b0 > 1 ? b0 : 1, i1 = b1 < nblk - 1 ? b1 : nblk - 1;
+  if (i0 >= i1) return;
+  auto load4 = [&](uint64_t b, u32x4 (&v)[4]) {
+    const uint8_t *S = src + b * kPay - 4 + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * kRowBytes));
+  };
+  auto frame = [&](uint64_t b, const u32x4 (&cur)[4]) {
+    uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+    uint32_t c[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 v = cur[r];
+      // every lane stores (no divergent branch between the loads and their
+      // use); lane 0 writes zeros to bytes 0..3 and the CRC over them below
+      if (r == 0) v.x = lane == 0 ? 0u : v.x;
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+      if (r == 0) v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : row_step(c[k], w[k]);
+    }
     const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
     const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
     if (lane == 0) {
-      keep.x = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
-      *reinterpret_cast<uint4 *>(ob) = keep;
+      *reinterpret_cast<uint32_t *>(ob) = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
       if (crc_out) crc_out[b] = crcv;
     }
+  };
+  // two register sets, alternating roles (no copies that would wait on the
+  // prefetch); unconditional loads: past the end a wave re-reads its last block
+  u32x4 A[4], B[4];
+  load4(i0, A);
+  for (uint64_t b = i0; b < i1; b += 2) {
+    load4(b + 1 < i1 ? b + 1 : i1 - 1, B);
+    frame(b, A);
+    if (b + 1 >= i1) break;
+    load4(b + 2 < i1 ? b + 2 : i1 - 1, A);
+    frame(b + 1, B);
   }
 }
 
