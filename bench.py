@@ -41,6 +41,9 @@ WORKLOADS = {
     # f2: fused AddCRCsToData (k_frame): 1M output blocks = 4092 MB payload read
     # from an unaligned address, 4096 MB framed blocks written
     "frame": (1_000_000, "frame", "weak"),
+    # f1: batched ReadFromDisk (k_unframe): verify 1M x 4 KiB blocks and strip
+    # the CRC words (4096 MB read, 4092 MB payload written)
+    "unframe": (1_000_000, "unframe", "weak"),
 }
 
 
@@ -69,7 +72,7 @@ def pmc_traffic(args):
     if not exe:
         return None, "rocprofv3 not found"
     out = {}
-    kern = "k_frame" if WORKLOADS[args.workload][1] == "frame" else "k_crc_fast"
+    kern = {"frame": "k_frame", "unframe": "k_unframe"}.get(WORKLOADS[args.workload][1], "k_crc_fast")
     tmp = tempfile.mkdtemp(prefix="hc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
              "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off"]
@@ -207,6 +210,17 @@ def main():
         kw = None
         step_bytes = npay + my * 4096  # one read of the payload + one write of the blocks
         block_desc = "AddCRCsToData: 4092-B payload slices -> 4096-B stamped blocks"
+    elif bsize == "unframe":
+        buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
+        crc.dev_fill_blocks(buf, seed ^ rank, stride=4096, ulen=4096, nblocks=my)
+        crc.dev_crc32_blocks(buf, None, stride=4096, ulen=4096, nblocks=my, flags=crc.HC_F_STAMP)
+        dst = torch.empty(my * 4092, dtype=torch.uint8, device=dev)
+        bitmap = torch.empty((my + 31) // 32, dtype=torch.int32, device=dev)
+        first_bad = torch.empty(1, dtype=torch.int64, device=dev)
+        crc.dev_verify_prepare(bitmap, first_bad, my)
+        kw = "unframe"
+        step_bytes = my * 4096 + my * 4092  # one read of the blocks + one write of the payload
+        block_desc = "ReadFromDisk: verify 4096-B blocks + strip CRCs"
     else:
         buf = torch.empty(my * bsize, dtype=torch.uint8, device=dev)
         crc.dev_fill_blocks(buf, seed ^ rank, stride=bsize, ulen=bsize, nblocks=my)
@@ -219,6 +233,8 @@ def main():
     def step():
         if kw is None:
             crc.dev_add_crcs(buf, dst, crc_out=out, stream=stream)
+        elif kw == "unframe":
+            crc.dev_read_blocks(buf, 4096, out=dst, bad_bitmap=bitmap, first_bad=first_bad, stream=stream)
         else:
             crc.dev_crc32_blocks(buf, out, stream=stream, **kw)
 
@@ -273,7 +289,7 @@ def main():
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "frame"):
+        if world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "frame", "unframe"):
             sample_blocks = min(my, (512 << 20) // bsize)
             host = buf[: sample_blocks * bsize].cpu().numpy()
             cpu = cpu_baseline(host, bsize, args.cpu_threads, args.cpu_seconds)

@@ -41,6 +41,7 @@ HC_OK = 0
 HC_ERR_INVALID_BLOCK = 1
 HC_ERR_CRC_MISMATCH = 2
 HC_ERR_TOO_SHORT = 3
+HC_E_ARG, HC_E_HIP, HC_E_NODEV, HC_E_NOMEM, HC_E_LAYOUT = -1, -2, -3, -4, -5
 HC_F_STAMP = 1
 HC_F_MESSAGES = 2
 
@@ -106,6 +107,8 @@ def _lib():
             "hc_dev_verify_prepare": (I, [I, P, P, U64, P]),
             "hc_dev_fill_blocks": (I, [I, P, P, P, U64, U32, U64, U64, P]),
             "hc_dev_add_crcs": (I, [I, P, U64, P, P, P]),
+            "hc_read_from_disk": (I, [P, U64, U32, U64, U64, P, P, P]),
+            "hc_dev_read_blocks": (I, [I, P, U64, U32, P, P, P, P, P]),
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_device_count": (I, []),
@@ -206,6 +209,34 @@ def FixLastBlockCRC(data) -> Optional[CRCError]:
     """crc_util.go:106-122 — restamp the last complete 4096-byte block in place."""
     p, n, _k = _rw_ptr(data)
     return _err(_lib().hc_fix_last_block(p if n else None, n))
+
+
+def ReadFromDisk(blocks, block_size: int, start_offset: int, size: int):
+    """lsm/block_manager/block_manager.go:189-242 minus the file I/O (row f1).
+
+    `blocks`: the blocks from index start_offset // block_size on, as read (bytes
+    past its end read as zeros).  Every touched block is verified in one batch.
+    Returns (payload, final_offset, None) or (None, 0, CRCError) like the Go
+    method; `last_bad_block()` gives the failing block's relative index."""
+    global _LAST_BAD
+    p, n, _k = _ro_ptr(blocks)
+    out = ctypes.create_string_buffer(max(1, size))
+    fo, bad = ctypes.c_uint64(0), ctypes.c_int64(-1)
+    rc = _lib().hc_read_from_disk(p if n else None, n, block_size, start_offset, size, out,
+                                  ctypes.byref(fo), ctypes.byref(bad))
+    _LAST_BAD = bad.value
+    if rc < 0:
+        raise HundCRCError(rc, "ReadFromDisk")
+    if rc != HC_OK:
+        return None, 0, CRCError(rc)
+    return out.raw[:size], fo.value, None
+
+
+_LAST_BAD = -1
+
+
+def last_bad_block() -> int:
+    return _LAST_BAD
 
 
 # ---- batched, host-resident (GPU) ---------------------------------------------
@@ -335,6 +366,25 @@ def dev_add_crcs(src, dst=None, crc_out=None, n=None, stream=None):
     if rc != HC_OK:
         raise HundCRCError(rc, "dev_add_crcs")
     return dst
+
+
+def dev_read_blocks(blocks, block_size=BLOCK_SIZE, out=None, crc_out=None, bad_bitmap=None, first_bad=None,
+                    nblocks=None, stream=None):
+    """Batched ReadFromDisk on device tensors (k_unframe): verify every block of the
+    uint8 tensor `blocks` and write the payloads back to back into `out`
+    (allocated when None).  Prepare bad_bitmap/first_bad with dev_verify_prepare."""
+    import torch
+    nb = blocks.numel() // block_size if nblocks is None else int(nblocks)
+    if out is None:
+        out = torch.empty(nb * (block_size - CRC_SIZE), dtype=torch.uint8, device=blocks.device)
+    if out.numel() < nb * (block_size - CRC_SIZE):
+        raise HundCRCError(HC_E_ARG, "dev_read_blocks: out too small")
+    dev = blocks.device.index if blocks.device.index is not None else 0
+    rc = _lib().hc_dev_read_blocks(dev, blocks.data_ptr(), nb, block_size, out.data_ptr(), _tptr(crc_out),
+                                   _tptr(bad_bitmap), _tptr(first_bad), _stream_ptr(stream))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_read_blocks")
+    return out
 
 
 def hc_add_crcs_size_py(n: int) -> int:

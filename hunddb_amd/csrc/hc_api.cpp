@@ -568,6 +568,73 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
                   bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes);
 }
 
+int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                      uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block) {
+  if (bad_block) *bad_block = -1;
+  const uint64_t B = block_size;
+  if (B <= HC_CRC_SIZE || (size && !out) || (avail && !blocks)) return HC_E_ARG;
+  uint64_t boff = start_offset % B;
+  if (boff < HC_CRC_SIZE) boff = HC_CRC_SIZE;  // block_manager.go:198-201
+  // blocks touched by the loop at :207-235
+  const uint64_t first = B - boff;
+  const uint64_t k = size == 0 ? 0 : (size <= first ? 1 : 1 + (size - first + (B - 5)) / (B - 4));
+  // verify all k blocks in one batch (a9); the first failing block in order is
+  // the one the Go loop stops at
+  const uint64_t nfull = std::min<uint64_t>(k, avail / B);
+  int64_t bad = -1;
+  int code = HC_OK;
+  static const uint64_t gpu_min = (uint64_t)env_int("HC_READ_GPU_MIN_BLOCKS", 256);
+  if (nfull >= gpu_min || (force_gpu() && nfull > 0 && B <= 0xFFFFFFFFu)) {
+    std::vector<uint32_t> crc(nfull);
+    int rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nfull, crc.data(), 0);
+    if (rc != HC_OK) return rc;
+    for (uint64_t i = 0; i < nfull && bad < 0; i++) {
+      uint32_t stored;
+      std::memcpy(&stored, blocks + i * B, 4);
+      if (stored != crc[i]) bad = (int64_t)i;
+    }
+  } else {
+    for (uint64_t i = 0; i < nfull && bad < 0; i++) {
+      uint32_t stored;
+      std::memcpy(&stored, blocks + i * B, 4);
+      if (stored != hc::cpu_crc32_update(0, blocks + i * B + HC_CRC_SIZE, B - HC_CRC_SIZE)) bad = (int64_t)i;
+    }
+  }
+  std::vector<uint8_t> tailbuf;
+  if (bad < 0 && nfull < k) {
+    // blocks past `avail`: ReadBlock returns a zero-extended short read (:130-146)
+    tailbuf.assign(B, 0);
+    for (uint64_t i = nfull; i < k && bad < 0; i++) {
+      std::fill(tailbuf.begin(), tailbuf.end(), 0);
+      const uint64_t o = i * B;
+      if (o < avail) std::memcpy(tailbuf.data(), blocks + o, std::min<uint64_t>(B, avail - o));
+      uint32_t stored;
+      std::memcpy(&stored, tailbuf.data(), 4);
+      if (stored != hc::cpu_crc32_update(0, tailbuf.data() + HC_CRC_SIZE, B - HC_CRC_SIZE)) bad = (int64_t)i;
+    }
+  }
+  if (bad >= 0) {
+    code = HC_ERR_CRC_MISMATCH;
+    if (bad_block) *bad_block = bad;
+    return code;
+  }
+  // append blockData[blockOffset : blockOffset+bytesToRead] per block (:221-231)
+  uint64_t produced = 0, rem = size;
+  for (uint64_t i = 0; i < k; i++) {
+    const uint64_t take = std::min<uint64_t>(rem, B - boff);
+    const uint64_t o = i * B + boff;
+    // bytes past `avail` are zeros
+    const uint64_t have = o >= avail ? 0 : std::min<uint64_t>(take, avail - o);
+    if (have) std::memcpy(out + produced, blocks + o, have);
+    if (have < take) std::memset(out + produced + have, 0, take - have);
+    produced += take;
+    rem -= take;
+    boff = HC_CRC_SIZE;
+  }
+  if (final_offset) *final_offset = hc_size_after_crcs(hc_size_without_crcs(start_offset) + size);  // :237-239
+  return HC_OK;
+}
+
 int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t *crc_out, void *stream) {
   if (n == 0) return HC_OK;  // Go returns an empty slice
   if (!src || !dst) return HC_E_ARG;
@@ -582,6 +649,29 @@ int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t
   t_last = info;
   return launch_frame(static_cast<const uint8_t *>(src), n, static_cast<uint8_t *>(dst), crc_out, d.dtab, grid,
                       static_cast<hipStream_t>(stream)) == hipSuccess
+             ? HC_OK
+             : HC_E_HIP;
+}
+
+int hc_dev_read_blocks(int device, const void *blocks, uint64_t nblocks, uint32_t block_size, void *payload_out,
+                       uint32_t *crc_out, uint32_t *bad_bitmap, int64_t *first_bad, void *stream) {
+  if (nblocks == 0) return HC_OK;
+  if (!blocks || !payload_out || (bad_bitmap && !first_bad)) return HC_E_ARG;
+  uint32_t lg = 0;
+  while (lg < 3 && (HC_BLOCK_SIZE << lg) != block_size) lg++;
+  if (lg == 3 || (reinterpret_cast<uintptr_t>(blocks) & 15u) != 0) return HC_E_LAYOUT;
+  int st = init_device(device);
+  if (st != HC_OK) return st;
+  DeviceGuard g(device);
+  DeviceState &d = g_dev[device];
+  const int grid =
+      (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.cus, (nblocks + kFastWaves - 1) / kFastWaves));
+  hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4), (uint32_t)grid, kFastThreads,
+                      kFastLdsBytes};
+  t_last = info;
+  return launch_unframe(static_cast<const uint8_t *>(blocks), nblocks, lg, static_cast<uint8_t *>(payload_out),
+                        crc_out, bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), d.dtab, grid,
+                        static_cast<hipStream_t>(stream)) == hipSuccess
              ? HC_OK
              : HC_E_HIP;
 }

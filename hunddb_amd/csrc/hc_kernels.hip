@@ -680,6 +680,122 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 }
 
 // ---------------------------------------------------------------------------
+// Batched ReadFromDisk on device (lsm/block_manager/block_manager.go:203-235,
+// row f1): verify every block of a contiguous run (CheckBlockIntegrity,
+// crc_util.go:88-100) and strip the CRC words, writing the payloads back to
+// back (block b's block[4:B] at out + b*(B-4)) -- the inverse of k_frame, one
+// read of the blocks and one write of the payload.  B = 4096 << lg_groups.
+// A wave walks its blocks in 4 KiB groups (4 rows of 1 KiB), the next group's
+// rows in flight while the current one is hashed and stored.  Payload stores
+// are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
+// block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
+// overlapping lane 1's store with identical bytes.
+__global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
+                                                           uint32_t lg_groups, uint8_t *__restrict__ out,
+                                                           uint32_t *__restrict__ crc_out,
+                                                           uint32_t *__restrict__ bad_bitmap,
+                                                           unsigned long long *__restrict__ first_bad,
+                                                           const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
+  }
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+  const uint32_t r4 = (lane & 31u) << 2;
+  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
+  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
+    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
+    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
+    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
+    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
+    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
+    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  const uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
+  const uint32_t gmask = (1u << lg_groups) - 1u;
+  const uint32_t wave = uni(tid >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
+  const uint64_t b0 = uni64(nblk * gw / W), b1 = uni64(nblk * (gw + 1) / W);
+  if (b0 >= b1) return;
+  const uint64_t p0 = b0 << lg_groups, p1 = b1 << lg_groups;  // 4 KiB groups of this wave
+  auto load4 = [&](uint64_t p, u32x4 (&v)[4]) {
+    const uint8_t *S = blocks + p * HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
+  };
+  uint32_t c[4] = {0, 0, 0, 0};
+  uint32_t stored = 0;
+  auto group = [&](uint64_t p, const u32x4 (&cur)[4]) {
+    const uint64_t b = p >> lg_groups;
+    const uint32_t g = (uint32_t)p & gmask;
+    uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 v = cur[r];
+      if (r == 0 && g == 0) {
+        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v.x, 0x101, 0xF, 0xF, false);  // lane+1's x
+        stored = __builtin_amdgcn_readfirstlane(v.x);                   // LE32(block[0:4])
+        const u32x4 first = {v.y, v.z, v.w, nx};
+        const u32x4 sv = lane == 0 ? first : v;
+        __builtin_nontemporal_store(sv, reinterpret_cast<u32x4_u *>(ob + (lane == 0 ? 4 : 0)));
+        v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
+      } else {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(ob + r * kRowBytes));
+      }
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) c[k] = (r == 0 && g == 0) ? w[k] : row_step(c[k], w[k]);
+    }
+    if (g == gmask) {
+      const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+      const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      if (lane == 0) {
+        if (crc_out) crc_out[b] = crcv;
+        if (first_bad && crcv != stored) {
+          if (bad_bitmap) atomicOr(&bad_bitmap[b >> 5], 1u << (b & 31));
+          atomicMin(first_bad, (unsigned long long)b);
+        }
+      }
+    }
+  };
+  u32x4 A[4], Bv[4];
+  load4(p0, A);
+  for (uint64_t p = p0; p < p1; p += 2) {
+    load4(p + 1 < p1 ? p + 1 : p1 - 1, Bv);
+    group(p, A);
+    if (p + 1 >= p1) break;
+    load4(p + 2 < p1 ? p + 2 : p1 - 1, A);
+    group(p + 1, Bv);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic workload fill: 64-bit word w of block i = splitmix64(seed, i, w).
 __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t blk, uint64_t w) {
   uint64_t z = seed + ((blk << 21) + w) * 0x9E3779B97F4A7C15ull;
@@ -749,6 +865,15 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
   hipLaunchKernelGGL(k_frame, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, crc_out, tables);
+  return hipGetLastError();
+}
+
+hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_groups, uint8_t *out,
+                          uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
+                          const DeviceTables *tables, int grid, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unframe, dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, lg_groups, out, crc_out,
+                     bad_bitmap, first_bad, tables);
   return hipGetLastError();
 }
 

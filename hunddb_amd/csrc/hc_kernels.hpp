@@ -46,6 +46,11 @@ hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream
 constexpr uint32_t HC_FRAME_BLOCK = 4096;
 hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
                         const DeviceTables *tables, int grid, hipStream_t s);
+// Batched ReadFromDisk: verify nblk blocks of 4096 << lg_groups bytes at `blocks`
+// (16-B aligned) and write their payloads back to back at `out`.
+hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_groups, uint8_t *out,
+                          uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
+                          const DeviceTables *tables, int grid, hipStream_t s);
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                        uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,

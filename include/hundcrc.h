@@ -119,6 +119,18 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
                         uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out,
                         uint32_t *bad_bitmap, int64_t *first_bad, uint32_t flags,
                         void *stream);
+/* lsm/block_manager/block_manager.go:189-242 ReadFromDisk, minus the file I/O
+ * (row f1): `blocks` holds the blocks from index start_offset/block_size on, as
+ * the caller read them (`avail` bytes; past that a block reads as zeros, like
+ * readBlockFromDisk's short read).  Every block the loop touches is verified in
+ * ONE batch (GPU above HC_READ_GPU_MIN_BLOCKS = 256, host CPU below), then the
+ * payload bytes [blockOffset:] of each are copied to out (size bytes), and
+ * *final_offset = SizeAfterAddingCRCs(SizeWithoutCRCs(start_offset) + size).
+ * Returns HC_OK or HC_ERR_CRC_MISMATCH with *bad_block = the index (relative to
+ * `blocks`) of the first failing block -- the one the Go loop would stop at. */
+int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                      uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block);
+
 /* Fused AddCRCsToData on device memory (utils/crc/crc_util.go:41-64): frame the
  * n-byte payload src (any alignment) into ceil(n/4092) zero-padded 4096-byte
  * blocks at dst (16-byte aligned, >= hc_add_crcs_size(n) bytes) and stamp each
@@ -127,6 +139,17 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
  * is not 16-byte aligned.  n == 0 writes nothing (Go returns an empty slice). */
 int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t *crc_out,
                     void *stream);
+/* Batched ReadFromDisk on device memory (block_manager.go:203-235, row f1):
+ * verify nblocks blocks of block_size (4096, 8192 or 16384) bytes at `blocks`
+ * (16-byte aligned) like CheckBlockIntegrity, and write each block's payload
+ * block[4:] back to back at payload_out (nblocks * (block_size - 4) bytes).
+ * Verification outputs as in hc_dev_crc32_blocks (crc_out = computed CRCs;
+ * bad_bitmap/first_bad prepared by hc_dev_verify_prepare).  Kernel k_unframe:
+ * one read of the blocks, one write of the payload.  HC_E_LAYOUT for another
+ * block size or an unaligned `blocks`. */
+int hc_dev_read_blocks(int device, const void *blocks, uint64_t nblocks, uint32_t block_size,
+                       void *payload_out, uint32_t *crc_out, uint32_t *bad_bitmap, int64_t *first_bad,
+                       void *stream);
 /* Zero a device bitmap of ceil(n/32) words and set *first_bad = INT64_MAX. */
 int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad,
                           uint64_t nblocks, void *stream);

@@ -20,6 +20,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 
 #if defined(__x86_64__)
@@ -254,6 +255,45 @@ int oc_fix_last_block_crc(uint8_t *p, size_t n) {
   if (n < OC_BLOCK_SIZE) return OC_ERR_TOO_SHORT;
   size_t complete = n / OC_BLOCK_SIZE;
   oc_add_crc_to_block_data(p + (complete - 1) * OC_BLOCK_SIZE, OC_BLOCK_SIZE);
+  return OC_OK;
+}
+
+/* BlockManager.ReadFromDisk, lsm/block_manager/block_manager.go:189-242, over
+ * an in-memory image: `blocks` holds the blocks from index start_offset /
+ * block_size on; `avail` bytes of it exist, the rest reads as zeros (the
+ * short-read / EOF behaviour of readBlockFromDisk, :130-146).  Each touched
+ * block is checked with CheckBlockIntegrity over the whole block (:215) before
+ * its bytes are appended.  On error *bad_block = relative index of the block. */
+int oc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                      uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block) {
+  const uint64_t B = block_size;
+  uint64_t block_offset = start_offset % B;
+  if (block_offset < OC_CRC_SIZE) block_offset = OC_CRC_SIZE; /* :198-201 */
+  uint8_t *blk = (uint8_t *)malloc(B);
+  uint64_t cur = 0, remaining = size, produced = 0;
+  *bad_block = -1;
+  while (remaining > 0) {
+    /* ReadBlock: make([]byte, blockSize) + file.Read (zeros past EOF) */
+    memset(blk, 0, B);
+    const uint64_t o = cur * B;
+    if (o < avail) memcpy(blk, blocks + o, (avail - o) < B ? (avail - o) : B);
+    int rc = oc_check_block_integrity(blk, B); /* :215 */
+    if (rc != OC_OK) {
+      *bad_block = (int64_t)cur;
+      free(blk);
+      return rc;
+    }
+    uint64_t take = B - block_offset; /* :221-225 */
+    if (take > remaining) take = remaining;
+    memcpy(out + produced, blk + block_offset, take);
+    produced += take;
+    remaining -= take;
+    cur++;
+    block_offset = OC_CRC_SIZE;
+  }
+  free(blk);
+  /* :237-239 */
+  *final_offset = oc_size_after_adding_crcs(oc_size_without_crcs(start_offset) + size);
   return OC_OK;
 }
 

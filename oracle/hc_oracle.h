@@ -60,6 +60,13 @@ uint64_t oc_size_without_crcs(uint64_t n);                            /* :79-83 
 int oc_check_block_integrity(const uint8_t *p, size_t n);             /* :88-100 */
 int oc_fix_last_block_crc(uint8_t *p, size_t n);                      /* :106-122 */
 
+/* lsm/block_manager/block_manager.go:189-242 ReadFromDisk over an in-memory
+ * block image starting at block start_offset/block_size (avail bytes, zeros
+ * after); returns OC_OK or the CheckBlockIntegrity code, *bad_block = relative
+ * index of the failing block (-1 if none). */
+int oc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                      uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block);
+
 /* ---- batches ----------------------------------------------------------- */
 /* CRC of blk[4:len] for each block (what CheckBlockIntegrity computes), on
  * nthreads host threads using oc_crc32_go_amd64.  off==NULL => off=i*stride;

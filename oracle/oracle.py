@@ -39,6 +39,7 @@ def lib():
             ("oc_mixed_size", U32, [U64, U64]),
             ("oc_wal_frame", U64, [U64, P, U64, U32, P, U64, I, P, P]),
             ("oc_wal_record_size", U32, [U64, U64, U32, U32]),
+            ("oc_read_from_disk", I, [P, U64, U32, U64, U64, P, P, P]),
         ]:
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
@@ -112,3 +113,14 @@ def wal_frame(seed, rec_sizes, bs=4096, max_blocks=None, stamp=True):
     nb = L.oc_wal_frame(seed, _p(rs), len(rs), bs, _p(buf), max_blocks, 1 if stamp else 0,
                         ctypes.byref(st), ctypes.byref(nxt))
     return buf[: nb * bs], st, nxt.value
+
+
+def read_from_disk(blocks: bytes, block_size: int, start_offset: int, size: int):
+    """block_manager.go:189-242 over an in-memory image (see oc_read_from_disk):
+    returns (payload bytes or None, final offset, error code, bad block)."""
+    out = ctypes.create_string_buffer(max(1, size))
+    fo, bad = ctypes.c_uint64(0), ctypes.c_int64(0)
+    rc = lib().oc_read_from_disk(blocks, len(blocks), block_size, start_offset, size, out,
+                                 ctypes.byref(fo), ctypes.byref(bad))
+    return (out.raw[:size] if rc == 0 else None), fo.value, rc, bad.value
+

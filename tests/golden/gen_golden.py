@@ -79,6 +79,27 @@ def fix_last_block_crc(b):           # crc_util.go:106-122
     return None, b
 
 
+def read_from_disk(image, B, start, size):
+    """lsm/block_manager/block_manager.go:189-242 over an in-memory file image
+    (blocks from index start//B on; zeros past the end, as readBlockFromDisk's
+    short read leaves them).  Returns (payload, final_offset, err, bad_block)."""
+    off = start % B
+    if off < CRC_SIZE:                                  # :198-201
+        off = CRC_SIZE
+    out, cur, rem = bytearray(), 0, size
+    while rem > 0:
+        blk = bytes(image[cur * B:(cur + 1) * B]).ljust(B, b"\0")   # ReadBlock
+        err = check_block_integrity(blk)                # :215
+        if err is not None:
+            return None, 0, err, cur
+        take = min(rem, B - off)                        # :221-225
+        out += blk[off:off + take]
+        rem -= take
+        cur += 1
+        off = CRC_SIZE
+    return bytes(out), size_after_adding_crcs((size_without_crcs(start) + size) & M64), None, -1  # uint64 wrap
+
+
 # ---- synthetic inputs: splitmix64 finaliser over (seed, block, word) -----
 def splitmix64(seed, block, words):
     w = np.asarray(words, dtype=np.uint64)
@@ -274,6 +295,28 @@ def main():
         ms.append(s)
         mc.append(get_crc(b[4:]))
     g["mixed"] = {"seed": mseed, "n": 256, "sizes": ms, "crcs": mc}
+
+    # 5. ReadFromDisk (block_manager.go:189-242) over framed images (f1)
+    rrng = np.random.default_rng(0x52464431)
+    rfd, images = [], {}
+    for B in (4096, 8192):
+        nb = 5
+        image = bytearray()
+        for i in range(nb):
+            image += add_crc_to_block_data(rrng.integers(0, 256, B, dtype=np.uint8).tobytes())
+        bad = bytearray(image)
+        bad[3 * B + 1000] ^= 0x04                        # corrupt block 3
+        for name, img in (("clean", image), ("bad3", bad)):
+            for start, size in [(0, 0), (0, 1), (0, B - 4), (1, 10), (3, B), (4, B - 4), (5, B - 5),
+                                (B - 1, 2), (B, 1), (B + 2, 3 * B), (B + 7, 4 * (B - 4) - 3),
+                                (2 * B + 100, 5 * B)]:
+                got, fo, err, badblk = read_from_disk(img, B, start, size)
+                rfd.append({"block_size": B, "image": name, "start": start, "size": size,
+                            "sha256": None if got is None else sha(got), "final_offset": fo,
+                            "err": err, "bad_block": badblk})
+        images[str(B)] = bytes(image).hex()       # small enough to store (5 blocks)
+    g["read_from_disk"] = {"seed": 0x52464431, "blocks": 5, "flip": "image[3*B+1000] ^= 0x04",
+                           "cases": rfd, "image_hex": images}
 
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
     with open(path, "w") as f:

@@ -189,3 +189,43 @@ def test_batch_entries_fail_loudly_without_gpu(hc):
     # multi-hundred-block AddCRCsToData is a GPU batch too
     with pytest.raises(hc.HundCRCError):
         hc.AddCRCsToData(bytes(4092 * 300))
+
+
+def test_read_from_disk_host(hc, golden, oracle):
+    """hc_read_from_disk (row f1) on the host path: the golden ReadFromDisk cases,
+    then random (start, size) over a larger image with corruptions, vs the oracle."""
+    g = golden["read_from_disk"]
+    for c in g["cases"]:
+        B = c["block_size"]
+        img = bytearray.fromhex(g["image_hex"][str(B)])
+        if c["image"] == "bad3":
+            img[3 * B + 1000] ^= 0x04
+        got, fo, err = hc.ReadFromDisk(bytes(img), B, c["start"], c["size"])
+        assert (None if err is None else str(err)) == c["err"], c
+        if err is None:
+            assert hashlib.sha256(got).hexdigest() == c["sha256"] and fo == c["final_offset"]
+        else:
+            assert hc.last_bad_block() == c["bad_block"] and got is None and fo == 0
+    rng = np.random.default_rng(31)
+    for B in (4096, 8192, 16384, 1500):
+        nb = 40
+        img = bytearray()
+        for i in range(nb):
+            blk = bytearray(rng.integers(0, 256, B, dtype=np.uint8).tobytes())
+            hc.AddCRCToBlockData(blk)
+            img += blk
+        for trial in range(60):
+            start = int(rng.integers(0, 3 * B))
+            size = int(rng.integers(0, 45 * B))           # may run past the image (zero blocks)
+            view = bytes(img[(start // B) * B:])
+            if trial % 3 == 0:
+                v = bytearray(view)
+                v[int(rng.integers(0, len(v)))] ^= 0x80
+                view = bytes(v)
+            got, fo, err = hc.ReadFromDisk(view, B, start, size)
+            want, wfo, wrc, wbad = oracle.read_from_disk(view, B, start, size)
+            assert (0 if err is None else err.code) == wrc
+            if wrc == 0:
+                assert got == want and fo == wfo
+            else:
+                assert hc.last_bad_block() == wbad

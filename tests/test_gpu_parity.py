@@ -352,3 +352,103 @@ def test_dev_add_crcs_large_properties(cuda, hc, oracle):
     assert (oracle.crc32_blocks(blocks) == crc_stream[idx]).all()
     with pytest.raises(hc.HundCRCError):
         hc.dev_add_crcs(src[:5000], torch.empty(8192 + 16, dtype=torch.uint8, device="cuda")[1:])
+
+
+def _stamped_blocks(oracle, rng, n, B):
+    raw = rng.integers(0, 256, n * B, dtype=np.uint8)
+    crcs = oracle.crc32_blocks(raw, stride=B, ulen=B)
+    raw.view(np.uint32).reshape(n, B // 4)[:, 0] = crcs
+    return raw
+
+
+@pytest.mark.parametrize("B", [4096, 8192, 16384])
+def test_dev_read_blocks_parity(cuda, hc, oracle, B):
+    """k_unframe (batched ReadFromDisk, block_manager.go:203-235) vs the oracle:
+    payloads byte-exact, CRC words, and the corrupt blocks found."""
+    torch = cuda
+    rng = np.random.default_rng(B)
+    for n in [1, 2, 3, 17, 1000, 4099]:
+        host = _stamped_blocks(oracle, rng, n, B)
+        bad_idx = sorted(set(rng.integers(0, n, max(1, n // 300)).tolist())) if n > 2 else []
+        for i in bad_idx:
+            host[i * B + int(rng.integers(0, B))] ^= 1 << int(rng.integers(0, 8))
+        want_crc = oracle.crc32_blocks(host, stride=B, ulen=B)
+        stored = host.view(np.uint32).reshape(n, B // 4)[:, 0]
+        want_bad = np.nonzero(stored != want_crc)[0]
+        d = torch.from_numpy(host).to("cuda")
+        bitmap = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+        fb = torch.empty(1, dtype=torch.int64, device="cuda")
+        crcs = torch.empty(n, dtype=torch.int32, device="cuda")
+        hc.dev_verify_prepare(bitmap, fb, n)
+        out = torch.full((n * (B - 4) + 32,), 0x5A, dtype=torch.uint8, device="cuda")
+        hc.dev_read_blocks(d, B, out=out, crc_out=crcs, bad_bitmap=bitmap, first_bad=fb)
+        torch.cuda.synchronize()
+        assert hc.last_launch()["kernel"] == "k_unframe"
+        got = out.cpu().numpy()
+        assert got[: n * (B - 4)].tobytes() == host.reshape(n, B)[:, 4:].tobytes(), (n, B)
+        assert (got[n * (B - 4):] == 0x5A).all()
+        assert (u32(crcs) == want_crc).all()
+        bits = np.unpackbits(u32(bitmap).view(np.uint8), bitorder="little")[:n]
+        assert np.nonzero(bits)[0].tolist() == want_bad.tolist()
+        assert int(fb.item()) == (int(want_bad[0]) if len(want_bad) else 2**63 - 1)
+
+
+def test_frame_unframe_round_trip_full_size(cuda, hc):
+    """1M blocks: AddCRCsToData (k_frame) then batched ReadFromDisk (k_unframe)
+    gives back the payload, every block verifies, and the CRC words agree with
+    the streaming kernel's."""
+    torch = cuda
+    n_blk = 1_000_000
+    npay = n_blk * 4092 - 777
+    raw = torch.empty(npay + 5, dtype=torch.uint8, device="cuda")
+    hc.dev_fill_blocks(raw, 4242, stride=npay + 5, ulen=npay + 5, nblocks=1)
+    src = raw[5:]
+    framed = hc.dev_add_crcs(src)
+    assert framed.numel() == n_blk * 4096
+    bitmap = torch.empty((n_blk + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bitmap, fb, n_blk)
+    pay = hc.dev_read_blocks(framed, 4096, bad_bitmap=bitmap, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == 2**63 - 1 and int(bitmap.count_nonzero()) == 0
+    assert torch.equal(pay[:npay], src) and int(pay[npay:].count_nonzero()) == 0
+    # corrupt three blocks of the framed image: exactly those are reported
+    for i in (0, 123457, n_blk - 1):
+        framed[i * 4096 + 4000] ^= 1
+    hc.dev_verify_prepare(bitmap, fb, n_blk)
+    hc.dev_read_blocks(framed, 4096, out=pay, bad_bitmap=bitmap, first_bad=fb)
+    torch.cuda.synchronize()
+    bits = np.unpackbits(u32(bitmap).view(np.uint8), bitorder="little")[:n_blk]
+    assert np.nonzero(bits)[0].tolist() == [0, 123457, n_blk - 1] and int(fb.item()) == 0
+
+
+def test_dev_read_blocks_16k_full_size(cuda, hc):
+    torch = cuda
+    n, B = 500_000, 16384
+    buf = dev_uniform(torch, hc, 99, n, B)
+    hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, flags=hc.HC_F_STAMP)
+    bitmap = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bitmap, fb, n)
+    pay = hc.dev_read_blocks(buf, B, bad_bitmap=bitmap, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == 2**63 - 1
+    assert torch.equal(pay.view(n, B - 4), buf.view(n, B)[:, 4:])
+
+
+def test_read_from_disk_gpu_batch(cuda, hc, oracle, monkeypatch):
+    """hc_read_from_disk with >= 256 touched blocks verifies them in one GPU batch."""
+    rng = np.random.default_rng(77)
+    B = 4096
+    img = _stamped_blocks(oracle, rng, 3000, B)
+    for start, size, flip in [(5, 2000 * 4092, None), (4096 * 3 + 9, 2500 * 4092, 1700), (0, 3000 * 4092, 2999)]:
+        view = bytearray(img[(start // B) * B:].tobytes())
+        if flip is not None:
+            view[flip * B + 77] ^= 0x10
+        got, fo, err = hc.ReadFromDisk(bytes(view), B, start, size)
+        want, wfo, wrc, wbad = oracle.read_from_disk(bytes(view), B, start, size)
+        assert (0 if err is None else err.code) == wrc
+        if wrc == 0:
+            assert got == want and fo == wfo
+        else:
+            assert hc.last_bad_block() == wbad == flip

@@ -140,3 +140,21 @@ def test_global_key_dict_header(oracle, golden):
     blk = bytearray(4096)
     blk[4:12] = h["count"].to_bytes(8, "little")
     assert oracle.checksum(bytes(blk[4:])) == h["crc"]
+
+
+def test_read_from_disk(oracle, golden):
+    """oc_read_from_disk (block_manager.go:189-242) against the zlib-derived fixtures."""
+    g = golden["read_from_disk"]
+    for c in g["cases"]:
+        B = c["block_size"]
+        img = bytearray.fromhex(g["image_hex"][str(B)])
+        if c["image"] == "bad3":
+            img[3 * B + 1000] ^= 0x04
+        start_blk = 0  # fixtures index the image from block 0
+        got, fo, rc, bad = oracle.read_from_disk(bytes(img[start_blk * B:]), B, c["start"], c["size"])
+        want_rc = {None: 0, "CRC mismatch in block": 2}[c["err"]]
+        assert rc == want_rc, c
+        if rc == 0:
+            assert hashlib.sha256(got).hexdigest() == c["sha256"] and fo == c["final_offset"], c
+        else:
+            assert bad == c["bad_block"], c
