@@ -69,6 +69,48 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
          __builtin_amdgcn_readlane(v, 32) ^ __builtin_amdgcn_readlane(v, 48);
 }
 
+// Lane-0 side effects of a wave (CRC word, crc_out, verify atomics) issued with
+// exec = lane 0 inside one asm statement.  Written as plain `if (lane == 0)`
+// code these become branches around VMEM instructions, and the waitcnt pass
+// then assumes the fewest VMEM ops on every path: every wait on a row
+// prefetched before the branch turns conservative and also waits for the
+// previous block's payload stores.  The asm ops are invisible to that pass;
+// that is safe because an extra in-order VMEM op can only make a later
+// vmcnt(N) stricter, never looser, and these ops return no data.
+__device__ __forceinline__ void lane0_store_u32(uint32_t *p, uint32_t v) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "global_store_dword %1, %2, off\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv)
+      : "v"(p), "v"(v)
+      : "memory");
+}
+__device__ __forceinline__ void lane0_atomic_or(uint32_t *p, uint32_t v) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "global_atomic_or %1, %2, off\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv)
+      : "v"(p), "v"(v)
+      : "memory");
+}
+__device__ __forceinline__ void lane0_atomic_umin64(unsigned long long *p, uint64_t v) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "global_atomic_umin_x2 %1, %2, off\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv)
+      : "v"(p), "v"(v)
+      : "memory");
+}
+
 // ---------------------------------------------------------------------------
 // Streaming kernel.  Pointer arguments are separate __restrict__ kernel
 // arguments so the per-block metadata reads (off/len) become scalar s_loads
@@ -661,21 +703,25 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
     }
     const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
     const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
-    if (lane == 0) {
-      *reinterpret_cast<uint32_t *>(ob) = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
-      if (crc_out) crc_out[b] = crcv;
-    }
+    // binary.LittleEndian.PutUint32(block[:4], crc): lane 0's ob is the block start
+    lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);
+    if (crc_out) lane0_store_u32(crc_out + b, crcv);
   };
   // two register sets, alternating roles (no copies that would wait on the
   // prefetch); unconditional loads: past the end a wave re-reads its last block
+  // The first block is peeled so that the loop header is entered with the same
+  // VMEM sequence from both edges ([next rows loaded][4 row stores]); a
+  // mismatch there makes the waitcnt pass wait for the stores as well.
   u32x4 A[4], B[4];
   load4(i0, A);
-  for (uint64_t b = i0; b < i1; b += 2) {
-    load4(b + 1 < i1 ? b + 1 : i1 - 1, B);
-    frame(b, A);
+  load4(i0 + 1 < i1 ? i0 + 1 : i1 - 1, B);
+  frame(i0, A);
+  for (uint64_t b = i0 + 1; b < i1; b += 2) {
+    load4(b + 1 < i1 ? b + 1 : i1 - 1, A);
+    frame(b, B);
     if (b + 1 >= i1) break;
-    load4(b + 2 < i1 ? b + 2 : i1 - 1, A);
-    frame(b + 1, B);
+    load4(b + 2 < i1 ? b + 2 : i1 - 1, B);
+    frame(b + 1, A);
   }
 }
 
@@ -690,8 +736,9 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
 // block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
 // overlapping lane 1's store with identical bytes.
+template <uint32_t lg_groups>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
-                                                           uint32_t lg_groups, uint8_t *__restrict__ out,
+                                                           uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
                                                            uint32_t *__restrict__ bad_bitmap,
                                                            unsigned long long *__restrict__ first_bad,
@@ -775,23 +822,25 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
     if (g == gmask) {
       const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
       const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
-      if (lane == 0) {
-        if (crc_out) crc_out[b] = crcv;
-        if (first_bad && crcv != stored) {
-          if (bad_bitmap) atomicOr(&bad_bitmap[b >> 5], 1u << (b & 31));
-          atomicMin(first_bad, (unsigned long long)b);
-        }
+      if (crc_out) lane0_store_u32(crc_out + b, crcv);
+      if (first_bad && crcv != stored) {  // wave-uniform
+        if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+        lane0_atomic_umin64(first_bad, b);
       }
     }
   };
+  // first group peeled: both edges into the loop header carry the same VMEM
+  // sequence (see k_frame)
   u32x4 A[4], Bv[4];
   load4(p0, A);
-  for (uint64_t p = p0; p < p1; p += 2) {
-    load4(p + 1 < p1 ? p + 1 : p1 - 1, Bv);
-    group(p, A);
+  load4(p0 + 1 < p1 ? p0 + 1 : p1 - 1, Bv);
+  group(p0, A);
+  for (uint64_t p = p0 + 1; p < p1; p += 2) {
+    load4(p + 1 < p1 ? p + 1 : p1 - 1, A);
+    group(p, Bv);
     if (p + 1 >= p1) break;
-    load4(p + 2 < p1 ? p + 2 : p1 - 1, A);
-    group(p + 1, Bv);
+    load4(p + 2 < p1 ? p + 2 : p1 - 1, Bv);
+    group(p + 1, A);
   }
 }
 
@@ -872,8 +921,16 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
                           const DeviceTables *tables, int grid, hipStream_t s) {
   if (nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_unframe, dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, lg_groups, out, crc_out,
-                     bad_bitmap, first_bad, tables);
+#define HC_UNFRAME(L)                                                                                      \
+  hipLaunchKernelGGL((k_unframe<L>), dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, out, crc_out, bad_bitmap, \
+                     first_bad, tables)
+  if (lg_groups == 0)
+    HC_UNFRAME(0);
+  else if (lg_groups == 1)
+    HC_UNFRAME(1);
+  else
+    HC_UNFRAME(2);
+#undef HC_UNFRAME
   return hipGetLastError();
 }
 

@@ -109,3 +109,20 @@ func AddCRCToBlocks(data []byte, blockSize int) {
 	n := len(data) / blockSize
 	_ = goErr(C.hc_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize), C.uint64_t(n)))
 }
+
+// ReadVerified is BlockManager.ReadFromDisk (block_manager.go:189-242) minus
+// the file I/O: raw holds the blocks from startOffset/blockSize on, as read
+// (cache or disk).  Every touched block is verified in one batch, then the
+// payload bytes and the final physical offset are returned exactly as the Go
+// loop returns them; on a bad block it returns that block's error.
+func ReadVerified(raw []byte, blockSize uint16, startOffset, size uint64) ([]byte, uint64, error) {
+	out := make([]byte, size)
+	var final C.uint64_t
+	var bad C.int64_t
+	rc := C.hc_read_from_disk(ptr(raw), C.uint64_t(len(raw)), C.uint32_t(blockSize),
+		C.uint64_t(startOffset), C.uint64_t(size), ptr(out), &final, &bad)
+	if err := goErr(rc); err != nil {
+		return nil, 0, err
+	}
+	return out, uint64(final), nil
+}
