@@ -41,6 +41,8 @@ HC_OK = 0
 HC_ERR_INVALID_BLOCK = 1
 HC_ERR_CRC_MISMATCH = 2
 HC_ERR_TOO_SHORT = 3
+HC_ERR_WAL_FRAGMENT_TYPE = 4
+HC_ERR_WAL_TRUNCATED = 5
 HC_E_ARG, HC_E_HIP, HC_E_NODEV, HC_E_NOMEM, HC_E_LAYOUT = -1, -2, -3, -4, -5
 HC_F_STAMP = 1
 HC_F_MESSAGES = 2
@@ -109,6 +111,7 @@ def _lib():
             "hc_dev_add_crcs": (I, [I, P, U64, P, P, P]),
             "hc_read_from_disk": (I, [P, U64, U32, U64, U64, P, P, P]),
             "hc_dev_read_blocks": (I, [I, P, U64, U32, P, P, P, P, P]),
+            "hc_wal_replay": (I, [P, U64, U32, U64, U64, U64, P, U64, P, P, U64, P, P, P, P]),
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_device_count": (I, []),
@@ -237,6 +240,37 @@ _LAST_BAD = -1
 
 def last_bad_block() -> int:
     return _LAST_BAD
+
+
+def wal_replay(blocks, block_size: int = BLOCK_SIZE, start_block: int = 0, start_offset: int = CRC_SIZE,
+               max_records: int = 0, buf_cap=None, slots=None, as_arrays=False, out=None):
+    """WAL recovery (lsm/wal/wal.go:362-455, row f3): verify every written block in
+    one batch, then parse FULL records and reassemble fragments.
+
+    Returns (records, err, bad_block, (pos_block, pos_offset)): `records` is a
+    list of the serialized record bytes (what record.Deserialize receives),
+    `err` None or CRCError.  buf_cap/slots limit the output (resumable)."""
+    p, n, _k = _ro_ptr(blocks)
+    nb = n // block_size
+    cap = nb * block_size if buf_cap is None else int(buf_cap)
+    if slots is None:
+        slots = nb * ((block_size - CRC_SIZE) // 17 + 1)
+    buf = np.empty(max(1, cap), dtype=np.uint8) if out is None else out
+    cap = min(cap, buf.nbytes)
+    off = np.empty(max(1, slots), dtype=np.uint64)
+    ln = np.empty(max(1, slots), dtype=np.uint64)
+    cnt, pb, po, bad = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int64(-1)
+    rc = _lib().hc_wal_replay(p if n else None, nb, block_size, start_block, start_offset, max_records,
+                              buf.ctypes.data, cap, off.ctypes.data, ln.ctypes.data, slots,
+                              ctypes.byref(cnt), ctypes.byref(pb), ctypes.byref(po), ctypes.byref(bad))
+    if rc < 0:
+        raise HundCRCError(rc, "wal_replay")
+    if as_arrays:  # (record bytes back to back, offsets, lengths) without per-record copies
+        recs = (buf, off[:cnt.value], ln[:cnt.value])
+    else:
+        mv = memoryview(buf)
+        recs = [bytes(mv[int(off[i]):int(off[i]) + int(ln[i])]) for i in range(cnt.value)]
+    return recs, (None if rc == HC_OK else CRCError(rc)), bad.value, (pb.value, po.value)
 
 
 # ---- batched, host-resident (GPU) ---------------------------------------------

@@ -380,6 +380,8 @@ const char *hc_strerror(int code) {
     case HC_ERR_INVALID_BLOCK: return "invalid block data";
     case HC_ERR_CRC_MISMATCH: return "CRC mismatch in block";
     case HC_ERR_TOO_SHORT: return "data is too short to contain a complete block";
+    case HC_ERR_WAL_FRAGMENT_TYPE: return "unknown fragment type";
+    case HC_ERR_WAL_TRUNCATED: return "WAL fragment overruns its block";
     case HC_E_ARG: return "hundcrc: invalid argument";
     case HC_E_HIP: return "hundcrc: HIP runtime error";
     case HC_E_NODEV: return "hundcrc: no gfx950 device available (the GPU path never falls back to the CPU)";
@@ -633,6 +635,178 @@ int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size
   }
   if (final_offset) *final_offset = hc_size_after_crcs(hc_size_without_crcs(start_offset) + size);  // :237-239
   return HC_OK;
+}
+
+// ---- WAL recovery (row f3) ---------------------------------------------------
+namespace {
+// One parsed piece of a WAL block (wal_header.go:5-23 framing).
+struct WalItem {
+  enum Kind : uint8_t { kFull, kFrag, kLast, kClear, kErrType, kErrTrunc } kind;
+  uint64_t blk;
+  uint32_t hdr;  // offset of the piece's header in its block (or of the error)
+  uint32_t pay;  // payload offset
+  uint64_t len;  // payload length
+};
+
+// processBlockForRecovery (wal.go:412-453) for one block, as items.  Returns
+// false after an error item (the caller stops scanning).
+bool wal_scan_block(const uint8_t *b, uint32_t bs, uint64_t blk, uint64_t off, std::vector<WalItem> &out) {
+  // the rest of the block is padding iff off > last non-zero byte (:415-419)
+  int64_t last = (int64_t)bs - 1;
+  while (last >= 0 && b[last] == 0) last--;
+  while (off < bs) {
+    if ((int64_t)off > last) {
+      out.push_back({WalItem::kClear, blk, (uint32_t)off, 0, 0});
+      return true;
+    }
+    if (off + 17 > bs) {  // DeserializeWALHeader returns nil; Go then panics
+      out.push_back({WalItem::kErrTrunc, blk, (uint32_t)off, 0, 0});
+      return false;
+    }
+    uint64_t size;
+    std::memcpy(&size, b + off, 8);
+    const uint8_t type = b[off + 8];
+    const uint32_t hdr = (uint32_t)off;
+    off += 17;
+    if (size > bs - off) {  // block[offset:offset+size] out of range: Go panics
+      out.push_back({WalItem::kErrTrunc, blk, (uint32_t)off, 0, 0});
+      return false;
+    }
+    WalItem::Kind k;
+    if (type == 4) k = WalItem::kFull;                      // FRAGMENT_FULL
+    else if (type == 1 || type == 2) k = WalItem::kFrag;    // FIRST, MIDDLE
+    else if (type == 3) k = WalItem::kLast;                 // LAST
+    else {
+      out.push_back({WalItem::kErrType, blk, (uint32_t)(off + size), 0, 0});
+      return false;
+    }
+    out.push_back({k, blk, hdr, (uint32_t)off, size});
+    off += size;
+  }
+  return true;
+}
+}  // namespace
+
+int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, uint64_t start_block,
+                  uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t rec_buf_cap,
+                  uint64_t *rec_off, uint64_t *rec_len, uint64_t rec_slots, uint64_t *nrec, uint64_t *pos_block,
+                  uint64_t *pos_offset, int64_t *bad_block) {
+  if (!nrec || !pos_block || !pos_offset) return HC_E_ARG;
+  if (bad_block) *bad_block = -1;
+  *nrec = 0;
+  *pos_block = start_block;
+  *pos_offset = start_offset;
+  const uint64_t bs = block_size;
+  if (bs < 32 || (nblocks > start_block && !blocks) || start_offset < HC_CRC_SIZE) return HC_E_ARG;
+  if (start_block >= nblocks) return HC_OK;
+  const uint64_t n = nblocks - start_block;
+  const uint8_t *base = blocks + start_block * bs;
+  // 1. verify every block in one batch (wal.go:383), GPU from 256 blocks
+  int64_t first_bad = -1;
+  static const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", 256);
+  if (n >= gpu_min || force_gpu()) {
+    int rc = hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
+    if (rc < 0) return rc;
+  } else {
+    for (uint64_t i = 0; i < n && first_bad < 0; i++)
+      if (hc_check_block(base + i * bs, bs) != HC_OK) first_bad = (int64_t)i;
+  }
+  const uint64_t stop = first_bad >= 0 ? (uint64_t)first_bad : n;  // blocks that may be parsed
+  // 2. scan blocks into items, in parallel over contiguous block ranges
+  static const int threads_cfg = std::max(1, env_int("HC_COPY_THREADS", 8));
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, stop / 64));
+  std::vector<std::vector<WalItem>> items(T);
+  parallel_for(T, [&](int t) {
+    const uint64_t lo = stop * t / T, hi = stop * (t + 1) / T;
+    items[t].reserve((hi - lo) * 2 + 4);
+    for (uint64_t i = lo; i < hi; i++)
+      if (!wal_scan_block(base + i * bs, block_size, start_block + i, i == 0 ? start_offset : HC_CRC_SIZE,
+                          items[t]))
+        break;
+  });
+  // 3. sequential merge: fragment reassembly, memtable-full stop, capacity stop
+  struct Piece {
+    const uint8_t *p;
+    uint64_t len, dst;
+  };
+  std::vector<Piece> pieces, pending;
+  uint64_t used = 0, count = 0, pend_len = 0;
+  uint64_t pend_blk = 0, pend_hdr = 0;
+  int code = HC_OK;
+  bool done = false;
+  uint64_t pb = start_block + stop, po = HC_CRC_SIZE;  // position when everything parsed
+  auto emit = [&](const WalItem &it, uint64_t first_blk, uint64_t first_hdr) -> bool {
+    const uint64_t len = pend_len + it.len;
+    if (count >= rec_slots || used + len > rec_buf_cap || !rec_buf || !rec_off || !rec_len) {
+      pb = first_blk;  // resumable: the record starts at (first_blk, first_hdr)
+      po = first_hdr;
+      return false;
+    }
+    rec_off[count] = used;
+    rec_len[count] = len;
+    for (auto &q : pending) {
+      pieces.push_back({q.p, q.len, used});
+      used += q.len;
+    }
+    pieces.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, used});
+    used += it.len;
+    count++;
+    pending.clear();
+    pend_len = 0;
+    return true;
+  };
+  for (int t = 0; t < T && !done; t++) {
+    for (const WalItem &it : items[t]) {
+      if (it.kind == WalItem::kClear) {
+        pending.clear();
+        pend_len = 0;
+        continue;
+      }
+      if (it.kind == WalItem::kErrType || it.kind == WalItem::kErrTrunc) {
+        code = it.kind == WalItem::kErrType ? HC_ERR_WAL_FRAGMENT_TYPE : HC_ERR_WAL_TRUNCATED;
+        pb = it.blk;
+        po = it.hdr;
+        done = true;
+        break;
+      }
+      if (it.kind == WalItem::kFrag) {
+        if (pending.empty()) {
+          pend_blk = it.blk;
+          pend_hdr = it.hdr;
+        }
+        pending.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, 0});
+        pend_len += it.len;
+        continue;
+      }
+      const bool frag = it.kind == WalItem::kLast;
+      if (!emit(it, frag && !pending.empty() ? pend_blk : it.blk, frag && !pending.empty() ? pend_hdr : it.hdr)) {
+        done = true;  // out of caller capacity: HC_OK, position at this record
+        break;
+      }
+      if (max_records && count >= max_records) {  // memtable.IsFull: next block (wal.go:392-397)
+        pb = it.blk + 1;
+        po = HC_CRC_SIZE;
+        done = true;
+        break;
+      }
+    }
+  }
+  if (!done && first_bad >= 0) {
+    code = HC_ERR_CRC_MISMATCH;
+    if (bad_block) *bad_block = (int64_t)(start_block + first_bad);
+    pb = start_block + first_bad;
+    po = first_bad == 0 ? start_offset : HC_CRC_SIZE;
+  }
+  // 4. copy the record bytes, in parallel
+  const int C = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, used >> 22));
+  parallel_for(C, [&](int t) {
+    const uint64_t lo = pieces.size() * t / C, hi = pieces.size() * (t + 1) / C;
+    for (uint64_t i = lo; i < hi; i++) std::memcpy(rec_buf + pieces[i].dst, pieces[i].p, pieces[i].len);
+  });
+  *nrec = count;
+  *pos_block = pb;
+  *pos_offset = po;
+  return code;
 }
 
 int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t *crc_out, void *stream) {

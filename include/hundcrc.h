@@ -48,6 +48,8 @@ extern "C" {
 #define HC_ERR_INVALID_BLOCK 1 /* "invalid block data"                            crc_util.go:90  */
 #define HC_ERR_CRC_MISMATCH 2  /* "CRC mismatch in block"                         crc_util.go:96  */
 #define HC_ERR_TOO_SHORT 3     /* "data is too short to contain a complete block" crc_util.go:108 */
+#define HC_ERR_WAL_FRAGMENT_TYPE 4 /* "unknown fragment type"                     wal.go:451      */
+#define HC_ERR_WAL_TRUNCATED 5     /* a WAL header/payload runs past its block (Go panics there) */
 /* library errors */
 #define HC_E_ARG -1     /* invalid argument (null pointer, bad size, capacity too small) */
 #define HC_E_HIP -2     /* a HIP runtime call failed */
@@ -130,6 +132,24 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
  * `blocks`) of the first failing block -- the one the Go loop would stop at. */
 int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
                       uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block);
+
+/* WAL recovery (lsm/wal/wal.go:362-455 recoverMemtable + processBlockForRecovery,
+ * row f3) over nblocks written WAL blocks of block_size bytes (every log's
+ * written blocks back to back), starting at (start_block, start_offset).
+ * All blocks are verified in ONE batch (GPU from 256 blocks), then parsed:
+ * FULL payloads and reassembled FIRST/MIDDLE/LAST fragments are the records
+ * (the bytes record.Deserialize receives), copied back to back into rec_buf
+ * with rec_off/rec_len.  One call = one memtable: max_records plays
+ * memtable.IsFull (0 = never) and, as in Go, the next call starts at the
+ * NEXT block.  Returns HC_OK, HC_ERR_CRC_MISMATCH (*bad_block = absolute
+ * block index; the records before it are returned), HC_ERR_WAL_FRAGMENT_TYPE
+ * or HC_ERR_WAL_TRUNCATED.  If rec_buf_cap / rec_slots run out first, it
+ * returns HC_OK with *pos_* at the first record that did not fit (resume
+ * there); rec_buf of nblocks*block_size bytes always suffices. */
+int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, uint64_t start_block,
+                  uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t rec_buf_cap,
+                  uint64_t *rec_off, uint64_t *rec_len, uint64_t rec_slots, uint64_t *nrec, uint64_t *pos_block,
+                  uint64_t *pos_offset, int64_t *bad_block);
 
 /* Fused AddCRCsToData on device memory (utils/crc/crc_util.go:41-64): frame the
  * n-byte payload src (any alignment) into ceil(n/4092) zero-padded 4096-byte

@@ -198,6 +198,8 @@ const char *oc_strerror(int code) {
     case OC_ERR_INVALID_BLOCK: return "invalid block data";                           /* :90 */
     case OC_ERR_CRC_MISMATCH: return "CRC mismatch in block";                         /* :96 */
     case OC_ERR_TOO_SHORT: return "data is too short to contain a complete block";    /* :108 */
+    case OC_ERR_WAL_FRAGMENT_TYPE: return "unknown fragment type";                    /* wal.go:451 */
+    case OC_ERR_WAL_TRUNCATED: return "WAL fragment overruns its block";             /* Go panics */
     default: return "unknown error";
   }
 }
@@ -506,3 +508,80 @@ uint64_t oc_wal_frame(uint64_t seed, const uint32_t *rec_sizes, uint64_t nrec, u
   if (next_rec) *next_rec = r;
   return w.nblocks;
 }
+
+/* ------------------------------------------------------------------------ */
+/* WAL recovery, lsm/wal/wal.go:362-455 (recoverMemtable +                  */
+/* processBlockForRecovery) over a run of written blocks.  One call = one    */
+/* memtable: the fragment buffer is local (:365), max_records plays         */
+/* memtable.IsFull (0 = never full).  Records are the payload bytes          */
+/* record.Deserialize would receive, appended to rec_buf in order.          */
+int oc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t bs, uint64_t start_block,
+                  uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t *rec_off,
+                  uint64_t *rec_len, uint64_t *nrec, uint64_t *pos_block, uint64_t *pos_offset,
+                  int64_t *bad_block) {
+  uint8_t *frag = (uint8_t *)malloc((size_t)bs * (nblocks + 1));
+  uint64_t flen = 0, used = 0, n = 0;
+  uint64_t blk = start_block, off = start_offset;
+  int rc = OC_OK, full = 0;
+  *bad_block = -1;
+  for (; blk < nblocks && !full; blk++, off = OC_CRC_SIZE) { /* :370-396 */
+    const uint8_t *b = blocks + blk * (uint64_t)bs;
+    if (oc_check_block_integrity(b, bs) != OC_OK) { /* :383-386 */
+      rc = OC_ERR_CRC_MISMATCH;
+      *bad_block = (int64_t)blk;
+      break;
+    }
+    while (off < bs) { /* processBlockForRecovery, :412-453 */
+      uint64_t z = off;
+      while (z < bs && b[z] == 0) z++;
+      if (z == bs) { /* rest of the block is padding (:415-419) */
+        flen = 0;
+        break;
+      }
+      if (off + 17 > bs) { rc = OC_ERR_WAL_TRUNCATED; break; } /* nil header in Go */
+      uint64_t size;
+      memcpy(&size, b + off, 8);
+      const uint8_t type = b[off + 8];
+      off += 17;
+      if (size > bs - off) { rc = OC_ERR_WAL_TRUNCATED; break; } /* slice bounds panic in Go */
+      const uint8_t *pay = b + off;
+      off += size;
+      if (type == 4) { /* FRAGMENT_FULL */
+        memcpy(rec_buf + used, pay, size);
+        rec_off[n] = used;
+        rec_len[n] = size;
+        used += size;
+        n++;
+        if (max_records && n >= max_records) { full = 1; break; }
+      } else if (type == 1 || type == 2) { /* FIRST, MIDDLE */
+        memcpy(frag + flen, pay, size);
+        flen += size;
+      } else if (type == 3) { /* LAST */
+        memcpy(frag + flen, pay, size);
+        flen += size;
+        memcpy(rec_buf + used, frag, flen);
+        rec_off[n] = used;
+        rec_len[n] = flen;
+        used += flen;
+        n++;
+        flen = 0;
+        if (max_records && n >= max_records) { full = 1; break; }
+      } else {
+        rc = OC_ERR_WAL_FRAGMENT_TYPE;
+        break;
+      }
+    }
+    if (rc != OC_OK) break;
+  }
+  free(frag);
+  *nrec = n;
+  if (rc == OC_OK) { /* :392-393: the next memtable starts at the next block */
+    *pos_block = blk;
+    *pos_offset = OC_CRC_SIZE;
+  } else {
+    *pos_block = blk;
+    *pos_offset = off;
+  }
+  return rc;
+}
+

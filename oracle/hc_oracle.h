@@ -51,6 +51,8 @@ uint32_t oc_checksum_ieee(const uint8_t *p, size_t n);
 #define OC_ERR_INVALID_BLOCK 1   /* "invalid block data"                            */
 #define OC_ERR_CRC_MISMATCH 2    /* "CRC mismatch in block"                         */
 #define OC_ERR_TOO_SHORT 3       /* "data is too short to contain a complete block" */
+#define OC_ERR_WAL_FRAGMENT_TYPE 4 /* "unknown fragment type" (wal.go:451)            */
+#define OC_ERR_WAL_TRUNCATED 5   /* header/payload past the block end (Go panics)   */
 const char *oc_strerror(int code);
 uint32_t oc_get_crc(const uint8_t *p, size_t n);                      /* :15-17 */
 void oc_add_crc_to_block_data(uint8_t *p, size_t n);                  /* :21-33 */
@@ -99,6 +101,17 @@ uint64_t oc_wal_frame(uint64_t seed, const uint32_t *rec_sizes, uint64_t nrec, u
                       uint8_t *dst, uint64_t max_blocks, int stamp, oc_wal_stats *st,
                       uint64_t *next_rec);
 /* log-uniform serialized record size in [lo, hi] for record i */
+/* WAL recovery, lsm/wal/wal.go:362-455, over nblocks written blocks of bs
+ * bytes (all logs back to back), starting at (start_block, start_offset).
+ * Emits the serialized records (FULL payloads and reassembled FIRST..LAST
+ * fragments) into rec_buf (>= nblocks*bs bytes) with rec_off/rec_len, stops
+ * after max_records (memtable.IsFull; 0 = never), and returns OC_OK,
+ * OC_ERR_CRC_MISMATCH (*bad_block), OC_ERR_WAL_FRAGMENT_TYPE or
+ * OC_ERR_WAL_TRUNCATED.  *pos_* = where the next memtable's replay starts. */
+int oc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t bs, uint64_t start_block,
+                  uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t *rec_off,
+                  uint64_t *rec_len, uint64_t *nrec, uint64_t *pos_block, uint64_t *pos_offset,
+                  int64_t *bad_block);
 uint32_t oc_wal_record_size(uint64_t seed, uint64_t i, uint32_t lo, uint32_t hi);
 
 #ifdef __cplusplus

@@ -40,6 +40,7 @@ def lib():
             ("oc_wal_frame", U64, [U64, P, U64, U32, P, U64, I, P, P]),
             ("oc_wal_record_size", U32, [U64, U64, U32, U32]),
             ("oc_read_from_disk", I, [P, U64, U32, U64, U64, P, P, P]),
+            ("oc_wal_replay", I, [P, U64, U32, U64, U64, U64, P, P, P, P, P, P, P]),
         ]:
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
@@ -123,4 +124,22 @@ def read_from_disk(blocks: bytes, block_size: int, start_offset: int, size: int)
     rc = lib().oc_read_from_disk(blocks, len(blocks), block_size, start_offset, size, out,
                                  ctypes.byref(fo), ctypes.byref(bad))
     return (out.raw[:size] if rc == 0 else None), fo.value, rc, bad.value
+
+
+def wal_replay(blocks: bytes, bs: int = 4096, start_block: int = 0, start_offset: int = 4, max_records: int = 0):
+    """wal.go:362-455 over written blocks (see oc_wal_replay): returns
+    (list of record bytes, error code, bad block, (pos_block, pos_offset))."""
+    import numpy as np
+    nb = len(blocks) // bs
+    buf = ctypes.create_string_buffer(max(1, nb * bs))
+    slots = nb * ((bs - 4) // 17 + 1) + 1
+    off = np.zeros(slots, dtype=np.uint64)
+    ln = np.zeros(slots, dtype=np.uint64)
+    n, pb, po, bad = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int64(0)
+    rc = lib().oc_wal_replay(blocks, nb, bs, start_block, start_offset, max_records, buf,
+                             off.ctypes.data, ln.ctypes.data, ctypes.byref(n), ctypes.byref(pb),
+                             ctypes.byref(po), ctypes.byref(bad))
+    raw = buf.raw
+    recs = [raw[int(off[i]):int(off[i]) + int(ln[i])] for i in range(n.value)]
+    return recs, rc, bad.value, (pb.value, po.value)
 

@@ -100,6 +100,51 @@ def read_from_disk(image, B, start, size):
     return bytes(out), size_after_adding_crcs((size_without_crcs(start) + size) & M64), None, -1  # uint64 wrap
 
 
+def wal_replay(blocks, bs, start_block=0, start_off=CRC_SIZE, max_records=0):
+    """lsm/wal/wal.go:362-455 (recoverMemtable + processBlockForRecovery) over
+    written blocks; one call = one memtable, max_records = IsFull (0: never).
+    Returns (records, err, bad_block, pos).  Where Go panics (header or payload
+    past the block end) this returns "truncated"."""
+    frag, recs = bytearray(), []
+    blk, off = start_block, start_off
+    while blk < len(blocks):
+        b = blocks[blk]
+        err = check_block_integrity(b)
+        if err is not None:
+            return recs, err, blk, (blk, off)
+        full = False
+        while off < bs:
+            if not any(b[off:]):                       # padding (:415-419)
+                frag.clear()
+                break
+            if off + WAL_HDR > bs:
+                return recs, "truncated", -1, (blk, off)
+            size, typ, _log = struct.unpack("<QBQ", bytes(b[off:off + WAL_HDR]))
+            off += WAL_HDR
+            if size > bs - off:
+                return recs, "truncated", -1, (blk, off)
+            pay = bytes(b[off:off + size])
+            off += size
+            if typ == 4:
+                recs.append(pay)
+            elif typ in (1, 2):
+                frag += pay
+                continue
+            elif typ == 3:
+                frag += pay
+                recs.append(bytes(frag))
+                frag.clear()
+            else:
+                return recs, "unknown fragment type", -1, (blk, off)
+            if max_records and len(recs) >= max_records:
+                full = True
+                break
+        blk, off = blk + 1, CRC_SIZE                   # :392-393
+        if full:
+            break
+    return recs, None, -1, (blk, off)
+
+
 # ---- synthetic inputs: splitmix64 finaliser over (seed, block, word) -----
 def splitmix64(seed, block, words):
     w = np.asarray(words, dtype=np.uint64)
@@ -271,6 +316,46 @@ def main():
                      "refused": refused, "sha256": [sha(b) for b in blocks],
                      "crcs": [struct.unpack("<I", b[:4])[0] for b in blocks]}
     g["wal"] = wal
+    # WAL recovery (wal.go:362-455, row f3) over the same fixtures
+    rep = {}
+    for name, recsizes in [("one_full_record", [35]), ("record_1_5_blocks", [6138]),
+                           ("record_3_blocks", [12000]), ("exact_fill", [4092 - 17 - 17 - 100, 100]),
+                           ("refused_size", [4076, 64]),
+                           ("mixed_small", [64, 300, 1000, 4000, 70, 5000, 64])]:
+        blocks, _ = wal_frame(0xABCDEF, recsizes)
+        for mr in (0, 1, 2):
+            recs, err, bad, pos = wal_replay(blocks, 4096, max_records=mr)
+            rep[f"{name}/max{mr}"] = {"fixture": name, "max_records": mr, "err": err, "bad_block": bad,
+                                      "pos": list(pos), "lens": [len(r) for r in recs],
+                                      "sha256": [sha(r) for r in recs]}
+        if len(blocks) > 1:  # corrupt the last block: records before it are still returned
+            bb = [bytearray(x) for x in blocks]
+            bb[-1][100] ^= 1
+            recs, err, bad, pos = wal_replay([bytes(x) for x in bb], 4096)
+            rep[f"{name}/corrupt_last"] = {"fixture": name, "corrupt": [len(blocks) - 1, 100, 1],
+                                           "max_records": 0, "err": err, "bad_block": bad, "pos": list(pos),
+                                           "lens": [len(r) for r in recs], "sha256": [sha(r) for r in recs]}
+    # hand-built blocks: unknown fragment type; header past the block end
+    odd = {}
+    b = bytearray(4096)
+    b[4:21] = struct.pack("<QBQ", 10, 7, 1)
+    b[21:31] = bytes(range(1, 11))
+    odd["unknown_type"] = bytes(add_crc_to_block_data(b))
+    b = bytearray(4096)
+    b[4:21] = struct.pack("<QBQ", 4064, 4, 1)
+    b[21:4085] = bytes((i * 7 + 1) & 0xFF for i in range(4064))
+    b[4090] = 9                                          # 11 bytes left: a header cannot fit
+    odd["truncated_header"] = bytes(add_crc_to_block_data(b))
+    b = bytearray(4096)
+    b[4:21] = struct.pack("<QBQ", 5000, 4, 1)            # payload past the block end
+    b[21] = 1
+    odd["truncated_payload"] = bytes(add_crc_to_block_data(b))
+    for name, blk in odd.items():
+        recs, err, bad, pos = wal_replay([blk], 4096)
+        rep[f"hand/{name}"] = {"block_hex": blk.hex(), "max_records": 0, "err": err, "bad_block": bad,
+                               "pos": list(pos), "lens": [len(r) for r in recs],
+                               "sha256": [sha(r) for r in recs]}
+    g["wal_replay"] = rep
     # global_key_dict header block: [crc4 | count u64 | zero pad], recomputed CRC
     # (utils/global_key_dict/global_key_dict_test.go:31-38 builds it by hand)
     hdr = bytearray(4096)

@@ -452,3 +452,27 @@ def test_read_from_disk_gpu_batch(cuda, hc, oracle, monkeypatch):
             assert got == want and fo == wfo
         else:
             assert hc.last_bad_block() == wbad == flip
+
+
+def test_wal_replay_gpu_batch(cuda, hc, oracle):
+    """Row f3 at a size whose verify runs as one GPU batch: hc_wal_replay vs the
+    oracle's sequential wal.go:362-455 restatement, clean, memtable-full and
+    with a corrupt block in the middle."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import walgen
+    plan = walgen.WalPlan(0x57414C, nrec=40_000)
+    img = plan.render(0, plan.nblocks)
+    nb = plan.nblocks
+    assert nb > 10_000
+    for start, mr, corrupt in [(0, 0, None), (3, 5000, None), (0, 0, nb // 2), (nb // 3, 0, nb - 1)]:
+        view = img.copy()
+        if corrupt is not None:
+            view[corrupt * 4096 + 3000] ^= 0x40
+        (buf, off, ln), err, bad, pos = hc.wal_replay(view, 4096, start, 4, mr, as_arrays=True)
+        want, wrc, wbad, wpos = oracle.wal_replay(view.tobytes(), 4096, start, 4, mr)
+        assert (0 if err is None else err.code) == wrc
+        assert pos == wpos and bad == wbad and len(ln) == len(want)
+        assert [int(x) for x in ln] == [len(w) for w in want]
+        got = buf[: int(off[-1] + ln[-1])].tobytes() if len(ln) else b""
+        assert got == b"".join(want)

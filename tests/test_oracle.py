@@ -158,3 +158,30 @@ def test_read_from_disk(oracle, golden):
             assert hashlib.sha256(got).hexdigest() == c["sha256"] and fo == c["final_offset"], c
         else:
             assert bad == c["bad_block"], c
+
+
+def _replay_case_blocks(oracle, golden, c):
+    if "block_hex" in c:
+        return bytes.fromhex(c["block_hex"])
+    w = golden["wal"][c["fixture"]]
+    b, _, _ = oracle.wal_frame(w["seed"], w["record_sizes"])
+    b = bytearray(b.tobytes())
+    if "corrupt" in c:
+        blk, off, bit = c["corrupt"]
+        b[blk * 4096 + off] ^= bit
+    return bytes(b)
+
+
+ERRS = {None: 0, "CRC mismatch in block": 2, "unknown fragment type": 4, "truncated": 5}
+
+
+def test_wal_replay(oracle, golden):
+    """oc_wal_replay (wal.go:362-455) against the zlib-derived replay fixtures."""
+    for name, c in golden["wal_replay"].items():
+        blocks = _replay_case_blocks(oracle, golden, c)
+        recs, rc, bad, pos = oracle.wal_replay(blocks, 4096, max_records=c["max_records"])
+        assert rc == ERRS[c["err"]], name
+        assert [len(r) for r in recs] == c["lens"], name
+        assert [hashlib.sha256(r).hexdigest() for r in recs] == c["sha256"], name
+        assert list(pos) == c["pos"], name
+        assert bad == c["bad_block"], name

@@ -12,6 +12,10 @@
                   CheckBlockIntegrity, wal.go:383) through the streamed pipeline.
   --mode config5b GetCRC over each variable-length record, device-resident
                   (hc_dev_crc32_blocks with HC_F_MESSAGES).
+  --mode replay   row f3 end to end: the config-5 image (--records, default
+                  2M) through hc_wal_replay = one GPU verify batch + parallel
+                  block scan + fragment reassembly + record copy-out
+                  (wal.go:362-455); rate = WAL image bytes / wall time.
 
 --mem pinned|pageable chooses where the host image lives (pinned = as if the
 segment files were read into hipHostMalloc'd buffers).
@@ -40,7 +44,7 @@ def host_array(nbytes, mem):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["host8k", "config5", "config5b"], default="host8k")
+    ap.add_argument("--mode", choices=["host8k", "config5", "config5b", "replay"], default="host8k")
     ap.add_argument("--mem", choices=["pinned", "pageable"], default="pinned")
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--blocks", type=int, default=1_000_000)
@@ -108,6 +112,29 @@ def main():
         host[victim * 4096 + 4 + 17 + 10] ^= 1
         assert str(err) == "CRC mismatch in block" and fb == victim
         bytes_ = nb * 4096
+    elif args.mode == "replay":
+        import walgen
+        nrec = args.records if args.records != 10_000_000 else 2_000_000
+        plan = walgen.WalPlan(0x57414C, nrec=nrec)
+        nb = plan.nblocks
+        host, keep = host_array(nb * 4096, args.mem)
+        for b0 in range(0, nb, 1 << 18):
+            plan.render(b0, min(nb, b0 + (1 << 18)), out=host[b0 * 4096:min(nb, b0 + (1 << 18)) * 4096],
+                        threads=args.threads)
+        kept = plan.sizes[~((plan.sizes + 17 > 4092) & (plan.sizes + 17 <= 4096))]
+        res.update(records=nrec, blocks=nb, refused=plan.refused, image_gib=round(nb * 4096 / 2**30, 2))
+        crc.wal_replay(host[: 64 * 4096], 4096)  # warm
+        rec_out = np.empty(nb * 4096, dtype=np.uint8)
+        rec_out[::4096] = 0  # fault the output pages in once, outside the timed region
+        times = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            (rbuf, roff, rlen), err, bad, pos = crc.wal_replay(host, 4096, slots=nrec + 16, as_arrays=True,
+                                                                out=rec_out)
+            times.append(time.perf_counter() - t)
+            assert err is None and pos == (nb, 4), (err, pos)
+            assert np.array_equal(rlen, kept.astype(np.uint64)), "record lengths differ from the writer's"
+        bytes_ = nb * 4096
     else:  # config5b: per-record GetCRC, device-resident
         import walgen
         sizes = walgen.WalPlan(0x57414C, nrec=1).sizes  # noqa: F841 (lib init)
@@ -144,7 +171,7 @@ def main():
     best = min(times)
     res.update(bytes=bytes_, seconds=[round(x, 4) for x in times], gib_s=round(bytes_ / best / 2**30, 2),
                gb_s=round(bytes_ / best / 1e9, 2), pcie_gen5_x16_frac=round(bytes_ / best / 63e9, 3)
-               if args.mode != "config5b" else None)
+               if args.mode not in ("config5b",) else None)
     print(json.dumps(res), flush=True)
 
 
