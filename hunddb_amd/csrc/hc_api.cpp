@@ -701,29 +701,34 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   if (start_block >= nblocks) return HC_OK;
   const uint64_t n = nblocks - start_block;
   const uint8_t *base = blocks + start_block * bs;
-  // 1. verify every block in one batch (wal.go:383), GPU from 256 blocks
-  int64_t first_bad = -1;
+  // 1+2. verify every block in one batch (wal.go:383; GPU from 256 blocks) on the
+  // calling thread while worker threads scan the blocks into items (the scan
+  // does not depend on the CRCs; the merge below stops at the first bad block)
   static const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", 256);
-  if (n >= gpu_min || force_gpu()) {
-    int rc = hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
-    if (rc < 0) return rc;
-  } else {
-    for (uint64_t i = 0; i < n && first_bad < 0; i++)
-      if (hc_check_block(base + i * bs, bs) != HC_OK) first_bad = (int64_t)i;
-  }
-  const uint64_t stop = first_bad >= 0 ? (uint64_t)first_bad : n;  // blocks that may be parsed
-  // 2. scan blocks into items, in parallel over contiguous block ranges
   static const int threads_cfg = std::max(1, env_int("HC_COPY_THREADS", 8));
-  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, stop / 64));
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, n / 64));
   std::vector<std::vector<WalItem>> items(T);
-  parallel_for(T, [&](int t) {
-    const uint64_t lo = stop * t / T, hi = stop * (t + 1) / T;
-    items[t].reserve((hi - lo) * 2 + 4);
+  int64_t first_bad = -1;
+  int vrc = HC_OK;
+  parallel_for(T + 1, [&](int t) {
+    if (t == 0) {
+      if (n >= gpu_min || force_gpu()) {
+        vrc = hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
+      } else {
+        for (uint64_t i = 0; i < n && first_bad < 0; i++)
+          if (hc_check_block(base + i * bs, bs) != HC_OK) first_bad = (int64_t)i;
+      }
+      return;
+    }
+    const uint64_t lo = n * (t - 1) / T, hi = n * t / T;
+    items[t - 1].reserve((hi - lo) * 2 + 4);
     for (uint64_t i = lo; i < hi; i++)
       if (!wal_scan_block(base + i * bs, block_size, start_block + i, i == 0 ? start_offset : HC_CRC_SIZE,
-                          items[t]))
+                          items[t - 1]))
         break;
   });
+  if (vrc < 0) return vrc;
+  const uint64_t stop = first_bad >= 0 ? (uint64_t)first_bad : n;  // blocks the Go loop parses
   // 3. sequential merge: fragment reassembly, memtable-full stop, capacity stop
   struct Piece {
     const uint8_t *p;
@@ -733,7 +738,7 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   uint64_t used = 0, count = 0, pend_len = 0;
   uint64_t pend_blk = 0, pend_hdr = 0;
   int code = HC_OK;
-  bool done = false;
+  bool done = false, hit_bad = false;
   uint64_t pb = start_block + stop, po = HC_CRC_SIZE;  // position when everything parsed
   auto emit = [&](const WalItem &it, uint64_t first_blk, uint64_t first_hdr) -> bool {
     const uint64_t len = pend_len + it.len;
@@ -757,6 +762,11 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   };
   for (int t = 0; t < T && !done; t++) {
     for (const WalItem &it : items[t]) {
+      if (it.blk >= start_block + stop) {  // the first bad block: nothing after it is parsed
+        hit_bad = true;
+        done = true;
+        break;
+      }
       if (it.kind == WalItem::kClear) {
         pending.clear();
         pend_len = 0;
@@ -791,7 +801,7 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
       }
     }
   }
-  if (!done && first_bad >= 0) {
+  if (hit_bad || (!done && first_bad >= 0)) {
     code = HC_ERR_CRC_MISMATCH;
     if (bad_block) *bad_block = (int64_t)(start_block + first_bad);
     pb = start_block + first_bad;
