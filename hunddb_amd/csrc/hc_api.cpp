@@ -705,7 +705,7 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   // calling thread while worker threads scan the blocks into items (the scan
   // does not depend on the CRCs; the merge below stops at the first bad block)
   static const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", 256);
-  static const int threads_cfg = std::max(1, env_int("HC_COPY_THREADS", 8));
+  static const int threads_cfg = std::max(1, env_int("HC_WAL_THREADS", 16));  // 16: the GPU box's CPU share
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, n / 64));
   std::vector<std::vector<WalItem>> items(T);
   int64_t first_bad = -1;

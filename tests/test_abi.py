@@ -229,3 +229,25 @@ def test_read_from_disk_host(hc, golden, oracle):
                 assert got == want and fo == wfo
             else:
                 assert hc.last_bad_block() == wbad
+
+
+def test_global_key_dict_sites(hc, golden):
+    """Row f4: the blocks utils/global_key_dict writes (initializeNewFile,
+    global_key_dict.go:354-390) stamped and verified through the library give
+    the zlib-derived CRCs, and a flipped bit is caught."""
+    import struct
+    import zlib
+    hdr = bytearray(4096)
+    struct.pack_into("<QQQ", hdr, 4, 1, 1, 4)          # nextID, lastBlockIndex, lastBlockOffset
+    hc.AddCRCToBlockData(hdr)
+    assert struct.unpack("<I", hdr[:4])[0] == zlib.crc32(bytes(hdr[4:]))
+    assert hc.CheckBlockIntegrity(bytes(hdr)) is None
+    data = bytearray(4096)
+    hc.AddCRCToBlockData(data)
+    assert struct.unpack("<I", data[:4])[0] == golden["known"]["zero_payload"]["4096"]
+    g = golden["global_key_dict_header"]
+    blk = bytearray(4096)
+    blk[4:12] = struct.pack("<Q", g["count"])
+    assert hc.GetCRC(bytes(blk[4:])) == g["crc"]
+    hdr[100] ^= 4
+    assert str(hc.CheckBlockIntegrity(bytes(hdr))) == "CRC mismatch in block"
