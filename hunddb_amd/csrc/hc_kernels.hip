@@ -489,10 +489,15 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       const uint32_t m = (uint32_t)(A0 & 15u), q = m >> 2, rb = m & 3u;
       const uintptr_t Abase = A0 - m;
       uint32_t c[4] = {0, 0, 0, 0};
-      for (uint32_t r0 = 0; r0 < rows; r0 += kBatch) {
-        uint4 ch0[kBatch], ch1[kBatch];
+      {
+        // rows 0 and 1 may hold the virtual prefix (z zeros + W0; z + 4 <= 1027
+        // bytes): aligned chunks predicated on the payload range + funnel
+        // shift + masks
+        constexpr int kSlow = 2;
+        const uint32_t r0 = 0;
+        uint4 ch0[kSlow], ch1[kSlow];
 #pragma unroll
-        for (int b = 0; b < kBatch; b++) {
+        for (int b = 0; b < kSlow; b++) {
           ch0[b] = ch1[b] = make_uint4(0, 0, 0, 0);
           if (r0 + b < rows) {
             const uintptr_t X0 = Abase + (uintptr_t)(r0 + b) * kRowBytes + 16u * lane, X1 = X0 + 16;
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
           }
         }
 #pragma unroll
-        for (int b = 0; b < kBatch; b++) {
+        for (int b = 0; b < kSlow; b++) {
           if (r0 + b < rows) {
             const uint4 fw = funnel16(ch0[b], ch1[b], q, rb);
             uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
@@ -526,6 +531,27 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 #pragma unroll
               for (int k2 = 0; k2 < 4; k2++) c[k2] = row_step(c[k2], w[k2]);
             }
+          }
+        }
+      }
+      // rows >= 2 start inside the payload (2048 > z + 4) and the last row
+      // ends at P+Lp: one unaligned 16-B load per lane per row, no funnel, no
+      // masks
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      typedef u32x4 u32x4_u __attribute__((aligned(1)));
+      for (uint32_t r0 = 2; r0 < rows; r0 += kBatch) {
+        u32x4 v[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; b++)  // unconditional (clamped to the last row): no branch among the loads
+          v[b] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(
+              A0 + (uintptr_t)(r0 + b < rows ? r0 + b : rows - 1) * kRowBytes + 16u * lane));
+#pragma unroll
+        for (int b = 0; b < kBatch; b++) {
+          if (r0 + b < rows) {
+            c[0] = row_step(c[0], v[b].x);
+            c[1] = row_step(c[1], v[b].y);
+            c[2] = row_step(c[2], v[b].z);
+            c[3] = row_step(c[3], v[b].w);
           }
         }
       }
