@@ -47,7 +47,9 @@ HC_E_ARG, HC_E_HIP, HC_E_NODEV, HC_E_NOMEM, HC_E_LAYOUT = -1, -2, -3, -4, -5
 HC_F_STAMP = 1
 HC_F_MESSAGES = 2
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhundcrc.so")
+# HUNDCRC_LIB: load another build of the library (A/B timing of kernel variants)
+_LIB_PATH = os.environ.get("HUNDCRC_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "libhundcrc.so")
 
 
 class HundCRCError(RuntimeError):

@@ -464,11 +464,13 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       const uint32_t k = (uint32_t)__builtin_ctzll(todo);
       todo &= todo - 1;
       const uint64_t blk = g + k;
-      // scalar re-read of the selected block's entry (no ring here to protect)
-      typedef const __attribute__((address_space(4))) uint64_t *c64p;
-      typedef const __attribute__((address_space(4))) uint32_t *c32p;
-      const uint64_t o = offs ? ((c64p)offs)[blk] : blk * stride;
-      const uint32_t l = lens ? ((c32p)lens)[blk] : ulen;
+      // the selected entry from lane k of the sweep (k is wave-uniform).
+      // readlane returns int: cast each half to uint32_t BEFORE widening, or
+      // a low word >= 2^31 sign-extends into the high word (a wild address).
+      const uint32_t o_lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)oj, k);
+      const uint32_t o_hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(oj >> 32), k);
+      const uint64_t o = ((uint64_t)o_hi << 32) | (uint64_t)o_lo;
+      const uint32_t l = (uint32_t)__builtin_amdgcn_readlane(lj, k);
       const uint8_t *blkp = base + o;
       if (!msg && l < 4) {  // "invalid block data": no CRC, always bad
         if (lane == 0) {
@@ -501,8 +503,16 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
           ch0[b] = ch1[b] = make_uint4(0, 0, 0, 0);
           if (r0 + b < rows) {
             const uintptr_t X0 = Abase + (uintptr_t)(r0 + b) * kRowBytes + 16u * lane, X1 = X0 + 16;
-            if (X0 + 16 > P && X0 < P + Lp) ch0[b] = load_row<1>(reinterpret_cast<const uint8_t *>(X0), 0);
-            if (X1 + 16 > P && X1 < P + Lp) ch1[b] = load_row<1>(reinterpret_cast<const uint8_t *>(X1), 0);
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            typedef const __attribute__((address_space(1))) v4u *g16;  // global_load, not flat_load
+            if (X0 + 16 > P && X0 < P + Lp) {
+              const v4u t = __builtin_nontemporal_load((g16)X0);
+              ch0[b] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+            if (X1 + 16 > P && X1 < P + Lp) {
+              const v4u t = __builtin_nontemporal_load((g16)X1);
+              ch1[b] = make_uint4(t.x, t.y, t.z, t.w);
+            }
           }
         }
 #pragma unroll
@@ -512,15 +522,15 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
             uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
             const int64_t srow = (int64_t)(r0 + b) * kRowBytes - (int64_t)z - 4;
             if (srow < 0) {  // zeros, then W0, then data
+              // word k2 starts d bytes before the payload: keep its bytes
+              // j >= d, and bytes ob = j - d in [-4, -1] are W0's byte ob + 4,
+              // i.e. the window of Y = W0 << 32 that starts at byte 8 - d
+              const uint64_t Y = (uint64_t)w0 << 32;
 #pragma unroll
               for (int k2 = 0; k2 < 4; k2++) {
-                uint32_t dm = 0, wv = 0;
-#pragma unroll
-                for (int jb = 0; jb < 4; jb++) {
-                  const int64_t ob = srow + 16 * (int64_t)lane + 4 * k2 + jb;
-                  if (ob >= 0) dm |= 0xFFu << (8 * jb);
-                  else if (ob >= -4) wv |= ((w0 >> (8 * (ob + 4))) & 0xFFu) << (8 * jb);
-                }
+                const int32_t d = -((int32_t)srow + 16 * (int32_t)lane + 4 * k2);
+                const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : 0xFFFFFFFFu << (8 * d));
+                const uint32_t wv = (d >= 1 && d <= 8) ? (uint32_t)(Y >> (64 - 8 * d)) : 0u;
                 w[k2] = (w[k2] & dm) | wv;
               }
             }
@@ -539,12 +549,13 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       // masks
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       typedef u32x4 u32x4_u __attribute__((aligned(1)));
+      typedef const __attribute__((address_space(1))) u32x4_u *g16u;  // global_load, not flat_load
       for (uint32_t r0 = 2; r0 < rows; r0 += kBatch) {
         u32x4 v[kBatch];
 #pragma unroll
         for (int b = 0; b < kBatch; b++)  // unconditional (clamped to the last row): no branch among the loads
-          v[b] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(
-              A0 + (uintptr_t)(r0 + b < rows ? r0 + b : rows - 1) * kRowBytes + 16u * lane));
+          v[b] = __builtin_nontemporal_load(
+              (g16u)(A0 + (uintptr_t)(r0 + b < rows ? r0 + b : rows - 1) * kRowBytes + 16u * lane));
 #pragma unroll
         for (int b = 0; b < kBatch; b++) {
           if (r0 + b < rows) {

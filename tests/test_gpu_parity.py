@@ -476,3 +476,40 @@ def test_wal_replay_gpu_batch(cuda, hc, oracle):
         assert [int(x) for x in ln] == [len(w) for w in want]
         got = buf[: int(off[-1] + ln[-1])].tobytes() if len(ln) else b""
         assert got == b"".join(want)
+
+
+@pytest.mark.parametrize("flags", [0, 2])
+def test_offsets_beyond_2_and_4_GiB(cuda, hc, oracle, flags):
+    """off/len batches whose offsets have bit 31 of the low word set, and exceed
+    4 GiB: the per-entry metadata path of k_crc_fast / k_crc_any must widen
+    offsets as unsigned 64-bit (blocks mode and whole-message mode)."""
+    torch = cuda
+    rng = np.random.default_rng(4242 + flags)
+    total = 5 * 2**30 + 12345
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    n = 3000
+    lens = rng.integers(64, 20000, n).astype(np.uint32)
+    lens[: n // 3] = 8192                                   # conforming sizes for the streaming kernel
+    bases = np.array([0, 2**31 - 70000, 2**31 + 16, 3 * 2**31 + 5, 2**32 + 48, total - 11_000_000],
+                     dtype=np.uint64)
+    offs = []
+    for i in range(n):
+        b = bases[i % len(bases)]
+        offs.append(int(b) + (i // len(bases)) * 20480 + (0 if i < n // 3 else int(rng.integers(0, 7))))
+    off = np.array(offs, dtype=np.uint64)
+    assert (off + lens <= total).all() and ((off & 0xFFFFFFFF) >= 2**31).any() and (off >= 2**32).any()
+    doff = torch.from_numpy(off.view(np.int64)).to("cuda")
+    dlen = torch.from_numpy(lens.view(np.int32)).to("cuda")
+    hc.dev_fill_blocks(buf, 77, off=doff, lens=dlen, nblocks=n)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=n, flags=flags)
+    torch.cuda.synchronize()
+    got = u32(out)
+    host = np.concatenate([buf[int(o):int(o) + int(l)].cpu().numpy() for o, l in zip(off, lens)])
+    hoff = np.zeros(n, dtype=np.uint64)
+    hoff[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    if flags:
+        want = oracle.crc32_messages(host, hoff, lens)
+    else:
+        want = oracle.crc32_blocks(host, off=hoff, lens=lens)
+    assert (got == want).all(), int((got != want).sum())
