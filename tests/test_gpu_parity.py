@@ -490,7 +490,7 @@ def test_offsets_beyond_2_and_4_GiB(cuda, hc, oracle, flags):
     n = 3000
     lens = rng.integers(64, 20000, n).astype(np.uint32)
     lens[: n // 3] = 8192                                   # conforming sizes for the streaming kernel
-    bases = np.array([0, 2**31 - 70000, 2**31 + 16, 3 * 2**31 + 5, 2**32 + 48, total - 11_000_000],
+    bases = np.array([0, 2**31 - 70000, 2**31 + 16, 2**32 - 3_000_000, 2**32 + 48, total - 11_000_000],
                      dtype=np.uint64)
     offs = []
     for i in range(n):
