@@ -44,6 +44,8 @@ WORKLOADS = {
     # f1: batched ReadFromDisk (k_unframe): verify 1M x 4 KiB blocks and strip
     # the CRC words (4096 MB read, 4092 MB payload written)
     "unframe": (1_000_000, "unframe", "weak"),
+    # config2's blocks described by off/len arrays (the per-block metadata path)
+    "offlen4k": (1_000_000, "offlen4k", "weak"),
 }
 
 
@@ -201,6 +203,14 @@ def main():
         kw = dict(off=doff, lens=dlen, nblocks=my)
         step_bytes = total
         block_desc = "mixed 4/8/16 KiB"
+    elif bsize == "offlen4k":
+        buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
+        crc.dev_fill_blocks(buf, seed ^ rank, stride=4096, ulen=4096, nblocks=my)
+        doff = torch.arange(my, dtype=torch.int64, device=dev) * 4096
+        dlen = torch.full((my,), 4096, dtype=torch.int32, device=dev)
+        kw = dict(off=doff, lens=dlen, nblocks=my)
+        step_bytes = my * 4096
+        block_desc = "4096 B via off/len arrays"
     elif bsize == "frame":
         npay = my * 4092 - 1000  # ragged last block
         raw = torch.empty(npay + 1, dtype=torch.uint8, device=dev)
@@ -289,7 +299,7 @@ def main():
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "frame", "unframe"):
+        if world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "frame", "unframe", "offlen4k"):
             sample_blocks = min(my, (512 << 20) // bsize)
             host = buf[: sample_blocks * bsize].cpu().numpy()
             cpu = cpu_baseline(host, bsize, args.cpu_threads, args.cpu_seconds)

@@ -222,20 +222,57 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
   const uint8_t *pptr = nullptr;
   uint32_t prow = 0, prows = 0;
   bool pvalid = false;
+#ifndef HC_META_WINDOW
+#define HC_META_WINDOW 1
+#endif
+#if HC_META_WINDOW
+  // Metadata (off/len arrays only): a window of 64 blocks lives in 3 VGPRs
+  // (lane j holds block wbase + j*step) and is read per block with
+  // v_readlane.  It is refilled synchronously once per 64 blocks: that one
+  // wait drains the row ring, 1/64 of the per-block stall a scalar or vector
+  // load of every block's entry costs (SMEM returns out of order, so any
+  // pending s_load turns the next LDS-lookup wait into lgkmcnt(0)).
+  uint64_t wbase = ~0ull;
+  uint32_t wo_lo = 0, wo_hi = 0, wl = 0;
+  auto meta = [&](uint64_t i, uint64_t &o, uint32_t &l) {
+    if (wbase == ~0ull || (i - wbase) / step >= 64) {
+      wbase = i;
+      // opaque copy of i: the window address is computed afresh, never
+      // strength-reduced across the inlined call sites
+      uint64_t iw = i;
+      asm volatile("" : "+s"(iw));
+      const uint64_t j = iw + (uint64_t)lane * step;
+      const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
+      wo_lo = (uint32_t)oj;
+      wo_hi = (uint32_t)(oj >> 32);
+      wl = j < b1 ? (lens ? lens[j] : ulen) : 0;
+      // consume the loads here, inside the refill branch, so hipcc's
+      // vmcnt(0) for them is not hoisted to the (per-block) merge point
+      asm volatile("" : "+v"(wo_lo), "+v"(wo_hi), "+v"(wl));
+    }
+    const uint32_t k = uni((uint32_t)((i - wbase) / step));
+    // readlane returns int: each half goes through uint32_t before widening,
+    // or an offset whose low word is >= 2^31 sign-extends into the high word
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(wo_lo, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(wo_hi, k);
+    o = ((uint64_t)hi << 32) | (uint64_t)lo;
+    l = (uint32_t)__builtin_amdgcn_readlane(wl, k);
+  };
+#else
   // Metadata (off/len arrays only) is read through the constant address
   // space so hipcc emits scalar s_loads, counted by lgkmcnt -- never by the
-  // vmcnt of the row ring.  The next block's entry is fetched when the
-  // current one starts, so its latency hides behind the current block's rows.
+  // vmcnt of the row ring.
   typedef const __attribute__((address_space(4))) uint64_t *c64p;
   typedef const __attribute__((address_space(4))) uint32_t *c32p;
   const c64p coffs = (c64p)offs;
   const c32p clens = (c32p)lens;
-  uint64_t qb = ~0ull, qo = 0;  // prefetched entry (block qb)
-  uint32_t ql = 0;
   auto meta = [&](uint64_t i, uint64_t &o, uint32_t &l) {
     o = coffs ? coffs[i] : i * stride;
     l = clens ? clens[i] : ulen;
   };
+  uint64_t qb = ~0ull, qo = 0;  // prefetched entry (block qb)
+  uint32_t ql = 0;
+#endif
   auto start_from = [&](uint64_t i) {
     if constexpr (kUniform) {  // loop-free: keeps hipcc's vmcnt counting exact
       pvalid = i < b1;
@@ -250,20 +287,26 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     for (; i < b1; i += step) {
       uint64_t o;
       uint32_t l;
-      if (i == qb) {
+#if HC_META_WINDOW
+      meta(i, o, l);
+#else
+      if (i == qb) {  // the next block's entry, fetched one block ahead
         o = qo;
         l = ql;
       } else {
         meta(i, o, l);
       }
+#endif
       if (conform(o, l)) {
         pb = i;
         pptr = base + o;
         prows = l >> 10;
         prow = 0;
         pvalid = true;
+#if !HC_META_WINDOW
         qb = i + step;
         if (qb < b1) meta(qb, qo, ql);
+#endif
         return;
       }
     }
