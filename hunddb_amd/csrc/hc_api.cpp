@@ -701,17 +701,23 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   if (start_block >= nblocks) return HC_OK;
   const uint64_t n = nblocks - start_block;
   const uint8_t *base = blocks + start_block * bs;
-  // 1+2. verify every block in one batch (wal.go:383; GPU from 256 blocks) on the
-  // calling thread while worker threads scan the blocks into items (the scan
-  // does not depend on the CRCs; the merge below stops at the first bad block)
+  // The verify batch (wal.go:383; GPU from 256 blocks) runs on the calling
+  // thread while a second thread scans, merges and copies the records out
+  // without waiting for it (none of that depends on the CRCs).  The result is
+  // then cut where the Go loop would have stopped: at the first bad block.
   static const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", 256);
   static const int threads_cfg = std::max(1, env_int("HC_WAL_THREADS", 16));  // 16: the GPU box's CPU share
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, n / 64));
-  std::vector<std::vector<WalItem>> items(T);
   int64_t first_bad = -1;
   int vrc = HC_OK;
-  parallel_for(T + 1, [&](int t) {
-    if (t == 0) {
+  // merge outcome
+  enum Stop { kAll, kErr, kFull, kCap } stop = kAll;
+  uint64_t stop_blk = 0;  // block of the error / of the record that filled the memtable / of the record that did not fit
+  int err_code = HC_OK;
+  uint64_t pb = 0, po = HC_CRC_SIZE, count = 0;
+  std::vector<uint64_t> rec_done_blk;  // block in which each record completed
+  parallel_for(2, [&](int role) {
+    if (role == 0) {
       if (n >= gpu_min || force_gpu()) {
         vrc = hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
       } else {
@@ -720,99 +726,103 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
       }
       return;
     }
-    const uint64_t lo = n * (t - 1) / T, hi = n * t / T;
-    items[t - 1].reserve((hi - lo) * 2 + 4);
-    for (uint64_t i = lo; i < hi; i++)
-      if (!wal_scan_block(base + i * bs, block_size, start_block + i, i == 0 ? start_offset : HC_CRC_SIZE,
-                          items[t - 1]))
-        break;
+    // 1. scan the blocks into items, T threads over contiguous block ranges
+    std::vector<std::vector<WalItem>> items(T);
+    parallel_for(T, [&](int t) {
+      const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+      items[t].reserve((hi - lo) * 2 + 4);
+      for (uint64_t i = lo; i < hi; i++)
+        if (!wal_scan_block(base + i * bs, block_size, start_block + i, i == 0 ? start_offset : HC_CRC_SIZE,
+                            items[t]))
+          break;
+    });
+    // 2. sequential merge: fragment reassembly, memtable-full stop, capacity stop
+    struct Piece {
+      const uint8_t *p;
+      uint64_t len, dst;
+    };
+    std::vector<Piece> pieces, pending;
+    uint64_t used = 0, pend_len = 0, pend_blk = 0, pend_hdr = 0;
+    pb = start_block + n;
+    auto emit = [&](const WalItem &it, uint64_t first_blk, uint64_t first_hdr) -> bool {
+      const uint64_t len = pend_len + it.len;
+      if (count >= rec_slots || used + len > rec_buf_cap || !rec_buf || !rec_off || !rec_len) {
+        stop = kCap;  // resumable: the record starts at (first_blk, first_hdr)
+        stop_blk = first_blk;
+        pb = first_blk;
+        po = first_hdr;
+        return false;
+      }
+      rec_off[count] = used;
+      rec_len[count] = len;
+      for (auto &q : pending) {
+        pieces.push_back({q.p, q.len, used});
+        used += q.len;
+      }
+      pieces.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, used});
+      used += it.len;
+      rec_done_blk.push_back(it.blk);
+      count++;
+      pending.clear();
+      pend_len = 0;
+      return true;
+    };
+    for (int t = 0; t < T && stop == kAll; t++) {
+      for (const WalItem &it : items[t]) {
+        if (it.kind == WalItem::kClear) {
+          pending.clear();
+          pend_len = 0;
+          continue;
+        }
+        if (it.kind == WalItem::kErrType || it.kind == WalItem::kErrTrunc) {
+          stop = kErr;
+          stop_blk = it.blk;
+          err_code = it.kind == WalItem::kErrType ? HC_ERR_WAL_FRAGMENT_TYPE : HC_ERR_WAL_TRUNCATED;
+          pb = it.blk;
+          po = it.hdr;
+          break;
+        }
+        if (it.kind == WalItem::kFrag) {
+          if (pending.empty()) {
+            pend_blk = it.blk;
+            pend_hdr = it.hdr;
+          }
+          pending.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, 0});
+          pend_len += it.len;
+          continue;
+        }
+        const bool frag = it.kind == WalItem::kLast && !pending.empty();
+        if (!emit(it, frag ? pend_blk : it.blk, frag ? pend_hdr : it.hdr)) break;
+        if (max_records && count >= max_records) {  // memtable.IsFull: next block (wal.go:392-397)
+          stop = kFull;
+          stop_blk = it.blk;
+          pb = it.blk + 1;
+          po = HC_CRC_SIZE;
+          break;
+        }
+      }
+    }
+    // 3. copy the record bytes out, T threads
+    const int C = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)T, used >> 22));
+    parallel_for(C, [&](int t) {
+      const uint64_t lo = pieces.size() * t / C, hi = pieces.size() * (t + 1) / C;
+      for (uint64_t i = lo; i < hi; i++) std::memcpy(rec_buf + pieces[i].dst, pieces[i].p, pieces[i].len);
+    });
   });
   if (vrc < 0) return vrc;
-  const uint64_t stop = first_bad >= 0 ? (uint64_t)first_bad : n;  // blocks the Go loop parses
-  // 3. sequential merge: fragment reassembly, memtable-full stop, capacity stop
-  struct Piece {
-    const uint8_t *p;
-    uint64_t len, dst;
-  };
-  std::vector<Piece> pieces, pending;
-  uint64_t used = 0, count = 0, pend_len = 0;
-  uint64_t pend_blk = 0, pend_hdr = 0;
-  int code = HC_OK;
-  bool done = false, hit_bad = false;
-  uint64_t pb = start_block + stop, po = HC_CRC_SIZE;  // position when everything parsed
-  auto emit = [&](const WalItem &it, uint64_t first_blk, uint64_t first_hdr) -> bool {
-    const uint64_t len = pend_len + it.len;
-    if (count >= rec_slots || used + len > rec_buf_cap || !rec_buf || !rec_off || !rec_len) {
-      pb = first_blk;  // resumable: the record starts at (first_blk, first_hdr)
-      po = first_hdr;
-      return false;
-    }
-    rec_off[count] = used;
-    rec_len[count] = len;
-    for (auto &q : pending) {
-      pieces.push_back({q.p, q.len, used});
-      used += q.len;
-    }
-    pieces.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, used});
-    used += it.len;
-    count++;
-    pending.clear();
-    pend_len = 0;
-    return true;
-  };
-  for (int t = 0; t < T && !done; t++) {
-    for (const WalItem &it : items[t]) {
-      if (it.blk >= start_block + stop) {  // the first bad block: nothing after it is parsed
-        hit_bad = true;
-        done = true;
-        break;
-      }
-      if (it.kind == WalItem::kClear) {
-        pending.clear();
-        pend_len = 0;
-        continue;
-      }
-      if (it.kind == WalItem::kErrType || it.kind == WalItem::kErrTrunc) {
-        code = it.kind == WalItem::kErrType ? HC_ERR_WAL_FRAGMENT_TYPE : HC_ERR_WAL_TRUNCATED;
-        pb = it.blk;
-        po = it.hdr;
-        done = true;
-        break;
-      }
-      if (it.kind == WalItem::kFrag) {
-        if (pending.empty()) {
-          pend_blk = it.blk;
-          pend_hdr = it.hdr;
-        }
-        pending.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, 0});
-        pend_len += it.len;
-        continue;
-      }
-      const bool frag = it.kind == WalItem::kLast;
-      if (!emit(it, frag && !pending.empty() ? pend_blk : it.blk, frag && !pending.empty() ? pend_hdr : it.hdr)) {
-        done = true;  // out of caller capacity: HC_OK, position at this record
-        break;
-      }
-      if (max_records && count >= max_records) {  // memtable.IsFull: next block (wal.go:392-397)
-        pb = it.blk + 1;
-        po = HC_CRC_SIZE;
-        done = true;
-        break;
-      }
+  int code = stop == kErr ? err_code : HC_OK;
+  if (first_bad >= 0) {
+    const uint64_t B = start_block + (uint64_t)first_bad;
+    // the Go loop checks a block's CRC before parsing it: a stop at or after
+    // the bad block did not happen, and no record completing there exists
+    if (stop == kAll || stop_blk >= B) {
+      while (count > 0 && rec_done_blk[count - 1] >= B) count--;
+      code = HC_ERR_CRC_MISMATCH;
+      if (bad_block) *bad_block = (int64_t)B;
+      pb = B;
+      po = first_bad == 0 ? start_offset : HC_CRC_SIZE;
     }
   }
-  if (hit_bad || (!done && first_bad >= 0)) {
-    code = HC_ERR_CRC_MISMATCH;
-    if (bad_block) *bad_block = (int64_t)(start_block + first_bad);
-    pb = start_block + first_bad;
-    po = first_bad == 0 ? start_offset : HC_CRC_SIZE;
-  }
-  // 4. copy the record bytes, in parallel
-  const int C = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, used >> 22));
-  parallel_for(C, [&](int t) {
-    const uint64_t lo = pieces.size() * t / C, hi = pieces.size() * (t + 1) / C;
-    for (uint64_t i = lo; i < hi; i++) std::memcpy(rec_buf + pieces[i].dst, pieces[i].p, pieces[i].len);
-  });
   *nrec = count;
   *pos_block = pb;
   *pos_offset = po;
