@@ -251,3 +251,24 @@ def test_global_key_dict_sites(hc, golden):
     assert hc.GetCRC(bytes(blk[4:])) == g["crc"]
     hdr[100] ^= 4
     assert str(hc.CheckBlockIntegrity(bytes(hdr))) == "CRC mismatch in block"
+
+
+def test_device_entry_argument_checks(hc):
+    """The device entries validate their layout before touching a device, so
+    these run without a GPU (the pointers are never dereferenced)."""
+    L = hc.lib()
+    fake = 0x10000  # 16-B aligned, never dereferenced
+    assert L.hc_dev_add_crcs(0, fake, 0, fake, None, None) == hc.HC_OK            # n == 0: nothing to do
+    assert L.hc_dev_add_crcs(0, None, 10, fake, None, None) == hc.HC_E_ARG
+    assert L.hc_dev_add_crcs(0, fake, 10, fake + 4, None, None) == hc.HC_E_LAYOUT  # dst not 16-B aligned
+    assert L.hc_dev_read_blocks(0, fake, 0, 4096, fake, None, None, None, None) == hc.HC_OK
+    for bs in (0, 1024, 5000, 4096 * 8):
+        assert L.hc_dev_read_blocks(0, fake, 4, bs, fake, None, None, None, None) == hc.HC_E_LAYOUT
+    assert L.hc_dev_read_blocks(0, fake + 8, 4, 4096, fake, None, None, None, None) == hc.HC_E_LAYOUT
+    bm = ctypes.c_uint32(0)
+    assert L.hc_dev_read_blocks(0, fake, 4, 4096, fake, None, ctypes.addressof(bm), None, None) == hc.HC_E_ARG
+    nrec, pb, po = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.hc_wal_replay(None, 0, 4096, 0, 4, 0, None, 0, None, None, 0, ctypes.byref(nrec),
+                           ctypes.byref(pb), ctypes.byref(po), None) == hc.HC_OK
+    assert L.hc_wal_replay(None, 5, 4096, 0, 4, 0, None, 0, None, None, 0, ctypes.byref(nrec),
+                           ctypes.byref(pb), ctypes.byref(po), None) == hc.HC_E_ARG
