@@ -132,5 +132,58 @@ inline void AddCRCToBlocks(Bytes data, uint32_t blockSize) {
         "AddCRCToBlocks");
 }
 
+// ---- adjacent rows ----------------------------------------------
+
+// block_manager.go:189-242 ReadFromDisk minus the file I/O (f1): `blocks` holds
+// the blocks from startOffset/blockSize on, as read.  Every touched block is
+// verified in one batch.  Returns the payload and the final physical offset,
+// or the error of the first failing block (its index in *badBlock).
+struct ReadResult {
+  std::vector<uint8_t> data;
+  uint64_t finalOffset = 0;
+  Error err;
+};
+inline ReadResult ReadFromDisk(ConstBytes blocks, uint32_t blockSize, uint64_t startOffset, uint64_t size,
+                               int64_t *badBlock = nullptr) {
+  ReadResult r;
+  r.data.resize(size);
+  int64_t bad = -1;
+  r.err = check(hc_read_from_disk(blocks.data(), blocks.size(), blockSize, startOffset, size, r.data.data(),
+                                  &r.finalOffset, &bad),
+                "ReadFromDisk");
+  if (badBlock) *badBlock = bad;
+  if (r.err) {
+    r.data.clear();
+    r.finalOffset = 0;
+  }
+  return r;
+}
+
+// wal.go:362-455 recoverMemtable over written WAL blocks (f3): the serialized
+// records (what record.Deserialize receives) of one memtable, in order, and the
+// position the next memtable starts from.  maxRecords plays memtable.IsFull.
+struct WalReplayResult {
+  std::vector<std::vector<uint8_t>> records;
+  uint64_t posBlock = 0, posOffset = CRC_SIZE;
+  int64_t badBlock = -1;
+  Error err;
+};
+inline WalReplayResult WalReplay(ConstBytes blocks, uint32_t blockSize, uint64_t startBlock = 0,
+                                 uint64_t startOffset = CRC_SIZE, uint64_t maxRecords = 0) {
+  WalReplayResult r;
+  const uint64_t nb = blocks.size() / blockSize;
+  std::vector<uint8_t> buf(nb * blockSize);
+  const uint64_t slots = nb * ((blockSize - CRC_SIZE) / 17 + 1);
+  std::vector<uint64_t> off(slots ? slots : 1), len(slots ? slots : 1);
+  uint64_t n = 0;
+  r.err = check(hc_wal_replay(blocks.data(), nb, blockSize, startBlock, startOffset, maxRecords, buf.data(),
+                              buf.size(), off.data(), len.data(), slots, &n, &r.posBlock, &r.posOffset,
+                              &r.badBlock),
+                "WalReplay");
+  r.records.reserve(n);
+  for (uint64_t i = 0; i < n; i++) r.records.emplace_back(buf.begin() + off[i], buf.begin() + off[i] + len[i]);
+  return r;
+}
+
 }  // namespace crc
 }  // namespace hunddb

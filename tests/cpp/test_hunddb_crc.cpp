@@ -79,6 +79,50 @@ static void cpu_tests() {
   EXPECT(crc::FixLastBlockCRC(two) == nullptr);
   EXPECT(crc::CheckBlockIntegrity(crc::ConstBytes(two.data() + 4096, 4096)) == nullptr);
 
+  // ReadFromDisk (block_manager.go:189-242) over a 6-block image
+  std::vector<uint8_t> img;
+  for (int b = 0; b < 6; b++) {
+    auto blkb = rnd(4096, 100 + b);
+    crc::AddCRCToBlockData(blkb);
+    img.insert(img.end(), blkb.begin(), blkb.end());
+  }
+  // `blocks` starts at block startOffset / blockSize (here block 1)
+  auto rr = crc::ReadFromDisk(crc::ConstBytes(img.data() + 4096, img.size() - 4096), 4096, 4096 + 2, 3 * 4092);
+  EXPECT(rr.err == nullptr && rr.data.size() == 3 * 4092);
+  EXPECT(std::memcmp(rr.data.data(), img.data() + 4096 + 4, 4092) == 0);  // clamped to offset 4
+  EXPECT(rr.finalOffset == crc::SizeAfterAddingCRCs(crc::SizeWithoutCRCs(4096 + 2) + 3 * 4092));
+  auto badimg = img;
+  badimg[3 * 4096 + 999] ^= 1;
+  int64_t badb = -2;
+  auto rb = crc::ReadFromDisk(badimg, 4096, 0, 5 * 4092, &badb);
+  EXPECT(rb.err && rb.err.Error_() == "CRC mismatch in block" && badb == 3 && rb.data.empty());
+
+  // WalReplay (wal.go:362-455): one FULL record + a 2-fragment record
+  std::vector<uint8_t> wal(3 * 4096, 0);
+  auto put_hdr = [&](size_t at, uint64_t size, uint8_t type) {
+    std::memcpy(&wal[at], &size, 8);
+    wal[at + 8] = type;
+    uint64_t log = 1;
+    std::memcpy(&wal[at + 9], &log, 8);
+  };
+  auto rec1 = rnd(100, 7);
+  put_hdr(4, rec1.size(), 4);
+  std::memcpy(&wal[4 + 17], rec1.data(), rec1.size());
+  auto rec2 = rnd(4075 + 500, 8);
+  put_hdr(4096 + 4, 4075, 1);
+  std::memcpy(&wal[4096 + 21], rec2.data(), 4075);
+  put_hdr(2 * 4096 + 4, 500, 3);
+  std::memcpy(&wal[2 * 4096 + 21], rec2.data() + 4075, 500);
+  for (int b = 0; b < 3; b++) crc::AddCRCToBlockData(crc::Bytes(wal.data() + b * 4096, 4096));
+  auto wr = crc::WalReplay(wal, 4096);
+  EXPECT(wr.err == nullptr && wr.records.size() == 2 && wr.records[0] == rec1 && wr.records[1] == rec2);
+  EXPECT(wr.posBlock == 3 && wr.posOffset == 4);
+  auto w1 = crc::WalReplay(wal, 4096, 0, 4, 1);  // memtable full after one record: next block
+  EXPECT(w1.err == nullptr && w1.records.size() == 1 && w1.posBlock == 1);
+  wal[2 * 4096 + 300] ^= 2;
+  auto wb = crc::WalReplay(wal, 4096);
+  EXPECT(wb.err && wb.err.Error_() == "CRC mismatch in block" && wb.badBlock == 2 && wb.records.size() == 1);
+
   // size helpers (float64-ceil semantics, uint64 wrap)
   EXPECT(crc::SizeAfterAddingCRCs(4092) == 4096);
   EXPECT(crc::SizeAfterAddingCRCs(4093) == 4101);
