@@ -126,6 +126,42 @@ def mixed_sizes(seed, lo, n):
 
 
 # --------------------------------------------------------------------------
+def cpu_baseline_framing(kind, dev_src, budget_s):
+    """One host thread running the oracle's restatement of the reference loop
+    (Go runs each AddCRCsToData / ReadFromDisk call on one goroutine) over a
+    256 MB sample of the same data; bytes counted as in the GPU line (read +
+    written)."""
+    import ctypes
+    import numpy as np
+    from oracle import oracle as O
+    L = O.lib()
+    nblk = (256 << 20) // 4096
+    if kind == "frame":  # crc_util.go:41-64
+        src = dev_src[: nblk * 4092].cpu().numpy()
+        dst = np.empty(nblk * 4096, dtype=np.uint8)
+        run = lambda: L.oc_add_crcs_to_data(src.ctypes.data, src.size, dst.ctypes.data)  # noqa: E731
+        per = src.size + dst.size
+        what = f"oc_add_crcs_to_data over {src.size} B of payload (crc_util.go:41-64)"
+    else:  # block_manager.go:189-242
+        blocks = dev_src[: nblk * 4096].cpu().numpy()
+        out = np.empty(nblk * 4092, dtype=np.uint8)
+        fo, bad = ctypes.c_uint64(0), ctypes.c_int64(0)
+        run = lambda: L.oc_read_from_disk(blocks.ctypes.data, blocks.size, 4096, 0, out.size,  # noqa: E731
+                                          out.ctypes.data, ctypes.byref(fo), ctypes.byref(bad))
+        per = blocks.size + out.size
+        what = f"oc_read_from_disk over {nblk} stamped 4096-B blocks (block_manager.go:189-242)"
+    run()
+    t0, passes = time.perf_counter(), 0
+    while True:
+        run()
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(passes * per / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{what}, {passes} passes in {dt:.1f} s, read+written bytes"}
+
+
 def cpu_baseline(host_sample, block, threads, budget_s):
     """The oracle's restatement of Go's amd64 crc32.ChecksumIEEE (CLMUL +
     slicing-by-8) over the same blocks, on `threads` host threads."""
@@ -299,7 +335,9 @@ def main():
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "frame", "unframe", "offlen4k"):
+        if world == 1 and args.cpu_seconds > 0 and bsize in ("frame", "unframe"):
+            cpu = cpu_baseline_framing(bsize, buf, args.cpu_seconds)
+        elif world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "offlen4k"):
             sample_blocks = min(my, (512 << 20) // bsize)
             host = buf[: sample_blocks * bsize].cpu().numpy()
             cpu = cpu_baseline(host, bsize, args.cpu_threads, args.cpu_seconds)
