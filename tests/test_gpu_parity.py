@@ -513,3 +513,43 @@ def test_offsets_beyond_2_and_4_GiB(cuda, hc, oracle, flags):
     else:
         want = oracle.crc32_blocks(host, off=hoff, lens=lens)
     assert (got == want).all(), int((got != want).sum())
+
+
+@pytest.mark.parametrize("path", ["fast", "general", "unframe"])
+def test_verify_every_block_bad(cuda, hc, path):
+    """A batch where EVERY block fails CheckBlockIntegrity (unstamped random
+    blocks, e.g. a wiped or foreign file): every bitmap bit set, first_bad 0,
+    and no serialisation of all waves on the first_bad word (each wave lowers
+    it at most once) -- the launch stays within a small factor of a clean one."""
+    import time
+    torch = cuda
+    n, B = 1_000_000, 4096
+    buf = dev_uniform(torch, hc, 4242, n, B)  # random stored words: all mismatch
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * (B - 4), dtype=torch.uint8, device="cuda") if path == "unframe" else None
+    if path == "general":  # off/len with every block 4 bytes short of a 1 KiB multiple -> k_crc_any
+        off = torch.arange(n, dtype=torch.int64, device="cuda") * B
+        lens = torch.full((n,), B - 4, dtype=torch.int32, device="cuda")
+
+    def run():
+        hc.dev_verify_prepare(bm, fb, n)
+        if path == "fast":
+            hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, bad_bitmap=bm, first_bad=fb)
+        elif path == "general":
+            hc.dev_crc32_blocks(buf, None, off=off, lens=lens, nblocks=n, bad_bitmap=bm, first_bad=fb)
+        else:
+            hc.dev_read_blocks(buf, B, out=out, bad_bitmap=bm, first_bad=fb)
+
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert int(fb.item()) == 0
+    bits = np.unpackbits(u32(bm).view(np.uint8), bitorder="little")[:n]
+    assert int(bits.sum()) == n
+    # a clean 4 GB pass takes ~0.7-1.7 ms; before the once-per-wave rule the
+    # all-bad k_unframe pass took 11 ms (1M atomics on one word)
+    assert dt < 0.008, f"{path}: {dt * 1e3:.2f} ms"
