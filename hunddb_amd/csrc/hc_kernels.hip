@@ -447,7 +447,29 @@ __device__ __forceinline__ uint4 funnel16(const uint4 a, const uint4 b, uint32_t
   }
 }
 
-template <int kBatch>
+// Buffer load of 16 bytes at byte offset `voff` of the range `r`: an offset at
+// or past the range's end returns zeros WITHOUT touching memory (the buffer
+// range check).  That is how k_crc_any predicates its loads: no branch around
+// any VMEM instruction, so hipcc's vmcnt counting stays exact across the
+// software pipeline.  aux 2 = nt (read-once data).
+__device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 2));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_range(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+
+// Pipelined per wave over its messages (blocks in block mode): the edge rows
+// of message i+1 (and its stored word) are loaded while message i is
+// finalised, and message i's first body batch while its edge rows are hashed.
+// kVar (A/B, tools/kmsg): bit 0 = issue the first body batch only when the
+// message has body rows (else out-of-range loads); bit 1 = issue it together
+// with the message's edge rows (during the previous message's finalise).
+// Production: 3 (profiles/r1/s5/kmsg_variants2.txt: best or within 1 % of the
+// best on config 5b, equal-size messages and 4092-B off/len blocks).
+template <int kBatch, int kVar = 0>
 __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, int only_nonfast,
@@ -498,148 +520,208 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
   const uint64_t b0 = uni64(nblocks * gw / W), b1 = uni64(nblocks * (gw + 1) / W);
 
+  // ---- message cursor ------------------------------------------------------
+  // The metadata of 64 messages g .. g+63 sits one per lane (one coalesced
+  // load); `todo` ballots the ones this kernel must do (only_nonfast: those
+  // the streaming kernel skipped).  Entries are read with v_readlane.
+  uint64_t g = b0, todo = 0;
+  bool loaded = false;
+  uint32_t wo_lo = 0, wo_hi = 0, wl = 0;
+  struct Msg {
+    uint64_t blk;
+    const uint8_t *p;  // block / message start
+    uint32_t l;
+    bool valid;
+  };
+  auto next = [&](Msg &mm) {
+    for (;;) {
+      if (todo) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        // readlane returns int: cast each half to uint32_t BEFORE widening, or
+        // a low word >= 2^31 sign-extends into the high word (a wild address)
+        const uint32_t o_lo = (uint32_t)__builtin_amdgcn_readlane(wo_lo, k);
+        const uint32_t o_hi = (uint32_t)__builtin_amdgcn_readlane(wo_hi, k);
+        mm.blk = g + k;
+        mm.p = base + (((uint64_t)o_hi << 32) | (uint64_t)o_lo);
+        mm.l = (uint32_t)__builtin_amdgcn_readlane(wl, k);
+        mm.valid = true;
+        return;
+      }
+      if (loaded) g += 64;
+      loaded = true;
+      if (g >= b1) {
+        mm.valid = false;
+        mm.blk = 0;
+        mm.p = base;
+        mm.l = 0;
+        return;
+      }
+      uint64_t gv = g;
+      asm volatile("" : "+s"(gv));  // window address computed afresh each refill
+      const uint64_t j = gv + lane;
+      const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
+      const uint32_t lj = j < b1 ? (lens ? lens[j] : ulen) : 0;
+      // consume the loads inside the refill branch (their vmcnt(0) stays here)
+      wo_lo = (uint32_t)oj;
+      wo_hi = (uint32_t)(oj >> 32);
+      wl = lj;
+      asm volatile("" : "+v"(wo_lo), "+v"(wo_hi), "+v"(wl));
+      const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & 1023u) == 0 && lj != 0;
+      todo = __ballot(j < b1 && !(only_nonfast && fast));
+    }
+  };
+
+  // ---- per-message geometry ------------------------------------------------
+  // Payload M (block mode: bytes [4, len); message mode: all) is hashed as the
+  // virtual message zeros(z) || W0 || M of `rows` 1 KiB rows, right-aligned so
+  // the last row ends at the payload end.  Row r, lane l covers payload
+  // offsets 1024r - z - 4 + 16l .. +15.
+  struct Geo {
+    const uint8_t *P;  // payload start
+    uint32_t Lp, rows, z, q, rb;
+    uintptr_t Abase;   // 16-B aligned start of row 0's chunks
+    bool shortblk;     // block mode, len < 4: "invalid block data"
+  };
+  auto geo = [&](const Msg &mm) {
+    Geo e;
+    e.shortblk = !msg && mm.l < 4;
+    e.P = msg ? mm.p : mm.p + 4;
+    e.Lp = msg ? mm.l : (e.shortblk ? 0u : mm.l - 4);
+    const uint64_t Lv = (uint64_t)e.Lp + 4;
+    e.rows = (uint32_t)((Lv + kRowBytes - 1) / kRowBytes);
+    e.z = (uint32_t)((uint64_t)e.rows * kRowBytes - Lv);
+    const uintptr_t A0 = (uintptr_t)e.P - e.z - 4;
+    const uint32_t m = (uint32_t)(A0 & 15u);
+    e.q = m >> 2;
+    e.rb = m & 3u;
+    e.Abase = A0 - m;
+    return e;
+  };
+  // Edge rows 0 and 1 (they may hold the virtual prefix; z + 4 <= 1027): each
+  // lane loads the two aligned 16-B chunks around its window through a range
+  // [P & ~15, roundup16(P + Lp)); chunks that do not overlap the payload get an
+  // out-of-range offset, so no byte outside the payload's aligned chunks (its
+  // own pages) is touched.  Also the stored word (block mode) through a 4-byte range.
+  auto issue_edge = [&](const Msg &mm, const Geo &e, uint4 (&ch)[4], uint32_t &sw) {
+    const uintptr_t P = (uintptr_t)e.P, Pa = P & ~(uintptr_t)15;
+    const uint64_t span = mm.valid ? (((uint64_t)P + e.Lp + 15) & ~(uint64_t)15) - Pa : 0;
+    const __amdgpu_buffer_rsrc_t re = buf_range((const void *)Pa, (uint32_t)(span < 0xFFFFFFF0ull ? span : 0xFFFFFFF0ull));
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uintptr_t X = e.Abase + (uintptr_t)r * kRowBytes + 16u * lane + 16u * h;
+        const bool in = (uint32_t)r < e.rows && X + 16 > P && X < P + e.Lp;
+        ch[2 * r + h] = buf_load16(re, in ? (uint32_t)(X - Pa) : 0xFFFFFFFFu);
+      }
+    const __amdgpu_buffer_rsrc_t rs = buf_range(mm.p, (mm.valid && !msg && !e.shortblk) ? 4u : 0u);
+    sw = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 0);
+  };
+  // Body rows >= 2 start inside the payload (2048 > z + 4): one unaligned 16-B
+  // load per lane through the range [row 2, row `rows`); rows past the end are
+  // out of range (zeros, no memory access).
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto issue_body = [&](const __amdgpu_buffer_rsrc_t rb_, uint32_t r0, u32x4 (&v)[kBatch]) {
+#pragma unroll
+    for (int b = 0; b < kBatch; b++) {
+      const uint4 t = buf_load16(rb_, (r0 + b - 2) * kRowBytes + 16u * lane);
+      v[b] = u32x4{t.x, t.y, t.z, t.w};
+    }
+  };
+  auto hash_body = [&](const Geo &e, uint32_t r0, const u32x4 (&v)[kBatch], uint32_t (&c)[4]) {
+#pragma unroll
+    for (int b = 0; b < kBatch; b++)
+      if (r0 + b < e.rows) {
+        c[0] = row_step(c[0], v[b].x);
+        c[1] = row_step(c[1], v[b].y);
+        c[2] = row_step(c[2], v[b].z);
+        c[3] = row_step(c[3], v[b].w);
+      }
+  };
+
+  Msg cur;
+  next(cur);
+  if (!cur.valid) return;
+  Geo ge = geo(cur);
+  uint4 ch[4];
+  uint32_t sw;
+  auto body_range = [&](const Geo &e) {
+    const uintptr_t A0 = e.Abase + e.q * 4 + e.rb;
+    return buf_range((const void *)(A0 + 2 * kRowBytes), e.rows > 2 ? (e.rows - 2) * kRowBytes : 0u);
+  };
+  u32x4 VA[kBatch];
+  auto issue_first = [&](const Geo &e) {
+    if (!(kVar & 1) || e.rows > 2) issue_body(body_range(e), 2, VA);
+  };
+  issue_edge(cur, ge, ch, sw);
+  if constexpr ((kVar & 2) != 0) issue_first(ge);
   bool reported = false;  // wave-uniform: this wave already lowered first_bad (see k_crc_fast)
-  for (uint64_t g = b0; g < b1; g += 64) {
-    // metadata of blocks g .. g+63, one per lane (coalesced)
-    const uint64_t j = g + lane;
-    uint64_t oj = 0;
-    uint32_t lj = 0;
-    if (j < b1) {
-      oj = offs ? offs[j] : j * stride;
-      lj = lens ? lens[j] : ulen;
+  for (;;) {
+    const __amdgpu_buffer_rsrc_t rbody = body_range(ge);
+    // the first body batch goes out before the edge rows are hashed
+    if constexpr ((kVar & 2) == 0) issue_first(ge);
+    // edge rows
+    uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      if ((uint32_t)r < ge.rows) {
+        const uint4 fw = funnel16(ch[2 * r], ch[2 * r + 1], ge.q, ge.rb);
+        uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
+        const int64_t srow = (int64_t)r * kRowBytes - (int64_t)ge.z - 4;
+        if (srow < 0) {  // zeros, then W0, then data
+          // word k2 starts d bytes before the payload: keep its bytes j >= d,
+          // and bytes ob = j - d in [-4, -1] are W0's byte ob + 4, i.e. the
+          // window of Y = W0 << 32 that starts at byte 8 - d
+          const uint64_t Y = (uint64_t)w0 << 32;
+#pragma unroll
+          for (int k2 = 0; k2 < 4; k2++) {
+            const int32_t d = -((int32_t)srow + 16 * (int32_t)lane + 4 * k2);
+            const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : 0xFFFFFFFFu << (8 * d));
+            const uint32_t wv = (d >= 1 && d <= 8) ? (uint32_t)(Y >> (64 - 8 * d)) : 0u;
+            w[k2] = (w[k2] & dm) | wv;
+          }
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < 4; k2++) c[k2] = r == 0 ? w[k2] : row_step(c[k2], w[k2]);
+      }
     }
-    const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & 1023u) == 0 && lj != 0;
-    uint64_t todo = __ballot(j < b1 && !(only_nonfast && fast));
-    while (todo) {
-      const uint32_t k = (uint32_t)__builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint64_t blk = g + k;
-      // the selected entry from lane k of the sweep (k is wave-uniform).
-      // readlane returns int: cast each half to uint32_t BEFORE widening, or
-      // a low word >= 2^31 sign-extends into the high word (a wild address).
-      const uint32_t o_lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)oj, k);
-      const uint32_t o_hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(oj >> 32), k);
-      const uint64_t o = ((uint64_t)o_hi << 32) | (uint64_t)o_lo;
-      const uint32_t l = (uint32_t)__builtin_amdgcn_readlane(lj, k);
-      const uint8_t *blkp = base + o;
-      if (!msg && l < 4) {  // "invalid block data": no CRC, always bad
-        if (lane == 0) {
-          if (crc_out) crc_out[blk] = 0;
-          if (first_bad) {
-            if (bad_bitmap) atomicOr(&bad_bitmap[blk >> 5], 1u << (blk & 31));
-            if (!reported) atomicMin(first_bad, (unsigned long long)blk);
-          }
-        }
-        reported = reported || first_bad;
-        continue;
-      }
-      const uintptr_t P = (uintptr_t)(msg ? blkp : blkp + 4);
-      const uint64_t Lp = msg ? l : l - 4;
-      const uint64_t Lv = Lp + 4;
-      const uint32_t rows = (uint32_t)((Lv + kRowBytes - 1) / kRowBytes);
-      const uint64_t z = (uint64_t)rows * kRowBytes - Lv;
-      const uintptr_t A0 = P - z - 4;
-      const uint32_t m = (uint32_t)(A0 & 15u), q = m >> 2, rb = m & 3u;
-      const uintptr_t Abase = A0 - m;
-      uint32_t c[4] = {0, 0, 0, 0};
-      {
-        // rows 0 and 1 may hold the virtual prefix (z zeros + W0; z + 4 <= 1027
-        // bytes): aligned chunks predicated on the payload range + funnel
-        // shift + masks
-        constexpr int kSlow = 2;
-        const uint32_t r0 = 0;
-        uint4 ch0[kSlow], ch1[kSlow];
-#pragma unroll
-        for (int b = 0; b < kSlow; b++) {
-          ch0[b] = ch1[b] = make_uint4(0, 0, 0, 0);
-          if (r0 + b < rows) {
-            const uintptr_t X0 = Abase + (uintptr_t)(r0 + b) * kRowBytes + 16u * lane, X1 = X0 + 16;
-            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            typedef const __attribute__((address_space(1))) v4u *g16;  // global_load, not flat_load
-            if (X0 + 16 > P && X0 < P + Lp) {
-              const v4u t = __builtin_nontemporal_load((g16)X0);
-              ch0[b] = make_uint4(t.x, t.y, t.z, t.w);
-            }
-            if (X1 + 16 > P && X1 < P + Lp) {
-              const v4u t = __builtin_nontemporal_load((g16)X1);
-              ch1[b] = make_uint4(t.x, t.y, t.z, t.w);
-            }
-          }
-        }
-#pragma unroll
-        for (int b = 0; b < kSlow; b++) {
-          if (r0 + b < rows) {
-            const uint4 fw = funnel16(ch0[b], ch1[b], q, rb);
-            uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
-            const int64_t srow = (int64_t)(r0 + b) * kRowBytes - (int64_t)z - 4;
-            if (srow < 0) {  // zeros, then W0, then data
-              // word k2 starts d bytes before the payload: keep its bytes
-              // j >= d, and bytes ob = j - d in [-4, -1] are W0's byte ob + 4,
-              // i.e. the window of Y = W0 << 32 that starts at byte 8 - d
-              const uint64_t Y = (uint64_t)w0 << 32;
-#pragma unroll
-              for (int k2 = 0; k2 < 4; k2++) {
-                const int32_t d = -((int32_t)srow + 16 * (int32_t)lane + 4 * k2);
-                const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : 0xFFFFFFFFu << (8 * d));
-                const uint32_t wv = (d >= 1 && d <= 8) ? (uint32_t)(Y >> (64 - 8 * d)) : 0u;
-                w[k2] = (w[k2] & dm) | wv;
-              }
-            }
-            if (r0 + b == 0) {
-#pragma unroll
-              for (int k2 = 0; k2 < 4; k2++) c[k2] = w[k2];
-            } else {
-#pragma unroll
-              for (int k2 = 0; k2 < 4; k2++) c[k2] = row_step(c[k2], w[k2]);
-            }
-          }
-        }
-      }
-      // rows >= 2 start inside the payload (2048 > z + 4) and the last row
-      // ends at P+Lp: one unaligned 16-B load per lane per row, no funnel, no
-      // masks
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      typedef u32x4 u32x4_u __attribute__((aligned(1)));
-      typedef const __attribute__((address_space(1))) u32x4_u *g16u;  // global_load, not flat_load
-      for (uint32_t r0 = 2; r0 < rows; r0 += kBatch) {
-        u32x4 v[kBatch];
-#pragma unroll
-        for (int b = 0; b < kBatch; b++)  // unconditional (clamped to the last row): no branch among the loads
-          v[b] = __builtin_nontemporal_load(
-              (g16u)(A0 + (uintptr_t)(r0 + b < rows ? r0 + b : rows - 1) * kRowBytes + 16u * lane));
-#pragma unroll
-        for (int b = 0; b < kBatch; b++) {
-          if (r0 + b < rows) {
-            c[0] = row_step(c[0], v[b].x);
-            c[1] = row_step(c[1], v[b].y);
-            c[2] = row_step(c[2], v[b].z);
-            c[3] = row_step(c[3], v[b].w);
-          }
-        }
-      }
-      const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-      const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
-      // stored word (block mode), read by every lane before lane 0 stamps it
-      const uint32_t st = msg ? 0u
-                              : uni((uint32_t)blkp[0] | ((uint32_t)blkp[1] << 8) | ((uint32_t)blkp[2] << 16) |
-                                    ((uint32_t)blkp[3] << 24));
-      const bool bad = !msg && first_bad && st != crcv;  // wave-uniform
-      if (lane == 0) {
-        if (crc_out) crc_out[blk] = crcv;
-        if (!msg && (flags & kFlagStamp)) {
-          uint8_t *wp = const_cast<uint8_t *>(blkp);
-          wp[0] = (uint8_t)crcv;
-          wp[1] = (uint8_t)(crcv >> 8);
-          wp[2] = (uint8_t)(crcv >> 16);
-          wp[3] = (uint8_t)(crcv >> 24);
-        }
-        if (bad) {
-          if (bad_bitmap) atomicOr(&bad_bitmap[blk >> 5], 1u << (blk & 31));
-          if (!reported) atomicMin(first_bad, (unsigned long long)blk);
-        }
-      }
-      reported = reported || bad;
+    // every edge load is consumed here on every path (rows == 1 skips row 1's
+    // hash), else the waitcnt pass assumes them pending at the loop headers
+    // below and drains the queue there (vmcnt(0))
+    asm volatile("" ::"v"(ch[0].x), "v"(ch[1].x), "v"(ch[2].x), "v"(ch[3].x), "v"(sw));
+    const uint32_t dsw = uni(sw);
+    // body rows, the next batch in flight while one is hashed
+    // (no early exit: a second half past the end loads out of range and hashes
+    // nothing, so every path through the loop has the same VMEM sequence)
+    // body rows, one batch at a time.  tools/kmsg measured this against a
+    // double-buffered loop (the next batch in flight while one is hashed):
+    // single batches were 4-12 % faster -- more bytes in flight per wave than
+    // ~4 KiB do not help at 16 waves per CU (k_crc_fast: ring 4 beat ring 8)
+    for (uint32_t r0 = 2; r0 < ge.rows; r0 += kBatch) {
+      if (r0 > 2) issue_body(rbody, r0, VA);
+      hash_body(ge, r0, VA, c);
     }
+    // the next message's edge rows go out before this one is finalised
+    const Msg done = cur;
+    const bool dshort = ge.shortblk;
+    next(cur);
+    ge = geo(cur);
+    issue_edge(cur, ge, ch, sw);
+    if constexpr ((kVar & 2) != 0) issue_first(ge);
+
+    const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+    const uint32_t crcv = dshort ? 0u : wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    const bool bad = !msg && first_bad && (dshort || dsw != crcv);  // wave-uniform
+    if (crc_out) lane0_store_u32(crc_out + done.blk, crcv);
+    if (!msg && !dshort && (flags & kFlagStamp))  // PutUint32LE(block[0:4], crc)
+      lane0_store_u32(reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(done.p)), crcv);
+    if (bad) {
+      if (bad_bitmap) lane0_atomic_or(bad_bitmap + (done.blk >> 5), 1u << (done.blk & 31));
+      if (!reported) lane0_atomic_umin64(first_bad, done.blk);
+      reported = true;
+    }
+    if (!cur.valid) return;
   }
 }
 
@@ -1005,7 +1087,7 @@ hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t 
 }
 
 hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_crc_any<4>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+  hipLaunchKernelGGL((k_crc_any<4, 3>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
                      b.ulen, b.flags, b.nblocks, only_nonfast ? 1 : 0, b.crc_out, b.bad_bitmap, b.first_bad,
                      b.tables);
   return hipGetLastError();
