@@ -1,8 +1,26 @@
 // hc_wal.cpp — WAL recovery over a run of written WAL blocks (row f3):
 // lsm/wal/wal.go:362-455 (recoverMemtable + processBlockForRecovery) with the
 // per-block CheckBlockIntegrity replaced by one verify batch (hc_verify_blocks).
+//
+// Everything but a short sequential pass runs in parallel over contiguous
+// block ranges (a block always starts with a header, so ranges scan
+// independently):
+//   A. per range (T threads): scan the blocks and merge their pieces into
+//      records locally.  Only the range's "head" depends on the fragments
+//      still pending from earlier ranges: the FIRST/MIDDLE pieces before the
+//      range's first reset point (a LAST, which consumes the pending
+//      fragments, or a padding tail, which clears them -- wal.go:415-419).
+//   B. sequential over ranges: carry the pending fragments through the heads,
+//      number the records and apply the stops (framing error, memtable full,
+//      output capacity) -- O(ranges), plus one walk over the records of the
+//      range where a stop falls.
+//   C. per range (T threads): write rec_off/rec_len and copy the bytes out.
+// The verify batch runs on the calling thread meanwhile (GPU from 256 blocks);
+// the result is cut where the Go loop would have stopped: at the first bad block.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -12,28 +30,76 @@
 using namespace hc;
 
 namespace {
-// One parsed piece of a WAL block (wal_header.go:5-23 framing).
-struct WalItem {
-  enum Kind : uint8_t { kFull, kFrag, kLast, kClear, kErrType, kErrTrunc } kind;
-  uint64_t blk;
-  uint32_t hdr;  // offset of the piece's header in its block (or of the error)
-  uint32_t pay;  // payload offset
-  uint64_t len;  // payload length
+struct Piece {
+  const uint8_t *p;
+  uint64_t len;
 };
 
-// processBlockForRecovery (wal.go:412-453) for one block, as items.  Returns
-// false after an error item (the caller stops scanning).
-bool wal_scan_block(const uint8_t *b, uint32_t bs, uint64_t blk, uint64_t off, std::vector<WalItem> &out) {
-  // the rest of the block is padding iff off > last non-zero byte (:415-419)
+// Fragments waiting for their LAST (Go's fragmentBuffer), as piece references.
+struct Pending {
+  std::vector<Piece> pieces;
+  uint64_t len = 0;
+  uint64_t blk = 0;  // header position of the first pending piece
+  uint32_t hdr = 0;
+  void add(const Piece &q, uint64_t b, uint32_t h) {
+    if (pieces.empty()) {
+      blk = b;
+      hdr = h;
+    }
+    pieces.push_back(q);
+    len += q.len;
+  }
+  void clear() {
+    pieces.clear();
+    len = 0;
+  }
+};
+
+struct Rec {
+  uint64_t piece0;     // first piece in Range::pieces
+  uint32_t npieces;
+  bool head;           // the head LAST: the pending fragments of earlier ranges go first
+  uint64_t len;        // bytes (a head record: without that incoming prefix until phase B)
+  uint64_t start_blk;  // where the record starts (resume position when it does not fit)
+  uint32_t start_hdr;
+  uint64_t done_blk;   // block in which it completes
+};
+
+struct Range {
+  std::vector<Piece> pieces;
+  std::vector<Rec> recs;
+  bool reset = false;  // the range has a LAST or a padding tail
+  Pending head;        // FIRST/MIDDLE pieces before the first reset
+  Pending tail;        // pieces after the last reset (pending at the range end)
+  int64_t head_rec = -1;
+  bool err = false;
+  int err_code = HC_OK;
+  uint64_t err_blk = 0, err_hdr = 0;
+  uint64_t bytes = 0;  // sum of local record lengths
+  // phase B
+  std::vector<Piece> prefix;  // incoming pending pieces of the head record
+  uint64_t keep = 0;          // records kept
+  uint64_t rec_base = 0, byte_base = 0;
+};
+
+// processBlockForRecovery (wal.go:412-453) for one block, feeding the range's
+// local merge.  Returns false after a framing error (the range stops there).
+bool scan_block(Range &R, const uint8_t *b, uint32_t bs, uint64_t blk, uint64_t off) {
+  // the rest of the block is padding iff off > its last non-zero byte (:415-419)
   int64_t last = (int64_t)bs - 1;
   while (last >= 0 && b[last] == 0) last--;
   while (off < bs) {
-    if ((int64_t)off > last) {
-      out.push_back({WalItem::kClear, blk, (uint32_t)off, 0, 0});
+    if ((int64_t)off > last) {  // fragmentBuffer = fragmentBuffer[:0]
+      if (R.reset)
+        R.tail.clear();
+      R.reset = true;  // the head ends here (cleared: the incoming pending dies)
       return true;
     }
     if (off + 17 > bs) {  // DeserializeWALHeader returns nil; Go then panics
-      out.push_back({WalItem::kErrTrunc, blk, (uint32_t)off, 0, 0});
+      R.err = true;
+      R.err_code = HC_ERR_WAL_TRUNCATED;
+      R.err_blk = blk;
+      R.err_hdr = off;
       return false;
     }
     uint64_t size;
@@ -42,21 +108,44 @@ bool wal_scan_block(const uint8_t *b, uint32_t bs, uint64_t blk, uint64_t off, s
     const uint32_t hdr = (uint32_t)off;
     off += 17;
     if (size > bs - off) {  // block[offset:offset+size] out of range: Go panics
-      out.push_back({WalItem::kErrTrunc, blk, (uint32_t)off, 0, 0});
+      R.err = true;
+      R.err_code = HC_ERR_WAL_TRUNCATED;
+      R.err_blk = blk;
+      R.err_hdr = off;
       return false;
     }
-    WalItem::Kind k;
-    if (type == 4) k = WalItem::kFull;                      // FRAGMENT_FULL
-    else if (type == 1 || type == 2) k = WalItem::kFrag;    // FIRST, MIDDLE
-    else if (type == 3) k = WalItem::kLast;                 // LAST
-    else {
-      out.push_back({WalItem::kErrType, blk, (uint32_t)(off + size), 0, 0});
+    const Piece q{b + off, size};
+    if (type == 4) {  // FRAGMENT_FULL: Put(payload); the fragment buffer is untouched
+      R.recs.push_back({R.pieces.size(), 1, false, size, blk, hdr, blk});
+      R.pieces.push_back(q);
+      R.bytes += size;
+    } else if (type == 1 || type == 2) {  // FIRST, MIDDLE: append
+      (R.reset ? R.tail : R.head).add(q, blk, hdr);
+    } else if (type == 3) {  // LAST: record = fragment buffer + payload, buffer cleared
+      Pending &pd = R.reset ? R.tail : R.head;
+      Rec r{R.pieces.size(), (uint32_t)pd.pieces.size() + 1, !R.reset, pd.len + size,
+            pd.pieces.empty() ? blk : pd.blk, pd.pieces.empty() ? hdr : pd.hdr, blk};
+      R.pieces.insert(R.pieces.end(), pd.pieces.begin(), pd.pieces.end());
+      R.pieces.push_back(q);
+      if (!R.reset) R.head_rec = (int64_t)R.recs.size();
+      R.recs.push_back(r);
+      R.bytes += r.len;
+      if (R.reset) R.tail.clear();
+      R.reset = true;  // (head pieces stay in R.head for phase B's start position)
+    } else {
+      R.err = true;
+      R.err_code = HC_ERR_WAL_FRAGMENT_TYPE;
+      R.err_blk = blk;
+      R.err_hdr = off + size;
       return false;
     }
-    out.push_back({k, blk, hdr, (uint32_t)off, size});
     off += size;
   }
   return true;
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 }  // namespace
 
@@ -74,21 +163,23 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   if (start_block >= nblocks) return HC_OK;
   const uint64_t n = nblocks - start_block;
   const uint8_t *base = blocks + start_block * bs;
-  // The verify batch (wal.go:383; GPU from 256 blocks) runs on the calling
-  // thread while a second thread scans, merges and copies the records out
-  // without waiting for it (none of that depends on the CRCs).  The result is
-  // then cut where the Go loop would have stopped: at the first bad block.
   static const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", 256);
   static const int threads_cfg = std::max(1, env_int("HC_WAL_THREADS", 16));  // 16: the GPU box's CPU share
-  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, n / 64));
+  static const int trace = env_int("HC_WAL_TRACE", 0);
+  // blocks per range at least HC_WAL_MIN_RANGE (64; read per call so tests can
+  // force many small ranges and exercise the cross-range merge)
+  const uint64_t min_range = (uint64_t)std::max(1, env_int("HC_WAL_MIN_RANGE", 64));
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, n / min_range));
+  const bool have_out = rec_buf && rec_off && rec_len;
   int64_t first_bad = -1;
   int vrc = HC_OK;
-  // merge outcome
   enum Stop { kAll, kErr, kFull, kCap } stop = kAll;
-  uint64_t stop_blk = 0;  // block of the error / of the record that filled the memtable / of the record that did not fit
+  uint64_t stop_blk = 0;  // block of the error / of the record that filled the memtable / that did not fit
   int err_code = HC_OK;
-  uint64_t pb = 0, po = HC_CRC_SIZE, count = 0;
-  std::vector<uint64_t> rec_done_blk;  // block in which each record completed
+  uint64_t pb = start_block + n, po = HC_CRC_SIZE, count = 0;
+  std::vector<Range> R(T);
+  int last_range = T - 1;  // ranges after a stop are not used
+  double t0 = now_s(), tv = 0, ta = 0, tb = 0, tc = 0;
   parallel_for(2, [&](int role) {
     if (role == 0) {
       if (n >= gpu_min || force_gpu()) {
@@ -97,91 +188,107 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
         for (uint64_t i = 0; i < n && first_bad < 0; i++)
           if (hc_check_block(base + i * bs, bs) != HC_OK) first_bad = (int64_t)i;
       }
+      tv = now_s() - t0;
       return;
     }
-    // 1. scan the blocks into items, T threads over contiguous block ranges
-    std::vector<std::vector<WalItem>> items(T);
+    // A. scan + local merge per range
     parallel_for(T, [&](int t) {
       const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
-      items[t].reserve((hi - lo) * 2 + 4);
+      R[t].pieces.reserve((hi - lo) * 2 + 4);
+      R[t].recs.reserve((hi - lo) + 4);
       for (uint64_t i = lo; i < hi; i++)
-        if (!wal_scan_block(base + i * bs, block_size, start_block + i, i == 0 ? start_offset : HC_CRC_SIZE,
-                            items[t]))
+        if (!scan_block(R[t], base + i * bs, block_size, start_block + i, i == 0 ? start_offset : HC_CRC_SIZE))
           break;
     });
-    // 2. sequential merge: fragment reassembly, memtable-full stop, capacity stop
-    struct Piece {
-      const uint8_t *p;
-      uint64_t len, dst;
-    };
-    std::vector<Piece> pieces, pending;
-    uint64_t used = 0, pend_len = 0, pend_blk = 0, pend_hdr = 0;
-    pb = start_block + n;
-    auto emit = [&](const WalItem &it, uint64_t first_blk, uint64_t first_hdr) -> bool {
-      const uint64_t len = pend_len + it.len;
-      if (count >= rec_slots || used + len > rec_buf_cap || !rec_buf || !rec_off || !rec_len) {
-        stop = kCap;  // resumable: the record starts at (first_blk, first_hdr)
-        stop_blk = first_blk;
-        pb = first_blk;
-        po = first_hdr;
-        return false;
-      }
-      rec_off[count] = used;
-      rec_len[count] = len;
-      for (auto &q : pending) {
-        pieces.push_back({q.p, q.len, used});
-        used += q.len;
-      }
-      pieces.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, used});
-      used += it.len;
-      rec_done_blk.push_back(it.blk);
-      count++;
-      pending.clear();
-      pend_len = 0;
-      return true;
-    };
+    ta = now_s() - t0;
+    // B. pending fragments through the heads, numbering, stops
+    Pending pend;
+    uint64_t used = 0;
     for (int t = 0; t < T && stop == kAll; t++) {
-      for (const WalItem &it : items[t]) {
-        if (it.kind == WalItem::kClear) {
-          pending.clear();
-          pend_len = 0;
-          continue;
+      Range &G = R[t];
+      last_range = t;
+      if (G.head_rec >= 0) {  // the head LAST takes the incoming fragments first
+        Rec &h = G.recs[(size_t)G.head_rec];
+        G.prefix = pend.pieces;
+        h.len += pend.len;
+        G.bytes += pend.len;
+        if (!pend.pieces.empty()) {
+          h.start_blk = pend.blk;
+          h.start_hdr = pend.hdr;
         }
-        if (it.kind == WalItem::kErrType || it.kind == WalItem::kErrTrunc) {
-          stop = kErr;
-          stop_blk = it.blk;
-          err_code = it.kind == WalItem::kErrType ? HC_ERR_WAL_FRAGMENT_TYPE : HC_ERR_WAL_TRUNCATED;
-          pb = it.blk;
-          po = it.hdr;
-          break;
-        }
-        if (it.kind == WalItem::kFrag) {
-          if (pending.empty()) {
-            pend_blk = it.blk;
-            pend_hdr = it.hdr;
+      }
+      if (G.reset) {
+        pend = G.tail;
+      } else {
+        for (size_t i = 0; i < G.head.pieces.size(); i++)
+          pend.add(G.head.pieces[i], G.head.blk, G.head.hdr);
+      }
+      G.rec_base = count;
+      G.byte_base = used;
+      const uint64_t nr = G.recs.size();
+      const bool fits_all = have_out && count + nr <= rec_slots && used + G.bytes <= rec_buf_cap;
+      const bool fills = max_records && count + nr >= max_records;
+      if (fits_all && !fills) {
+        G.keep = nr;
+        count += nr;
+        used += G.bytes;
+      } else {  // a stop falls in this range: walk its records
+        G.keep = 0;
+        for (const Rec &r : G.recs) {
+          if (!have_out || count >= rec_slots || used + r.len > rec_buf_cap) {
+            stop = kCap;  // resumable: the record starts at (start_blk, start_hdr)
+            stop_blk = r.start_blk;
+            pb = r.start_blk;
+            po = r.start_hdr;
+            break;
           }
-          pending.push_back({base + (it.blk - start_block) * bs + it.pay, it.len, 0});
-          pend_len += it.len;
-          continue;
+          G.keep++;
+          count++;
+          used += r.len;
+          if (max_records && count >= max_records) {  // memtable.IsFull: next block (wal.go:392-397)
+            stop = kFull;
+            stop_blk = r.done_blk;
+            pb = r.done_blk + 1;
+            po = HC_CRC_SIZE;
+            break;
+          }
         }
-        const bool frag = it.kind == WalItem::kLast && !pending.empty();
-        if (!emit(it, frag ? pend_blk : it.blk, frag ? pend_hdr : it.hdr)) break;
-        if (max_records && count >= max_records) {  // memtable.IsFull: next block (wal.go:392-397)
-          stop = kFull;
-          stop_blk = it.blk;
-          pb = it.blk + 1;
-          po = HC_CRC_SIZE;
-          break;
-        }
+      }
+      if (stop == kAll && G.err) {
+        stop = kErr;
+        stop_blk = G.err_blk;
+        err_code = G.err_code;
+        pb = G.err_blk;
+        po = G.err_hdr;
       }
     }
-    // 3. copy the record bytes out, T threads
-    const int C = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)T, used >> 22));
-    parallel_for(C, [&](int t) {
-      const uint64_t lo = pieces.size() * t / C, hi = pieces.size() * (t + 1) / C;
-      for (uint64_t i = lo; i < hi; i++) std::memcpy(rec_buf + pieces[i].dst, pieces[i].p, pieces[i].len);
+    tb = now_s() - t0;
+    // C. offsets, lengths and record bytes, per range
+    parallel_for(last_range + 1, [&](int t) {
+      Range &G = R[t];
+      uint64_t o = G.byte_base;
+      for (uint64_t i = 0; i < G.keep; i++) {
+        const Rec &r = G.recs[i];
+        rec_off[G.rec_base + i] = o;
+        rec_len[G.rec_base + i] = r.len;
+        if (r.head)
+          for (const Piece &q : G.prefix) {
+            std::memcpy(rec_buf + o, q.p, q.len);
+            o += q.len;
+          }
+        for (uint32_t k = 0; k < r.npieces; k++) {
+          const Piece &q = G.pieces[r.piece0 + k];
+          std::memcpy(rec_buf + o, q.p, q.len);
+          o += q.len;
+        }
+      }
     });
+    tc = now_s() - t0;
   });
+  if (trace)
+    std::fprintf(stderr, "[hc_wal_replay] %llu blocks, %d ranges: verify %.3f s, scan+merge %.3f s, "
+                 "resolve %.3f s, copy-out %.3f s (from the call start)\n",
+                 (unsigned long long)n, T, tv, ta, tb, tc);
   if (vrc < 0) return vrc;
   int code = stop == kErr ? err_code : HC_OK;
   if (first_bad >= 0) {
@@ -189,7 +296,15 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
     // the Go loop checks a block's CRC before parsing it: a stop at or after
     // the bad block did not happen, and no record completing there exists
     if (stop == kAll || stop_blk >= B) {
-      while (count > 0 && rec_done_blk[count - 1] >= B) count--;
+      uint64_t keep = 0;
+      for (int t = 0; t <= last_range; t++) {
+        const Range &G = R[t];
+        uint64_t k = 0;
+        while (k < G.keep && G.recs[k].done_blk < B) k++;
+        keep += k;
+        if (k < G.keep) break;
+      }
+      count = keep;
       code = HC_ERR_CRC_MISMATCH;
       if (bad_block) *bad_block = (int64_t)B;
       pb = B;
@@ -201,4 +316,3 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   *pos_offset = po;
   return code;
 }
-

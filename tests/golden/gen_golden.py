@@ -350,8 +350,32 @@ def main():
     b[4:21] = struct.pack("<QBQ", 5000, 4, 1)            # payload past the block end
     b[21] = 1
     odd["truncated_payload"] = bytes(add_crc_to_block_data(b))
+    # hand-built multi-block images: a FULL between fragments leaves the fragment
+    # buffer alone (wal.go:432-437); padding clears it (:415-419); a LAST with
+    # nothing pending is a record by itself
+    def wal_block(items, pad_tail=True):
+        b = bytearray(4096)
+        off = 4
+        for typ, pay in items:
+            b[off:off + 17] = struct.pack("<QBQ", len(pay), typ, 1)
+            b[off + 17:off + 17 + len(pay)] = pay
+            off += 17 + len(pay)
+        return bytes(add_crc_to_block_data(b))
+    pb = lambda k, n: bytes(((i * 13 + k * 29 + 1) & 0xFF) or 1 for i in range(n))  # noqa: E731
+    multi = {
+        # (block 1 is filled to its end: no padding between the fragments)
+        "full_between_fragments": [wal_block([(1, pb(1, 300)), (4, pb(2, 200)), (2, pb(3, 4092 - 51 - 500))]),
+                                   wal_block([(4, pb(4, 50)), (3, pb(5, 70)), (4, pb(6, 10))])],
+        "padding_clears_fragments": [wal_block([(4, pb(1, 40)), (1, pb(2, 500))]),
+                                     wal_block([(3, pb(3, 60)), (1, pb(4, 30)), (3, pb(5, 30))])],
+        "last_without_first": [wal_block([(3, pb(1, 80)), (3, pb(2, 90))]),
+                               wal_block([(2, pb(3, 4075))]),
+                               wal_block([(3, pb(4, 20)), (4, pb(5, 5))])],
+    }
+    for name, bl in multi.items():
+        odd[name] = b"".join(bl)
     for name, blk in odd.items():
-        recs, err, bad, pos = wal_replay([blk], 4096)
+        recs, err, bad, pos = wal_replay([blk[i:i + 4096] for i in range(0, len(blk), 4096)], 4096)
         rep[f"hand/{name}"] = {"block_hex": blk.hex(), "max_records": 0, "err": err, "bad_block": bad,
                                "pos": list(pos), "lens": [len(r) for r in recs],
                                "sha256": [sha(r) for r in recs]}

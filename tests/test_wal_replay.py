@@ -1,7 +1,7 @@
 """Row f3: WAL recovery (lsm/wal/wal.go:362-455) through hc_wal_replay.
 
-The product path (one verify batch + parallel block scan + sequential
-fragment merge) against the golden replay fixtures and the oracle's
+The product path (one verify batch + per-range scan and merge + a short
+sequential pass over the ranges + parallel copy-out) against the golden replay fixtures and the oracle's
 sequential restatement, on WAL images framed exactly as wal.go:177-283
 (oracle oc_wal_frame).  Host-only sizes here (< 256 blocks verify on the CPU);
 the GPU-verified sizes are in test_gpu_parity.py.
@@ -14,7 +14,15 @@ import pytest
 from test_oracle import ERRS, _replay_case_blocks
 
 
-def test_wal_replay_golden(hc, oracle, golden):
+@pytest.fixture(params=[64, 3, 1], ids=["range64", "range3", "range1"])
+def ranges(request, monkeypatch):
+    """Blocks per parallel range (HC_WAL_MIN_RANGE): 1 and 3 put range
+    boundaries inside fragmented records, so the cross-range merge runs."""
+    monkeypatch.setenv("HC_WAL_MIN_RANGE", str(request.param))
+    return request.param
+
+
+def test_wal_replay_golden(hc, oracle, golden, ranges):
     for name, c in golden["wal_replay"].items():
         blocks = _replay_case_blocks(oracle, golden, c)
         recs, err, bad, pos = hc.wal_replay(blocks, 4096, max_records=c["max_records"])
@@ -33,7 +41,7 @@ def _image(oracle, seed, nrec, lo=64, hi=20000):
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_wal_replay_vs_oracle(hc, oracle, seed):
+def test_wal_replay_vs_oracle(hc, oracle, seed, ranges):
     img, sizes, st = _image(oracle, seed, 120)
     nb = len(img) // 4096
     rng = np.random.default_rng(seed)
@@ -63,7 +71,7 @@ def test_wal_replay_records_match_writer(hc, oracle):
     assert [len(r) for r in recs] == kept
 
 
-def test_wal_replay_capacity_resume(hc, oracle):
+def test_wal_replay_capacity_resume(hc, oracle, ranges):
     """Output capacity smaller than the image: resuming at the returned position
     yields exactly the unlimited replay's records."""
     img, sizes, st = _image(oracle, 9, 150)
@@ -83,3 +91,46 @@ def test_wal_replay_capacity_resume(hc, oracle):
 def test_wal_replay_bad_args(hc):
     with pytest.raises(hc.HundCRCError):
         hc.wal_replay(bytes(4096), 4096, 0, 0)   # start_offset < CRC_SIZE
+
+
+def _random_image(rng, nblocks, bs=4096):
+    """Blocks of random FIRST/MIDDLE/LAST/FULL pieces (any order, not only what
+    the writer produces), some ending in padding, some filled to the end."""
+    import struct
+    import zlib
+    out = bytearray()
+    for _ in range(nblocks):
+        b = bytearray(bs)
+        off = 4
+        while off + 17 < bs:
+            if rng.random() < 0.15:  # padding tail
+                break
+            room = bs - off - 17
+            size = int(rng.integers(0, min(room, 1500) + 1)) if rng.random() < 0.8 else room
+            typ = int(rng.choice([1, 2, 3, 4]))
+            b[off:off + 17] = struct.pack("<QBQ", size, typ, 7)
+            b[off + 17:off + 17 + size] = rng.integers(1, 256, size, dtype=np.uint8).tobytes()
+            off += 17 + size
+        b[0:4] = struct.pack("<I", zlib.crc32(bytes(b[4:])))
+        out += b
+    return bytes(out)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_wal_replay_random_pieces_vs_oracle(hc, oracle, seed, ranges):
+    """Arbitrary piece sequences across blocks (FULL between fragments, LAST
+    with nothing pending, padding clearing fragments) through the per-range
+    merge, against the oracle's sequential restatement of wal.go:362-455;
+    with memtable-full stops, start offsets and a corrupt block."""
+    rng = np.random.default_rng(100 + seed)
+    img = _random_image(rng, 40)
+    nb = len(img) // 4096
+    for sb, mr, corrupt in [(0, 0, None), (int(rng.integers(1, nb)), 0, None), (0, int(rng.integers(1, 30)), None),
+                            (0, 0, int(rng.integers(0, nb)))]:
+        view = bytearray(img)
+        if corrupt is not None:
+            view[corrupt * 4096 + 9] ^= 0x40
+        want, wrc, wbad, wpos = oracle.wal_replay(bytes(view), 4096, sb, 4, mr)
+        got, err, bad, pos = hc.wal_replay(bytes(view), 4096, sb, 4, mr)
+        assert (0 if err is None else err.code) == wrc
+        assert got == want and pos == wpos and bad == wbad
