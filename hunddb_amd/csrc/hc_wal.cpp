@@ -24,6 +24,8 @@
 #include <cstring>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "../../include/hundcrc.h"
 #include "hc_util.hpp"
 
@@ -142,6 +144,33 @@ bool scan_block(Range &R, const uint8_t *b, uint32_t bs, uint64_t blk, uint64_t 
     off += size;
   }
   return true;
+}
+
+// Record bytes are written once and not read back here: non-temporal 16-B
+// stores skip the write-allocate read of every destination line, which would
+// otherwise compete for host memory bandwidth with the verify batch's DMA of
+// the same image.
+void copy_nt(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  if (n < 64) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  for (; n >= 64; n -= 64, dst += 64, src += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 48), d);
+  }
+  std::memcpy(dst, src, n);
 }
 
 double now_s() {
@@ -273,15 +302,16 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
         rec_len[G.rec_base + i] = r.len;
         if (r.head)
           for (const Piece &q : G.prefix) {
-            std::memcpy(rec_buf + o, q.p, q.len);
+            copy_nt(rec_buf + o, q.p, q.len);
             o += q.len;
           }
         for (uint32_t k = 0; k < r.npieces; k++) {
           const Piece &q = G.pieces[r.piece0 + k];
-          std::memcpy(rec_buf + o, q.p, q.len);
+          copy_nt(rec_buf + o, q.p, q.len);
           o += q.len;
         }
       }
+      _mm_sfence();  // the streamed stores are visible before the call returns
     });
     tc = now_s() - t0;
   });
