@@ -553,3 +553,53 @@ def test_verify_every_block_bad(cuda, hc, path):
     # a clean 4 GB pass takes ~0.7-1.7 ms; before the once-per-wave rule the
     # all-bad k_unframe pass took 11 ms (1M atomics on one word)
     assert dt < 0.008, f"{path}: {dt * 1e3:.2f} ms"
+
+
+def test_config4_full_size_sampled_and_sharded(cuda, hc, oracle):
+    """configs[3] at full size on one GPU: 16M x 8 KiB = 131 GB resident.
+    The oracle re-generates 20k sampled blocks on the host (the fill is keyed by
+    block index) and checks their CRC words; the index-sharded launches of 8
+    ranks (hunddb_amd.shard.index_range, what bench.py --gpus 8 runs) give the
+    same words as the whole batch; a stamp -> verify pass over all 131 GB finds
+    exactly the blocks corrupted at far-apart indices (block offsets past 2^32
+    and 2^36 bytes)."""
+    import ctypes
+    from hunddb_amd import shard
+    torch = cuda
+    n, B, seed = 16_000_000, 8192, 0x48756E64
+    buf = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+    hc.dev_fill_blocks(buf, seed, stride=B, ulen=B, nblocks=n)
+    whole = torch.empty(n, dtype=torch.int32, device="cuda")
+    hc.dev_crc32_blocks(buf, whole, stride=B, ulen=B, nblocks=n)
+    assert hc.last_launch()["kernel"] == "k_crc_fast"
+    parts = torch.empty(n, dtype=torch.int32, device="cuda")
+    for r in range(8):
+        lo, hi = shard.index_range(n, 8, r)
+        hc.dev_crc32_blocks(buf[lo * B:hi * B], parts[lo:hi], stride=B, ulen=B, nblocks=hi - lo)
+    torch.cuda.synchronize()
+    assert torch.equal(whole, parts)
+    got = u32(whole)
+    rng = np.random.default_rng(4)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 20_000), [0, 1, n // 2, n - 2, n - 1]]))
+    host = np.empty(B, dtype=np.uint8)
+    L = oracle.lib()
+    want = np.empty(idx.size, dtype=np.uint32)
+    for k, i in enumerate(idx):
+        L.oc_fill_block(seed, int(i), host.ctypes.data, B)
+        want[k] = oracle.crc32_blocks(host, stride=B, ulen=B)[0]
+    assert np.array_equal(got[idx], want)
+    # stamp all, corrupt a few far-apart blocks, verify all
+    hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, flags=hc.HC_F_STAMP)
+    victims = [524_289, 8_388_609, n - 1]  # byte offsets > 2^32, > 2^36, the last block
+    for v in victims:
+        buf[v * B + 4000] ^= 1
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == victims[0]
+    bits = np.unpackbits(u32(bm).view(np.uint8), bitorder="little")[:n]
+    assert np.nonzero(bits)[0].tolist() == victims
+    del buf
+    torch.cuda.empty_cache()
