@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -255,7 +256,7 @@ int main(int argc, char **argv) {
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
-  std::vector<Case> cases(3);
+  std::vector<Case> cases(4);
   uint64_t seed = 0x57414C;
   cases[0].name = "config5b: log-uniform 64 B-64 KiB messages";
   cases[0].flags = hc::kFlagMessages;
@@ -263,6 +264,8 @@ int main(int argc, char **argv) {
   cases[1].flags = hc::kFlagMessages;
   cases[2].name = "4092-B blocks via off/len, verify";
   cases[2].flags = 0;
+  cases[3].name = "config5b sizes, byte-balanced per wave";
+  cases[3].flags = hc::kFlagMessages;
   uint64_t maxb = 0;
   for (int c = 0; c < 3; c++) {
     Case &k = cases[c];
@@ -283,6 +286,34 @@ int main(int argc, char **argv) {
     }
     k.bytes = o;
     maxb = std::max(maxb, o);
+  }
+  {  // case 3: config 5b's sizes dealt so that every wave's contiguous run has
+     // about the same bytes (greedy, largest first, into the kernel's per-wave
+     // index ranges): the imbalance share of config 5b's gap
+    const uint64_t W = (uint64_t)cus * hc::kFastWaves;
+    std::vector<uint32_t> sz(cases[0].len);
+    std::sort(sz.begin(), sz.end(), std::greater<uint32_t>());
+    std::vector<uint64_t> sum(W, 0), cnt(W, 0), cap(W);
+    for (uint64_t w = 0; w < W; w++) cap[w] = N * (w + 1) / W - N * w / W;
+    std::vector<std::vector<uint32_t>> bins(W);
+    typedef std::pair<uint64_t, uint64_t> E;
+    std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+    for (uint64_t w = 0; w < W; w++) pq.push({0, w});
+    for (uint32_t l : sz) {
+      E e = pq.top();
+      pq.pop();
+      bins[e.second].push_back(l);
+      if (bins[e.second].size() < cap[e.second]) pq.push({e.first + l, e.second});
+    }
+    Case &k = cases[3];
+    uint64_t o = 0;
+    for (uint64_t w = 0; w < W; w++)
+      for (uint32_t l : bins[w]) {
+        k.off.push_back(o);
+        k.len.push_back(l);
+        o += l;
+      }
+    k.bytes = o;
   }
   std::printf("device %s (%s), %d CUs; %llu messages per case\n", prop.name, prop.gcnArchName, cus,
               (unsigned long long)N);
