@@ -117,6 +117,14 @@ def _lib():
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_device_count": (I, []),
+            "hc_md5": (None, [P, S, P]),
+            "hc_md5_messages": (I, [P, P, P, U64, P]),
+            "hc_dev_md5_messages": (I, [I, P, P, P, U64, U32, U64, P, P, P]),
+            "hc_merkle_nodes": (U64, [U64]),
+            "hc_merkle_levels": (I, [P, U64, P]),
+            "hc_dev_merkle_levels": (I, [I, P, U64, P]),
+            "hc_merkle_serialize": (I, [P, U64, P, U64, P]),
+            "hc_merkle_validate": (I, [P, U64, P, U64, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

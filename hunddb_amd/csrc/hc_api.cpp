@@ -97,7 +97,27 @@ int init_device(int dev) {
 
 int default_device() { return env_int("HC_DEVICE", 0); }
 
+}  // namespace
+
+namespace hc {
+// for the other translation units (hc_merkle.cpp): init + CU count
+int dev_init(int device, int *cus) {
+  const int st = init_device(device);
+  if (st == HC_OK && cus) *cus = g_dev[device].cus;
+  return st;
+}
+void set_last_launch(const hc_launch_info &info);
+}  // namespace hc
+
+namespace {
+
 thread_local hc_launch_info t_last{"", 0, 0, 0, 0, 0, 0};
+
+}  // namespace
+
+void hc::set_last_launch(const hc_launch_info &info) { t_last = info; }
+
+namespace {
 
 // ---------------------------------------------------------------------------
 // Device batch dispatch (shared by _dev_ entries and the host pipeline)
@@ -165,6 +185,8 @@ struct Slot {
   hipEvent_t done = nullptr;
   uint64_t i0 = 0, nb = 0;  // block range of the in-flight chunk
   bool busy = false;
+  // MD5 batches (row f4), allocated on first use: tail workspace and digests
+  uint8_t *dtail = nullptr, *dmd5 = nullptr, *pin_md5 = nullptr;
 };
 
 struct HostPipe {
@@ -212,6 +234,9 @@ struct HostPipe {
       if (s.doff) (void)hipFree(s.doff);
       if (s.dlen) (void)hipFree(s.dlen);
       if (s.dcrc) (void)hipFree(s.dcrc);
+      if (s.dtail) (void)hipFree(s.dtail);
+      if (s.dmd5) (void)hipFree(s.dmd5);
+      if (s.pin_md5) (void)hipHostFree(s.pin_md5);
       if (s.stream) (void)hipStreamDestroy(s.stream);
       if (s.done) (void)hipEventDestroy(s.done);
       s = Slot{};
@@ -240,14 +265,25 @@ thread_local uint64_t t_host_bytes = 0;  // bytes moved by the last host batch (
 // Runs CRCs of host blocks on the GPU; results into crc_out[0..n).  Blocks
 // larger than one staging slot are rejected (HC_E_ARG): the on-disk block
 // sizes are 4-16 KiB (utils/config/config.go:137, README.md:191,255).
+// md5_out != nullptr: MD5 digests of whole messages instead (row f4; crc_out unused).
+constexpr uint64_t kMd5MaxPerChunk = 262144;  // bounds the 128 B/message tail workspace per slot
 int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
-               uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t flags) {
+               uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t flags, uint8_t *md5_out = nullptr) {
   const int dev = default_device();
   int st = init_device(dev);
   if (st != HC_OK) return st;
   HostPipe &P = t_pipe;
   if ((st = P.init(dev)) != HC_OK) return st;
   DeviceGuard g(dev);
+  const bool md5 = md5_out != nullptr;
+  const uint64_t maxmsg = md5 ? std::min<uint64_t>(P.maxblk, kMd5MaxPerChunk) : P.maxblk;
+  if (md5)
+    for (auto &sl : P.slot)
+      if (!sl.dtail && (hipMalloc(reinterpret_cast<void **>(&sl.dtail), maxmsg * 128) != hipSuccess ||
+                        hipMalloc(reinterpret_cast<void **>(&sl.dmd5), maxmsg * 16) != hipSuccess ||
+                        hipHostMalloc(reinterpret_cast<void **>(&sl.pin_md5), maxmsg * 16, hipHostMallocDefault) !=
+                            hipSuccess))
+        return HC_E_NOMEM;
   const int copy_threads = std::max(1, env_int("HC_COPY_THREADS", 8));
   // direct DMA: uniform, densely packed (stride == ulen, 16-B multiple) and already pinned
   const bool direct = !off && !len && stride == ulen && ulen > 0 && (ulen & 15u) == 0 &&
@@ -258,7 +294,10 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     if (!s.busy) return HC_OK;
     s.busy = false;
     if (hipEventSynchronize(s.done) != hipSuccess) return HC_E_HIP;
-    std::memcpy(crc_out + s.i0, s.pin_crc, s.nb * 4);
+    if (md5)
+      std::memcpy(md5_out + 16 * s.i0, s.pin_md5, s.nb * 16);
+    else
+      std::memcpy(crc_out + s.i0, s.pin_crc, s.nb * 4);
     return HC_OK;
   };
   while (i < n && rc == HC_OK) {
@@ -269,7 +308,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     uint32_t l0 = blk_len(len, ulen, i);
     if (direct) {
       j = std::min<uint64_t>(n, i + std::max<uint64_t>(1, P.chunk / ulen));
-      j = std::min<uint64_t>(j, i + P.maxblk);
+      j = std::min<uint64_t>(j, i + maxmsg);
       pos = (j - i) * (uint64_t)ulen;
       if (pos > P.chunk) {
         rc = HC_E_ARG;
@@ -283,7 +322,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     } else {
       // plan the chunk: blocks [i, j) packed at 16-B aligned offsets
       bool uniform = true;
-      while (j < n && j - i < P.maxblk) {
+      while (j < n && j - i < maxmsg) {
         const uint32_t l = blk_len(len, ulen, j);
         const uint64_t need = (pos + l + 15) & ~uint64_t(15);
         if (need > P.chunk) break;
@@ -322,12 +361,26 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
       }
     }
     const uint64_t nb = j - i;
-    rc = packed_uniform
-             ? dispatch(dev, s.dbuf, nullptr, nullptr, l0, l0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos)
-             : dispatch(dev, s.dbuf, s.doff, s.dlen, 0, 0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos);
-    if (rc != HC_OK) break;
-    if (hipMemcpyAsync(s.pin_crc, s.dcrc, nb * 4, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
-        hipEventRecord(s.done, s.stream) != hipSuccess) {
+    if (md5) {
+      const bool u = packed_uniform;
+      if (launch_md5(s.dbuf, u ? nullptr : s.doff, u ? nullptr : s.dlen, l0, l0, nb, s.dtail, s.dmd5,
+                     g_dev[dev].cus, s.stream) != hipSuccess ||
+          hipMemcpyAsync(s.pin_md5, s.dmd5, nb * 16, hipMemcpyDeviceToHost, s.stream) != hipSuccess) {
+        rc = HC_E_HIP;
+        break;
+      }
+      t_last = hc_launch_info{"k_md5", 0, nb, pos, 0, 256, 0};
+    } else {
+      rc = packed_uniform
+               ? dispatch(dev, s.dbuf, nullptr, nullptr, l0, l0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos)
+               : dispatch(dev, s.dbuf, s.doff, s.dlen, 0, 0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos);
+      if (rc != HC_OK) break;
+      if (hipMemcpyAsync(s.pin_crc, s.dcrc, nb * 4, hipMemcpyDeviceToHost, s.stream) != hipSuccess) {
+        rc = HC_E_HIP;
+        break;
+      }
+    }
+    if (hipEventRecord(s.done, s.stream) != hipSuccess) {
       rc = HC_E_HIP;
       break;
     }
@@ -487,6 +540,12 @@ int hc_crc32_messages(const uint8_t *base, const uint64_t *off, const uint32_t *
   if (n == 0) return HC_OK;
   if (!base || !off || !len || !crc_out) return HC_E_ARG;
   return host_batch(base, off, len, 0, 0, n, crc_out, kFlagMessages);
+}
+
+int hc_md5_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16) {
+  if (n == 0) return HC_OK;
+  if (!base || !off || !len || !out16) return HC_E_ARG;
+  return host_batch(base, off, len, 0, 0, n, nullptr, 0, out16);
 }
 
 int hc_verify_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,

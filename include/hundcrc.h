@@ -11,6 +11,7 @@
  *   utils/crc/crc_util.go:79-83  SizeWithoutCRCs                 -> hc_size_without_crcs
  *   utils/crc/crc_util.go:88-100 CheckBlockIntegrity             -> hc_check_block
  *   utils/crc/crc_util.go:106-122 FixLastBlockCRC                -> hc_fix_last_block
+ *   lsm/sstable/sstable.go:2287-2420 CheckIntegrity (md5 + merkle_tree) -> hc_md5*, hc_merkle_* (row f4)
  * New batched entries (the GPU hot path) for the per-block loops of
  *   lsm/block_manager/block_manager.go:203-235 (ReadFromDisk verify loop),
  *   lsm/wal/wal.go:260-271,362-406 (flushBlock / recoverMemtable),
@@ -179,6 +180,48 @@ int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad,
 int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32_t *len,
                        uint64_t stride, uint32_t ulen, uint64_t nblocks, uint64_t seed,
                        void *stream);
+
+/* ---- row f4: Merkle/MD5 integrity of SSTable data ----------------------------
+ * lsm/sstable/sstable.go:2287-2420 CheckIntegrity: md5.Sum of every record
+ * (:2358), merkle_tree.NewMerkleTree(leaves, true) (:2368,
+ * merkle_tree.go:36-81), Deserialize of the stored tree and Validate
+ * (merkle_tree.go:115-147,192-226).  Digests are the 16 bytes md5.Sum returns. */
+/* md5.Sum(p[0:n]) on the host CPU (one record or one node). */
+void hc_md5(const uint8_t *p, size_t n, uint8_t out[16]);
+/* md5.Sum of every message base[off[i] .. off[i]+len[i]) into out16 + 16*i:
+ * one GPU batch (the leaves of CheckIntegrity).  HC_E_NODEV without a GPU. */
+int hc_md5_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16);
+/* Device form: message i = base[off(i) .. +len(i)) (off/len arrays or
+ * i*stride / ulen, as hc_dev_crc32_blocks), digests into out16 (device,
+ * 16-B aligned).  workspace: device memory of n*128 bytes (the messages'
+ * padded tail blocks), or NULL to take it stream-ordered from the device pool.
+ * Kernels k_md5_tail + k_md5 (lane per message). */
+int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                        uint32_t ulen, uint64_t n, uint8_t *out16, void *workspace, void *stream);
+/* Entries of the Merkle level layout for n leaves: level 0 = the leaves, each
+ * level with an odd number (> 1) of nodes followed by its zero padding node
+ * (merkle_tree.go:60-66), then the parent levels up to the root (the last
+ * entry).  n == 0: one entry, md5.Sum([]byte{}) (merkle_tree.go:37). */
+uint64_t hc_merkle_nodes(uint64_t n);
+/* NewMerkleTree(leaves, hashedAlready=true) as level arrays: copies the n leaf
+ * digests into levels16 (hc_merkle_nodes(n)*16 bytes, may alias leaves16) and
+ * fills the padding nodes and parents (GPU from 65536 leaves, host below). */
+int hc_merkle_levels(const uint8_t *leaves16, uint64_t n, uint8_t *levels16);
+/* Device form: levels16 (device, 16-B aligned) already holds the n leaves in
+ * its first entries (e.g. from hc_dev_md5_messages); kernel k_merkle_level
+ * per level. */
+int hc_dev_merkle_levels(int device, uint8_t *levels16, uint64_t n, void *stream);
+/* MerkleTree.Serialize() (merkle_tree.go:173-187): DFS pre-order, 16 bytes
+ * per node, into out (cap bytes); *nbytes = hc_merkle_nodes(n)*16.  out ==
+ * NULL: size query only. */
+int hc_merkle_serialize(const uint8_t *levels16, uint64_t n, uint8_t *out, uint64_t cap, uint64_t *nbytes);
+/* tree.Validate(merkle_tree.Deserialize(stored)) exactly as CheckIntegrity
+ * calls it (sstable.go:2394-2411): *valid = 1 when the roots agree; else the
+ * mismatched leaf pair DeepValidate reports (*nmism = 0 or 1: Deserialize
+ * builds a left chain, so at most one pair), built-tree hash / stored hash.
+ * stored_len must be a positive multiple of 16 (Go panics otherwise). */
+int hc_merkle_validate(const uint8_t *levels16, uint64_t n, const uint8_t *stored, uint64_t stored_len, int *valid,
+                       uint8_t *mism_built16, uint8_t *mism_stored16, uint64_t *nmism);
 
 /* Per-launch accounting of the last device call on this thread (for the
  * roofline): kernel name, number of blocks routed to the streaming kernel and

@@ -19,6 +19,8 @@
  *     error strings, constant 4096 framing and float64 ceil size math.
  *   - The WAL block framing of lsm/wal/wal.go:177-283 + wal_header.go:5-77
  *     + model/record/record.go:85-119 (config 5 workload generator).
+ *   - Row f4: MD5 (Go crypto/md5, RFC 1321) and lsm/sstable/merkle_tree
+ *     (oc_merkle.c), pinned by the RFC 1321 suite and merkle_tree_test.go.
  *
  * Pinning: tests/golden/ (JSON fixtures), generated in the build container by
  * tests/golden/gen_golden.py with Python zlib.crc32 (zlib 1.2.11, the same
@@ -100,7 +102,6 @@ typedef struct {
 uint64_t oc_wal_frame(uint64_t seed, const uint32_t *rec_sizes, uint64_t nrec, uint32_t bs,
                       uint8_t *dst, uint64_t max_blocks, int stamp, oc_wal_stats *st,
                       uint64_t *next_rec);
-/* log-uniform serialized record size in [lo, hi] for record i */
 /* WAL recovery, lsm/wal/wal.go:362-455, over nblocks written blocks of bs
  * bytes (all logs back to back), starting at (start_block, start_offset).
  * Emits the serialized records (FULL payloads and reassembled FIRST..LAST
@@ -112,7 +113,25 @@ int oc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t bs, uint64_t
                   uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t *rec_off,
                   uint64_t *rec_len, uint64_t *nrec, uint64_t *pos_block, uint64_t *pos_offset,
                   int64_t *bad_block);
+/* log-uniform serialized record size in [lo, hi] for record i */
 uint32_t oc_wal_record_size(uint64_t seed, uint64_t i, uint32_t lo, uint32_t hi);
+
+/* ---- row f4: Merkle/MD5 integrity (oc_merkle.c) ------------------------- */
+/* md5.Sum (RFC 1321) */
+void oc_md5(const uint8_t *p, size_t n, uint8_t out[16]);
+void oc_md5_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint8_t *out, size_t n);
+/* NewMerkleTree(leaves, hashedAlready=true) root; n == 0: md5("") */
+void oc_merkle_root(const uint8_t *leaves, uint64_t n, uint8_t root[16]);
+/* ... .Serialize(): DFS pre-order, 16 B per node; returns bytes (out may be NULL) */
+uint64_t oc_merkle_serialize(const uint8_t *leaves, uint64_t n, uint8_t *out);
+/* tree(leaves).Validate(Deserialize(stored)): 1 equal roots, 0 not (mismatched
+ * leaf pairs, DeepValidate order, into mism1/mism2, up to cap; *nmism = all),
+ * -1 when stored is empty (a nil root: Go panics) */
+int oc_merkle_validate(const uint8_t *leaves, uint64_t n, const uint8_t *stored, uint64_t stored_len,
+                       uint8_t *mism1, uint8_t *mism2, uint64_t cap, uint64_t *nmism);
+/* tree(leaves1).Validate(tree(leaves2)), both built (merkle_tree_test.go TestValidate) */
+int oc_merkle_validate_trees(const uint8_t *l1, uint64_t n1, const uint8_t *l2, uint64_t n2, uint8_t *mism1,
+                             uint8_t *mism2, uint64_t cap, uint64_t *nmism);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,10 @@ def lib():
             ("oc_wal_record_size", U32, [U64, U64, U32, U32]),
             ("oc_read_from_disk", I, [P, U64, U32, U64, U64, P, P, P]),
             ("oc_wal_replay", I, [P, U64, U32, U64, U64, U64, P, P, P, P, P, P, P]),
+            ("oc_md5", None, [P, S, P]), ("oc_md5_messages", None, [P, P, P, P, S]),
+            ("oc_merkle_root", None, [P, U64, P]), ("oc_merkle_serialize", U64, [P, U64, P]),
+            ("oc_merkle_validate", I, [P, U64, P, U64, P, P, U64, P]),
+            ("oc_merkle_validate_trees", I, [P, U64, P, U64, P, P, U64, P]),
         ]:
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
@@ -143,3 +147,46 @@ def wal_replay(blocks: bytes, bs: int = 4096, start_block: int = 0, start_offset
     recs = [raw[int(off[i]):int(off[i]) + int(ln[i])] for i in range(n.value)]
     return recs, rc, bad.value, (pb.value, po.value)
 
+
+
+def md5(data) -> bytes:
+    b = bytes(data)
+    out = ctypes.create_string_buffer(16)
+    lib().oc_md5(b, len(b), out)
+    return out.raw
+
+
+def merkle_root(leaves: bytes) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().oc_merkle_root(leaves, len(leaves) // 16, out)
+    return out.raw
+
+
+def merkle_serialize(leaves: bytes) -> bytes:
+    n = len(leaves) // 16
+    size = lib().oc_merkle_serialize(leaves, n, None)
+    out = ctypes.create_string_buffer(max(1, size))
+    lib().oc_merkle_serialize(leaves, n, out)
+    return out.raw[:size]
+
+
+def merkle_validate(leaves: bytes, stored: bytes, cap: int = 1 << 16):
+    """(valid, [(tree1 hash, tree2 hash) of mismatched leaves]) or (None, []) when Go panics."""
+    m1 = ctypes.create_string_buffer(16 * cap)
+    m2 = ctypes.create_string_buffer(16 * cap)
+    nm = ctypes.c_uint64(0)
+    r = lib().oc_merkle_validate(leaves, len(leaves) // 16, stored, len(stored), m1, m2, cap, ctypes.byref(nm))
+    if r < 0:
+        return None, []
+    k = min(nm.value, cap)
+    return bool(r), [(m1.raw[16 * i:16 * i + 16], m2.raw[16 * i:16 * i + 16]) for i in range(k)]
+
+
+def merkle_validate_trees(leaves1: bytes, leaves2: bytes, cap: int = 1 << 16):
+    m1 = ctypes.create_string_buffer(16 * cap)
+    m2 = ctypes.create_string_buffer(16 * cap)
+    nm = ctypes.c_uint64(0)
+    r = lib().oc_merkle_validate_trees(leaves1, len(leaves1) // 16, leaves2, len(leaves2) // 16, m1, m2, cap,
+                                       ctypes.byref(nm))
+    k = min(nm.value, cap)
+    return bool(r), [(m1.raw[16 * i:16 * i + 16], m2.raw[16 * i:16 * i + 16]) for i in range(k)]

@@ -427,6 +427,59 @@ def main():
     g["read_from_disk"] = {"seed": 0x52464431, "blocks": 5, "flip": "image[3*B+1000] ^= 0x04",
                            "cases": rfd, "image_hex": images}
 
+    # 6. row f4: MD5 (hashlib, the RFC 1321 function of Go crypto/md5) and the
+    # Merkle tree of lsm/sstable/merkle_tree/merkle_tree.go restated below
+    rfc = ["", "a", "abc", "message digest", "abcdefghijklmnopqrstuvwxyz",
+           "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789",
+           "1234567890" * 8]
+    md5k = {"rfc1321": [[m, hashlib.md5(m.encode()).hexdigest()] for m in rfc]}
+    rng = np.random.default_rng(0x4D4435)
+    rnd = []
+    for n in list(range(0, 130)) + [255, 256, 1000, 4092, 4096, 9815, 65536, 100000]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        rnd.append({"seed_len": n, "sha256": sha(b), "md5": hashlib.md5(b).hexdigest()})
+    md5k["random"] = {"seed": 0x4D4435, "note": "rng = numpy default_rng(seed); b = rng.integers(0,256,n,uint8) in order",
+                      "cases": rnd}
+    g["md5"] = md5k
+
+    def merkle_levels(leaves):  # NewMerkleTree(leaves, true) (:36-81) as level lists
+        if not leaves:
+            return [[hashlib.md5(b"").digest()]], 0
+        lv = [list(leaves)]
+        real = [len(leaves)]
+        while len(lv[-1]) > 1:
+            cur = lv[-1]
+            if len(cur) % 2:
+                cur.append(bytes(16))                    # neutral node (:60-66)
+            lv.append([hashlib.md5(cur[i] + cur[i + 1]).digest() for i in range(0, len(cur), 2)])
+            real.append(len(lv[-1]))
+        return lv, real
+
+    def merkle_serialize(leaves):  # Serialize (:173-187): DFS pre-order
+        lv, real = merkle_levels(leaves)
+        if not leaves:
+            return lv[0][0]
+        out, stack = [], [(len(lv) - 1, 0)]
+        while stack:
+            L, i = stack.pop()
+            out.append(lv[L][i])
+            if L > 0 and i < real[L]:
+                stack += [(L - 1, 2 * i + 1), (L - 1, 2 * i)]
+        return b"".join(out)
+
+    # expected roots from the reference's own test (merkle_tree_test.go:11-21)
+    ref_roots = [[["block1", "block2", "block3", "block4"], "52b6ec49b1ed0eed625adcef9073f0c2"],
+                 [["block1", "block2", "block3"], "ac491d1ea728dc2fb488cf3bc8b3a898"],
+                 [["block1", "block2"], "423a3d793bb8c91da536a90361dc09ff"],
+                 [["block1"], "9dd085e96a8813854138d29b8a6fdf58"]]
+    trees = []
+    for n in list(range(0, 18)) + [31, 32, 33, 100, 255]:
+        leaves = [hashlib.md5(b"record-%d" % i).digest() for i in range(n)]
+        ser = merkle_serialize(leaves)
+        trees.append({"n": n, "leaves": "md5(b'record-%d' % i)", "root": merkle_levels(leaves)[0][-1][0].hex(),
+                      "serialized_nodes": len(ser) // 16, "serialized_sha256": sha(ser)})
+    g["merkle"] = {"reference_test_roots": ref_roots, "trees": trees}
+
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
     with open(path, "w") as f:
         json.dump(g, f, indent=0)
