@@ -121,6 +121,7 @@ def _lib():
             "hc_md5_messages": (I, [P, P, P, U64, P]),
             "hc_dev_md5_messages": (I, [I, P, P, P, U64, U32, U64, P, P, P]),
             "hc_merkle_nodes": (U64, [U64]),
+            "hc_md5_workspace_bytes": (U64, [U64]),
             "hc_merkle_levels": (I, [P, U64, P]),
             "hc_dev_merkle_levels": (I, [I, P, U64, P]),
             "hc_merkle_serialize": (I, [P, U64, P, U64, P]),

@@ -266,7 +266,7 @@ thread_local uint64_t t_host_bytes = 0;  // bytes moved by the last host batch (
 // larger than one staging slot are rejected (HC_E_ARG): the on-disk block
 // sizes are 4-16 KiB (utils/config/config.go:137, README.md:191,255).
 // md5_out != nullptr: MD5 digests of whole messages instead (row f4; crc_out unused).
-constexpr uint64_t kMd5MaxPerChunk = 262144;  // bounds the 128 B/message tail workspace per slot
+constexpr uint64_t kMd5MaxPerChunk = 262144;  // bounds the per-message MD5 workspace of a slot
 int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t flags, uint8_t *md5_out = nullptr) {
   const int dev = default_device();
@@ -279,7 +279,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
   const uint64_t maxmsg = md5 ? std::min<uint64_t>(P.maxblk, kMd5MaxPerChunk) : P.maxblk;
   if (md5)
     for (auto &sl : P.slot)
-      if (!sl.dtail && (hipMalloc(reinterpret_cast<void **>(&sl.dtail), maxmsg * 128) != hipSuccess ||
+      if (!sl.dtail && (hipMalloc(reinterpret_cast<void **>(&sl.dtail), md5_workspace_bytes(maxmsg)) != hipSuccess ||
                         hipMalloc(reinterpret_cast<void **>(&sl.dmd5), maxmsg * 16) != hipSuccess ||
                         hipHostMalloc(reinterpret_cast<void **>(&sl.pin_md5), maxmsg * 16, hipHostMallocDefault) !=
                             hipSuccess))

@@ -53,11 +53,13 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
                           const DeviceTables *tables, int grid, hipStream_t s);
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                        uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s);
-// Row f4 (hc_md5.hip): MD5 of each message (16-B digests at out16; tails = a
-// workspace of n * 128 bytes), and the Merkle levels above n leaves stored at
-// levels16 (layout: hc_merkle_nodes in include/hundcrc.h).
+// Row f4 (hc_md5.hip): MD5 of each message (16-B digests at out16; workspace
+// = md5_workspace_bytes(n) bytes of device memory: tail slots + schedule), and
+// the Merkle levels above n leaves stored at levels16 (layout:
+// hc_merkle_nodes in include/hundcrc.h).
+uint64_t md5_workspace_bytes(uint64_t n);
 hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
-                      uint64_t n, uint8_t *tails, uint8_t *out16, int cus, hipStream_t s);
+                      uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s);
 hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
                                  hipStream_t s);

@@ -4,22 +4,21 @@
 // parents md5.Sum(left || right)).
 //
 // MD5 (RFC 1321) chains 64-byte blocks, so one message is one sequential
-// chain: the parallelism is across messages.
-//   * k_md5_tail (thread per message): writes each message's last one or two
-//     padded blocks (data tail, 0x80, zeros, bit length) into a 128-byte slot
-//     of a workspace, so the main loop never builds a padded block itself.
-//   * k_md5 (lane per message): every lane of a wave pulls messages from the
-//     wave's pool as it finishes one (ballot + mbcnt), so the 64 lanes stay
-//     busy whatever the message lengths; each iteration a lane hashes one
-//     64-byte block: the next full block of its message (four unaligned
-//     16-byte loads) or one of its tail blocks from the workspace.  The block
-//     function is 64 steps of v_bitop3 (F/G/H/I), v_add3, v_add and v_alignbit
-//     (rotate).  Bound: VALU (about 5 ops per byte), not HBM.
+// chain: the parallelism is across messages, one lane per message.
+//   * k_md5_tail (thread per message): writes each message's padded tail
+//     blocks (its last len % 64 bytes, 0x80, zeros, the bit length) into a
+//     128-byte slot of the workspace.
+//   * k_md5 (lane per message): lanes take messages as they
+//     free up, longest length class first; message bytes reach the lanes in
+//     stages of up to 4 blocks, fetched by coalesced 256-byte pieces and
+//     swapped through LDS.  The block function is 64 steps of v_bitop3
+//     (F/G/H/I), v_add, v_add3, v_alignbit (rotate) and v_add: VALU-bound.
 //   * k_merkle_level (thread per parent): parent = md5(left || right), one
 //     block; an odd level is padded with a zero node (merkle_tree.go:60-66).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "hc_kernels.hpp"
 
@@ -126,67 +125,229 @@ __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ ba
 }
 
 // ---------------------------------------------------------------------------
-// Lane per message, messages pulled from the wave's pool as lanes free up.
-__global__ __launch_bounds__(256) void k_md5(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-                                             const uint32_t *__restrict__ lens, uint64_t stride, uint32_t ulen,
-                                             uint64_t n, const uint8_t *__restrict__ tails,
-                                             uint8_t *__restrict__ out16) {
+// Lane per message, blocks staged by coalesced loads through LDS.
+//
+// A lane consumes its message in stages of up to 4 blocks (256 B) and ends it
+// with a stage from its tail slot (k_md5_tail, 1-2 blocks).  The 64 stages of
+// a wave are fetched by 16 wave-instructions, each covering 4 messages x 256
+// contiguous bytes (16 lanes x 16 B per message): HBM sees >= 128-B pieces,
+// not the 64 scattered half-lines of a lane-per-message load (1.8 vs 5.5-6.2
+// TB/s in tools/kmd5's probes).  The pieces go to the wave's LDS image (slot m
+// = the stage of lane m, odd pitch: conflict-free writes and per-lane
+// ds_read_b128 at immediate offsets); two stages are in flight while one is
+// compressed.  Pieces past a stage's blocks re-read its last piece: no load
+// leaves a message's full blocks or its tail slot.
+//
+// Free lanes take messages from 64-entry metadata windows (lane j holds
+// message wbase + j; the next window is prefetched), by ballot rank through a
+// small LDS hand-off.  The wave walks its range once per length class,
+// longest first (md5_class).
+constexpr int kMd5Waves = 4;        // waves per workgroup; 2 workgroups per CU by LDS
+constexpr int kMd5StageBlocks = 4;  // 64-byte blocks per lane per stage
+constexpr int kMd5Classes = 4;
+
+// Length class, longest first.  In range order, the lane that draws a 64 KiB
+// record last keeps the wave busy alone (+26 % stages for config 5's sizes);
+// these four classes come within 1 % of longest-first order.
+__device__ __forceinline__ uint32_t md5_class(uint32_t l) {
+  return l >= 32768u ? 0u : l >= 8192u ? 1u : l >= 2048u ? 2u : 3u;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+
+template <bool kOff, bool kLen>
+__global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restrict__ base,
+                                                        const uint64_t *__restrict__ offs,
+                                                        const uint32_t *__restrict__ lens, uint64_t stride,
+                                                        uint32_t ulen, uint64_t n, const uint8_t *__restrict__ tails,
+                                                        uint8_t *__restrict__ out16) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  // stage pieces are addressed as integers: name the global address space, or
+  // they become flat loads, which also count on lgkmcnt (the LDS waits of the
+  // compression would wait for the stages in flight: -9 %, tools/kmd5)
+  typedef const u32x4 __attribute__((aligned(1), address_space(1))) *gpiece;
+  constexpr uint32_t kSlot = 4 * kMd5StageBlocks;  // 16-B chunks per stage
+  constexpr int kDepth = 2;                       // stages in flight
+  // slot m (lane m's stage) at m * kPitch chunks: an odd pitch keeps both the
+  // loaders' writes and the per-lane ds_read_b128 conflict-free, and every
+  // address is a per-lane base plus an immediate offset
+  constexpr uint32_t kPitch = kSlot + 1;
+  __shared__ u32x4 lds[kMd5Waves][64 * kPitch];
+  __shared__ uint4 handoff[kMd5Waves][64];
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uni_u32(threadIdx.x >> 6);
-  const uint64_t wpb = blockDim.x >> 6;
-  const uint64_t gw = (uint64_t)blockIdx.x * wpb + wave, W = (uint64_t)gridDim.x * wpb;
-  const uint64_t p1 = n * (gw + 1) / W;
-  uint64_t next = n * gw / W;  // wave-uniform pool cursor
-  bool act = false;
+  u32x4 *L = lds[wave];
+  uint4 *H = handoff[wave];
+  const uint64_t gw = (uint64_t)blockIdx.x * kMd5Waves + wave, W = (uint64_t)gridDim.x * kMd5Waves;
+  const uint64_t p0 = n * gw / W, p1 = n * (gw + 1) / W;
+  if (p0 >= p1) return;
+  // metadata windows: lane j holds message wbase + j; the next window of the
+  // walk is prefetched into nw_*
+  auto fetch = [&](uint64_t b, uint64_t &o, uint32_t &l) {
+    const uint64_t i = b + lane < p1 ? b + lane : p1 - 1;
+    // (compile-time layout: a uniform branch around these loads would make the
+    // waitcnt pass drain every load in flight at the join)
+    if constexpr (kOff)
+      o = offs[i];
+    else
+      o = i * stride;
+    if constexpr (kLen)
+      l = lens[i];
+    else
+      l = ulen;
+  };
+  uint64_t wbase = p0, nwbase = p0, w_off = 0, nw_off = 0;
+  uint32_t c = 0, nc = 0, w_len = 0, nw_len = 0;
+  auto next_pos = [&]() {
+    if (wbase + 64 < p1) {
+      nwbase = wbase + 64;
+      nc = c;
+    } else {
+      nwbase = p0;
+      nc = c + 1;
+    }
+    if (nc < (uint32_t)kMd5Classes) fetch(nwbase, nw_off, nw_len);
+  };
+  fetch(p0, w_off, w_len);
+  next_pos();
+  uint64_t wmask = __ballot(wbase + lane < p1 && md5_class(w_len) == c);
+  bool more = true;  // windows left (wave-uniform)
+  bool act = false, fresh = false;
   uint64_t msg = 0;
-  const uint8_t *p = nullptr;   // next full data block
-  const uint8_t *tp = nullptr;  // next tail block
+  uint64_t p = 0;  // address of the message's next full block
   uint32_t nfull = 0, ntail = 0;
-  uint32_t st[4] = {0, 0, 0, 0};
-  for (;;) {
-    const uint64_t need = __ballot(!act);
-    if (need) {
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      const uint64_t idx = next + rank;
-      next += (uint64_t)__builtin_popcountll(need);
-      if (!act && idx < p1) {
-        const uint64_t o = offs ? offs[idx] : idx * stride;
-        const uint32_t l = lens ? lens[idx] : ulen;
-        msg = idx;
-        p = base + o;
-        nfull = l >> 6;
-        ntail = (l & 63u) < 56 ? 1u : 2u;
-        tp = tails + idx * 128;
-        md5_init(st);
-        act = true;
-      }
-    }
-    if (!__ballot(act)) break;
-    if (act) {
-      const uint8_t *src = nfull ? p : tp;
-      uint32_t M[16];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(src + 16 * q));
-        M[4 * q] = v.x;
-        M[4 * q + 1] = v.y;
-        M[4 * q + 2] = v.z;
-        M[4 * q + 3] = v.w;
-      }
-      md5_compress(st, M);
-      if (nfull) {
-        p += 64;
-        nfull--;
-      } else {
-        tp += 64;
-        if (--ntail == 0) {
-          *reinterpret_cast<uint4 *>(out16 + msg * 16) = make_uint4(st[0], st[1], st[2], st[3]);
-          act = false;
+  auto assign = [&]() {
+    uint64_t need = __ballot(!act);
+    while (need && more) {
+      if (!wmask) {
+        if (nc >= (uint32_t)kMd5Classes) {
+          more = false;
+          break;
         }
+        wbase = nwbase;
+        c = nc;
+        w_off = nw_off;
+        w_len = nw_len;
+        wmask = __ballot(wbase + lane < p1 && md5_class(w_len) == c);
+        next_pos();
+        continue;
+      }
+      const uint32_t na = (uint32_t)__builtin_popcountll(need), nw = (uint32_t)__builtin_popcountll(wmask);
+      const uint32_t k = na < nw ? na : nw;
+      // the first k window entries of the class go to the first k free lanes
+      const bool mine = (wmask >> lane) & 1u;
+      const uint32_t rj = lane_rank(wmask);
+      if (mine && rj < k) H[rj] = make_uint4((uint32_t)w_off, (uint32_t)(w_off >> 32), w_len, lane);
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t r = lane_rank(need);
+      if (!act && r < k) {
+        const uint4 h = H[r];
+        msg = wbase + h.w;
+        p = (uint64_t)(uintptr_t)base + (((uint64_t)h.y << 32) | h.x);
+        nfull = h.z >> 6;
+        ntail = (h.z & 63u) < 56 ? 1u : 2u;
+        act = true;
+        fresh = true;
+      }
+      __builtin_amdgcn_wave_barrier();
+      wmask = __ballot(mine && rj >= k);
+      need = __ballot(!act);
+    }
+  };
+  // Stages are planned kDepth ahead of the one being compressed: the lane's
+  // next blocks of its message (src, nb), or its tail slot (fin: the digest
+  // is complete after it; the lane is free for the next message at once).
+  struct Stage {
+    uint64_t msg;
+    uint32_t nb;  // blocks, 0 = none
+    bool first, fin;
+  };
+  auto plan = [&](Stage &t, uint64_t &src) {
+    assign();
+    t.first = fresh;
+    fresh = false;
+    t.fin = false;
+    t.msg = msg;
+    if (!act) {
+      src = (uint64_t)(uintptr_t)tails;
+      t.nb = 0;
+    } else if (nfull) {
+      src = p;
+      t.nb = nfull < (uint32_t)kMd5StageBlocks ? nfull : (uint32_t)kMd5StageBlocks;
+      p += 64u * t.nb;
+      nfull -= t.nb;
+    } else {
+      src = (uint64_t)(uintptr_t)tails + msg * 128;
+      t.nb = ntail;
+      t.fin = true;
+      act = false;
+    }
+  };
+  // kSlot wave-instructions per stage; each covers 4 messages x kSlot chunks
+  const uint32_t pj = 16u * (lane & (kSlot - 1));  // this lane's piece offset in every stage
+  auto issue = [&](u32x4(&R)[kSlot], uint64_t src, uint32_t nb) {
+    // the owner's last valid piece offset: pieces past the stage's blocks
+    // re-read it (nb == 0: src is the tail workspace, offset 0)
+    const uint32_t cap = nb ? 64u * nb - 16u : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < kSlot; q++) {
+      const uint32_t m = 4u * q + (lane >> 4);
+      const uint64_t t = ((uint64_t)shfl32((uint32_t)(src >> 32), m) << 32) | shfl32((uint32_t)src, m);
+      const uint32_t mc = shfl32(cap, m);
+      R[q] = *(gpiece)(t + (pj < mc ? pj : mc));
+    }
+  };
+  uint32_t st[4] = {0, 0, 0, 0};
+  auto compress_stage = [&](const Stage &t) {
+    if (t.first) md5_init(st);
+    for (uint32_t b = 0; b < (uint32_t)kMd5StageBlocks; b++) {
+      if (b < t.nb) {
+        uint32_t M[16];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          const u32x4 v = L[lane * kPitch + 4u * b + q];
+          M[4 * q] = v.x;
+          M[4 * q + 1] = v.y;
+          M[4 * q + 2] = v.z;
+          M[4 * q + 3] = v.w;
+        }
+        md5_compress(st, M);
       }
     }
+    if (t.fin) *reinterpret_cast<uint4 *>(out16 + t.msg * 16) = make_uint4(st[0], st[1], st[2], st[3]);
+  };
+  u32x4 R[kDepth][kSlot];
+  Stage T[kDepth];
+#pragma unroll
+  for (int d = 0; d < kDepth; d++) {
+    uint64_t src;
+    plan(T[d], src);
+    issue(R[d], src, T[d].nb);
+  }
+  // one step on register set d (a template argument, so R[d] stays in registers)
+  auto step = [&](auto dc) -> bool {
+    constexpr int d = decltype(dc)::value;
+    // the oldest stage empty everywhere: so are the later ones
+    if (!__ballot(T[d].nb != 0)) return false;
+    // pieces -> LDS: chunk j of slot m at m * kPitch + j
+#pragma unroll
+    for (uint32_t q = 0; q < kSlot; q++) L[(4u * q + (lane >> 4)) * kPitch + (lane & (kSlot - 1))] = R[d][q];
+    __builtin_amdgcn_wave_barrier();
+    const Stage cur = T[d];
+    uint64_t src;
+    plan(T[d], src);
+    issue(R[d], src, T[d].nb);  // in flight while the older stages are compressed
+    compress_stage(cur);
+    __builtin_amdgcn_wave_barrier();
+    return true;
+  };
+  static_assert(kDepth == 2, "the loop below alternates two register sets");
+  while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{})) {
   }
 }
 
@@ -217,17 +378,26 @@ __global__ void k_md5_empty(uint8_t *out16) {  // md5.Sum([]byte{}) (merkle_tree
 
 }  // namespace
 
+uint64_t md5_workspace_bytes(uint64_t n) { return n * 128; }
+
 hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
-                      uint64_t n, uint8_t *tails, uint8_t *out16, int cus, hipStream_t s) {
+                      uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const int tgrid = (int)((n + 255) / 256 < (uint64_t)cus * 8 ? (n + 255) / 256 : (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_md5_tail, dim3(tgrid), dim3(256), 0, s, base, off, len, stride, ulen, n, tails);
-  // 4 waves per workgroup; enough waves that every lane has messages (>= 64 per wave)
-  uint64_t waves = (n + 63) / 64;
-  const uint64_t maxw = (uint64_t)cus * 32;  // 8 waves per SIMD
-  if (waves > maxw) waves = maxw;
-  const int grid = (int)((waves + 3) / 4);
-  hipLaunchKernelGGL(k_md5, dim3(grid), dim3(256), 0, s, base, off, len, stride, ulen, n, tails, out16);
+  hipLaunchKernelGGL(k_md5_tail, dim3(tgrid), dim3(256), 0, s, base, off, len, stride, ulen, n, workspace);
+  // 2 workgroups (8 waves) per CU fit the LDS; a wave's range should give its
+  // 64 lanes several messages
+  uint64_t grid = (n + 64 * 4 * kMd5Waves - 1) / (64 * 4 * kMd5Waves);
+  if (grid > (uint64_t)cus * 2) grid = (uint64_t)cus * 2;
+  const dim3 g((unsigned)grid), b(64 * kMd5Waves);
+  if (off && len)
+    hipLaunchKernelGGL((k_md5<true, true>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+  else if (off)
+    hipLaunchKernelGGL((k_md5<true, false>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+  else if (len)
+    hipLaunchKernelGGL((k_md5<false, true>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+  else
+    hipLaunchKernelGGL((k_md5<false, false>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
   return hipGetLastError();
 }
 

@@ -136,6 +136,8 @@ void hc_md5(const uint8_t *p, size_t n, uint8_t out[16]) { md5(p, n, out); }
 
 uint64_t hc_merkle_nodes(uint64_t n) { return Levels(n).total; }
 
+uint64_t hc_md5_workspace_bytes(uint64_t n) { return md5_workspace_bytes(n); }
+
 int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                         uint32_t ulen, uint64_t n, uint8_t *out16, void *workspace, void *stream) {
   if (n == 0) return HC_OK;
@@ -148,7 +150,7 @@ int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const
   hipStream_t s = static_cast<hipStream_t>(stream);
   void *ws = workspace;
   int rc = HC_OK;
-  if (!ws && hipMallocAsync(&ws, n * 128, s) != hipSuccess) rc = HC_E_NOMEM;
+  if (!ws && hipMallocAsync(&ws, md5_workspace_bytes(n), s) != hipSuccess) rc = HC_E_NOMEM;
   if (rc == HC_OK && launch_md5(static_cast<const uint8_t *>(base), off, len, stride, ulen, n,
                                 static_cast<uint8_t *>(ws), out16, cus, s) != hipSuccess)
     rc = HC_E_HIP;

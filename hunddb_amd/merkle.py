@@ -57,6 +57,11 @@ def dev_md5_messages(buf, out16, off=None, lens=None, stride=0, ulen=0, n=None, 
     return out16
 
 
+def md5_workspace_bytes(n: int) -> int:
+    """Device workspace of dev_md5_messages for n messages (hc_md5_workspace_bytes)."""
+    return int(_lib().hc_md5_workspace_bytes(n))
+
+
 def merkle_nodes(n: int) -> int:
     """Entries of the level layout for n leaves (hc_merkle_nodes)."""
     return int(_lib().hc_merkle_nodes(n))

@@ -193,9 +193,11 @@ void hc_md5(const uint8_t *p, size_t n, uint8_t out[16]);
 int hc_md5_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16);
 /* Device form: message i = base[off(i) .. +len(i)) (off/len arrays or
  * i*stride / ulen, as hc_dev_crc32_blocks), digests into out16 (device,
- * 16-B aligned).  workspace: device memory of n*128 bytes (the messages'
- * padded tail blocks), or NULL to take it stream-ordered from the device pool.
- * Kernels k_md5_tail + k_md5 (lane per message). */
+ * 16-B aligned).  workspace: device memory of hc_md5_workspace_bytes(n)
+ * bytes, 16-B aligned (the messages' padded tail blocks and the per-wave
+ * schedule), or NULL to take it stream-ordered from the device pool.
+ * Kernels k_md5_plan + k_md5 (lane per message). */
+uint64_t hc_md5_workspace_bytes(uint64_t n);
 int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                         uint32_t ulen, uint64_t n, uint8_t *out16, void *workspace, void *stream);
 /* Entries of the Merkle level layout for n leaves: level 0 = the leaves, each

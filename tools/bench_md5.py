@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--only", default="", help="run only this part: loguniform | 4096 | levels")
     args = ap.parse_args()
 
     import torch
@@ -56,6 +57,15 @@ def main():
 
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0x4D4435)
+    if args.only in ("", "loguniform"):
+        leaves_loguniform(args, torch, crc, M, dev, rng)
+    if args.only in ("", "4096"):
+        leaves_4096(args, torch, crc, M, dev)
+    if args.only in ("", "levels"):
+        levels(args, torch, crc, M, dev, rng)
+
+
+def leaves_loguniform(args, torch, crc, M, dev, rng):
     n = args.records
     lens = np.minimum(np.exp(rng.uniform(np.log(64), np.log(65536), n)), 65536).astype(np.uint32)
     off = np.zeros(n, dtype=np.uint64)
@@ -67,7 +77,7 @@ def main():
     doff = torch.from_numpy(off.view(np.int64)).to(dev)
     dlen = torch.from_numpy(lens.view(np.int32)).to(dev)
     out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    ws = torch.empty(n * 128, dtype=torch.uint8, device=dev)
+    ws = torch.empty(M.md5_workspace_bytes(n), dtype=torch.uint8, device=dev)
     rec_bytes = int(lens.astype(np.uint64).sum())
 
     def leaves(s):
@@ -96,12 +106,14 @@ def main():
     del buf, ws, out, doff, dlen
     torch.cuda.empty_cache()
 
-    # 4096-B records, uniform stride (SSTable-block-sized records)
+
+def leaves_4096(args, torch, crc, M, dev):
+    """4096-B records, uniform stride (SSTable-block-sized records)."""
     nb = 2_000_000
     b4 = torch.empty(nb * 4096, dtype=torch.uint8, device=dev)
     crc.dev_fill_blocks(b4, 7, stride=4096, ulen=4096, nblocks=nb)
     o4 = torch.empty(nb * 16, dtype=torch.uint8, device=dev)
-    w4 = torch.empty(nb * 128, dtype=torch.uint8, device=dev)
+    w4 = torch.empty(M.md5_workspace_bytes(nb), dtype=torch.uint8, device=dev)
 
     def uni(s):
         M.dev_md5_messages(b4, o4, stride=4096, ulen=4096, n=nb, workspace=w4, stream=s)
@@ -112,16 +124,18 @@ def main():
     del b4, o4, w4
     torch.cuda.empty_cache()
 
-    # Merkle levels
+
+def levels(args, torch, crc, M, dev, rng):
+    """NewMerkleTree parents over --leaves leaves."""
     nl = args.leaves
     total_nodes = M.merkle_nodes(nl)
     lv = torch.empty(total_nodes * 16, dtype=torch.uint8, device=dev)
     crc.dev_fill_blocks(lv[:nl * 16], 9, stride=16, ulen=16, nblocks=nl)
 
-    def levels(s):
+    def run(s):
         M.dev_merkle_levels(lv, nl, stream=s)
 
-    med, mean = timed(torch, levels, args.steps, args.warmup)
+    med, mean = timed(torch, run, args.steps, args.warmup)
     # spot-check parents at every level with hashlib (the GPU tests check the
     # whole tree against the oracle)
     lay = M._layout(nl)
