@@ -85,26 +85,54 @@ __device__ __forceinline__ uint32_t uni_u32(uint32_t v) { return __builtin_amdgc
 // Thread per message: the 128-byte tail slot = the message's last len % 64 data
 // bytes, 0x80, zeros and the 64-bit little-endian bit length at byte 56 (tail
 // < 56 bytes: one block) or 120 (two blocks).  The data bytes come from the
-// aligned dwords that hold them (an aligned dword holding a message byte never
-// leaves that byte's page), shifted per lane with v_alignbyte.
+// aligned 16-byte chunks that hold them (at most 5; an aligned chunk holding
+// a message byte never leaves that byte's page), loaded unconditionally
+// (chunks past the tail re-read the last one; no tail bytes: the slot itself)
+// and funnel-shifted per lane.
+template <bool kOff, bool kLen>
 __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t stride, uint32_t ulen,
                                                   uint64_t n, uint8_t *__restrict__ tails) {
   for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t o = offs ? offs[m] : m * stride;
-    const uint32_t l = lens ? lens[m] : ulen;
+    uint64_t o;
+    uint32_t l;
+    if constexpr (kOff)
+      o = offs[m];
+    else
+      o = m * stride;
+    if constexpr (kLen)
+      l = lens[m];
+    else
+      l = ulen;
     const uint32_t r = l & 63u;
     const uintptr_t tp = (uintptr_t)base + o + (l & ~63u);
-    const uint32_t sh = (uint32_t)(tp & 3u);
-    const uint32_t *A = reinterpret_cast<const uint32_t *>(tp - sh);
-    const uint32_t nd = r ? (sh + r + 3) >> 2 : 0u;  // aligned dwords holding the tail bytes (<= 17)
-    uint32_t dw[17];
+    const uint32_t sh = (uint32_t)(tp & 15u);
+    const uint32_t nc = r ? (sh + r + 15) >> 4 : 0u;  // aligned chunks holding the tail bytes (<= 5)
+    uint32_t D[21];
 #pragma unroll
-    for (int j = 0; j < 17; j++) dw[j] = (uint32_t)j < nd ? __builtin_nontemporal_load(A + j) : 0u;
+    for (int j = 0; j < 5; j++) {
+      const uintptr_t a = nc ? (tp - sh) + 16u * ((uint32_t)j < nc ? (uint32_t)j : nc - 1u)
+                             : (uintptr_t)(tails + m * 128);
+      const uint4 v = *reinterpret_cast<const uint4 *>(a);
+      D[4 * j] = v.x;
+      D[4 * j + 1] = v.y;
+      D[4 * j + 2] = v.z;
+      D[4 * j + 3] = v.w;
+    }
+    D[20] = 0;
+    // dword k of the tail = alignbyte(D[q + k + 1], D[q + k], sh & 3), q = sh / 4
+    const uint32_t q = sh >> 2, b = sh & 3u;
+    auto pick = [&](int k) {  // D[q + k], q in 0..3
+      const uint32_t x = (q & 1u) ? D[k + 1] : D[k], y = (q & 1u) ? D[k + 3] : D[k + 2];
+      return (q & 2u) ? y : x;
+    };
     uint32_t w[32];
+    uint32_t lo = pick(0);
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      uint32_t v = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+      const uint32_t hi = pick(i + 1);
+      uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, b);
+      lo = hi;
       const int32_t nb = (int32_t)r - 4 * i;  // tail bytes in this word
       v &= nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
       v |= (uint32_t)i == (r >> 2) ? (0x80u << (8 * (r & 3u))) : 0u;
@@ -120,7 +148,7 @@ __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ ba
     w[31] = two ? (uint32_t)(bits >> 32) : 0u;
     uint4 *dst = reinterpret_cast<uint4 *>(tails + m * 128);
 #pragma unroll
-    for (int q = 0; q < 8; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (int k = 0; k < 8; k++) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
   }
 }
 
@@ -384,20 +412,25 @@ hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const int tgrid = (int)((n + 255) / 256 < (uint64_t)cus * 8 ? (n + 255) / 256 : (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_md5_tail, dim3(tgrid), dim3(256), 0, s, base, off, len, stride, ulen, n, workspace);
   // 2 workgroups (8 waves) per CU fit the LDS; a wave's range should give its
   // 64 lanes several messages
   uint64_t grid = (n + 64 * 4 * kMd5Waves - 1) / (64 * 4 * kMd5Waves);
   if (grid > (uint64_t)cus * 2) grid = (uint64_t)cus * 2;
-  const dim3 g((unsigned)grid), b(64 * kMd5Waves);
+  const dim3 g((unsigned)grid), b(64 * kMd5Waves), tg(tgrid), tb(256);
+#define HC_MD5_LAUNCH(O, L)                                                                                 \
+  do {                                                                                                      \
+    hipLaunchKernelGGL((k_md5_tail<O, L>), tg, tb, 0, s, base, off, len, stride, ulen, n, workspace);       \
+    hipLaunchKernelGGL((k_md5<O, L>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);      \
+  } while (0)
   if (off && len)
-    hipLaunchKernelGGL((k_md5<true, true>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+    HC_MD5_LAUNCH(true, true);
   else if (off)
-    hipLaunchKernelGGL((k_md5<true, false>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+    HC_MD5_LAUNCH(true, false);
   else if (len)
-    hipLaunchKernelGGL((k_md5<false, true>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+    HC_MD5_LAUNCH(false, true);
   else
-    hipLaunchKernelGGL((k_md5<false, false>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);
+    HC_MD5_LAUNCH(false, false);
+#undef HC_MD5_LAUNCH
   return hipGetLastError();
 }
 
