@@ -32,6 +32,24 @@ def test_exports_every_declared_symbol(hc):
     assert not missing, missing
 
 
+def test_go_bindings_use_declared_symbols():
+    """The cgo files under integration/go (not compiled here: no Go toolchain)
+    call only entry points and constants include/hundcrc.h declares."""
+    declared = set(header_functions())
+    hdr = open(os.path.join(ROOT, "include", "hundcrc.h")).read()
+    consts = set(re.findall(r"#define\s+(HC_[A-Z0-9_]+)", hdr))
+    used_fns, used_consts = set(), set()
+    for dirpath, _dirs, files in os.walk(os.path.join(ROOT, "integration", "go")):
+        for f in files:
+            if f.endswith(".go"):
+                src = open(os.path.join(dirpath, f)).read()
+                used_fns |= set(re.findall(r"\bC\.(hc_[a-z0-9_]+)\(", src))
+                used_consts |= set(re.findall(r"\bC\.(HC_[A-Z0-9_]+)\b", src))
+    assert used_fns, "no cgo calls found"
+    assert used_fns <= declared, sorted(used_fns - declared)
+    assert used_consts <= consts, sorted(used_consts - consts)
+
+
 def test_version_and_strings(hc):
     L = hc.lib()
     assert b"gfx950" in L.hc_version()
