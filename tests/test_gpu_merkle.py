@@ -57,6 +57,22 @@ def test_md5_padding_boundaries(cuda, oracle):
         assert got[i].tobytes() == want, (i, int(ln[i]), int(off[i]) % 16)
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 1023, 1025])
+def test_md5_small_batches(cuda, oracle, n):
+    """Batches smaller than one wave's 64 lanes or one workgroup's range: idle
+    waves and lanes, ragged last window; a 1 MiB record and empty records."""
+    torch = cuda
+    rng = np.random.default_rng(100 + n)
+    lens = rng.integers(0, 5000, n).astype(np.uint32)
+    lens[0] = 1 << 20
+    if n > 2:
+        lens[-1] = 0
+    buf, off, ln = _packed(rng, lens, pad=7)
+    got = _dev_md5(torch, buf, off, ln)
+    want = _oracle_md5(oracle, buf, off, ln)
+    assert (got == want).all()
+
+
 def test_md5_records_batch_vs_oracle(cuda, oracle):
     """200k records, log-uniform 0 B .. 64 KiB (the record sizes of config 5),
     unaligned starts: every digest vs the oracle."""
