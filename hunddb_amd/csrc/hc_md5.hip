@@ -86,9 +86,9 @@ __device__ __forceinline__ uint32_t uni_u32(uint32_t v) { return __builtin_amdgc
 // bytes, 0x80, zeros and the 64-bit little-endian bit length at byte 56 (tail
 // < 56 bytes: one block) or 120 (two blocks).  The data bytes come from the
 // aligned 16-byte chunks that hold them (at most 5; an aligned chunk holding
-// a message byte never leaves that byte's page), loaded unconditionally
-// (chunks past the tail re-read the last one; no tail bytes: the slot itself)
-// and funnel-shifted per lane.
+// a message byte never leaves that byte's page; chunks past the tail re-read
+// the last one), funnel-shifted per lane.  The second block is written only
+// when the message needs it (len % 64 >= 56).
 template <bool kOff, bool kLen>
 __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t stride, uint32_t ulen,
@@ -110,16 +110,17 @@ __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ ba
     const uint32_t nc = r ? (sh + r + 15) >> 4 : 0u;  // aligned chunks holding the tail bytes (<= 5)
     uint32_t D[21];
 #pragma unroll
-    for (int j = 0; j < 5; j++) {
-      const uintptr_t a = nc ? (tp - sh) + 16u * ((uint32_t)j < nc ? (uint32_t)j : nc - 1u)
-                             : (uintptr_t)(tails + m * 128);
-      const uint4 v = *reinterpret_cast<const uint4 *>(a);
-      D[4 * j] = v.x;
-      D[4 * j + 1] = v.y;
-      D[4 * j + 2] = v.z;
-      D[4 * j + 3] = v.w;
+    for (int j = 0; j < 21; j++) D[j] = 0;
+    if (nc) {
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint4 v = *reinterpret_cast<const uint4 *>((tp - sh) + 16u * ((uint32_t)j < nc ? (uint32_t)j : nc - 1u));
+        D[4 * j] = v.x;
+        D[4 * j + 1] = v.y;
+        D[4 * j + 2] = v.z;
+        D[4 * j + 3] = v.w;
+      }
     }
-    D[20] = 0;
     // dword k of the tail = alignbyte(D[q + k + 1], D[q + k], sh & 3), q = sh / 4
     const uint32_t q = sh >> 2, b = sh & 3u;
     auto pick = [&](int k) {  // D[q + k], q in 0..3
@@ -148,7 +149,11 @@ __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ ba
     w[31] = two ? (uint32_t)(bits >> 32) : 0u;
     uint4 *dst = reinterpret_cast<uint4 *>(tails + m * 128);
 #pragma unroll
-    for (int k = 0; k < 8; k++) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    for (int k = 0; k < 4; k++) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    if (two) {
+#pragma unroll
+      for (int k = 4; k < 8; k++) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    }
   }
 }
 
@@ -246,11 +251,12 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   uint64_t wmask = __ballot(wbase + lane < p1 && md5_class(w_len) == c);
   bool more = true;  // windows left (wave-uniform)
   bool act = false, fresh = false;
-  uint64_t msg = 0;
+  uint32_t msg = 0;  // message index - p0 (a wave's range is < 2^32 messages)
   uint64_t p = 0;  // address of the message's next full block
   uint32_t nfull = 0, ntail = 0;
   auto assign = [&]() {
     uint64_t need = __ballot(!act);
+    if (!need || !more) return;
     while (need && more) {
       if (!wmask) {
         if (nc >= (uint32_t)kMd5Classes) {
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
       const uint32_t r = lane_rank(need);
       if (!act && r < k) {
         const uint4 h = H[r];
-        msg = wbase + h.w;
+        msg = (uint32_t)(wbase - p0) + h.w;
         p = (uint64_t)(uintptr_t)base + (((uint64_t)h.y << 32) | h.x);
         nfull = h.z >> 6;
         ntail = (h.z & 63u) < 56 ? 1u : 2u;
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   // next blocks of its message (src, nb), or its tail slot (fin: the digest
   // is complete after it; the lane is free for the next message at once).
   struct Stage {
-    uint64_t msg;
+    uint32_t msg;
     uint32_t nb;  // blocks, 0 = none
     bool first, fin;
   };
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
       p += 64u * t.nb;
       nfull -= t.nb;
     } else {
-      src = (uint64_t)(uintptr_t)tails + msg * 128;
+      src = (uint64_t)(uintptr_t)tails + (p0 + msg) * 128;
       t.nb = ntail;
       t.fin = true;
       act = false;
@@ -347,7 +353,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
         md5_compress(st, M);
       }
     }
-    if (t.fin) *reinterpret_cast<uint4 *>(out16 + t.msg * 16) = make_uint4(st[0], st[1], st[2], st[3]);
+    if (t.fin) *reinterpret_cast<uint4 *>(out16 + (p0 + t.msg) * 16) = make_uint4(st[0], st[1], st[2], st[3]);
   };
   u32x4 R[kDepth][kSlot];
   Stage T[kDepth];
