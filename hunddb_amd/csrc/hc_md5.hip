@@ -167,14 +167,16 @@ __global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ ba
 // not the 64 scattered half-lines of a lane-per-message load (1.8 vs 5.5-6.2
 // TB/s in tools/kmd5's probes).  The pieces go to the wave's LDS image (slot m
 // = the stage of lane m, odd pitch: conflict-free writes and per-lane
-// ds_read_b128 at immediate offsets); two stages are in flight while one is
-// compressed.  Pieces past a stage's blocks re-read its last piece: no load
-// leaves a message's full blocks or its tail slot.
+// ds_read_b128 at immediate offsets); the next stage is in flight while one
+// is compressed (kDepth 2 -- two in flight -- measured no faster: the kernel
+// is VALU-bound at 2 waves per SIMD, tools/kmd5).  Pieces past a stage's
+// blocks re-read its last piece: no load leaves a message's full blocks or
+// its tail slot.  kStage 3 (3 workgroups per CU) measured slower.
 //
 // Free lanes take messages from 64-entry metadata windows (lane j holds
-// message wbase + j; the next window is prefetched), by ballot rank through a
-// small LDS hand-off.  The wave walks its range once per length class,
-// longest first (md5_class).
+// message wbase + j; the next window is prefetched), by ballot rank through
+// the pad column of the LDS image.  The wave walks its range once per length
+// class, longest first (md5_class).
 constexpr int kMd5Waves = 4;        // waves per workgroup; 2 workgroups per CU by LDS
 constexpr int kMd5StageBlocks = 4;  // 64-byte blocks per lane per stage
 constexpr int kMd5Classes = 4;
@@ -193,7 +195,7 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-template <bool kOff, bool kLen>
+template <bool kOff, bool kLen, int kStage = kMd5StageBlocks, int kDepth = 1>
 __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restrict__ base,
                                                         const uint64_t *__restrict__ offs,
                                                         const uint32_t *__restrict__ lens, uint64_t stride,
@@ -204,18 +206,18 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   // they become flat loads, which also count on lgkmcnt (the LDS waits of the
   // compression would wait for the stages in flight: -9 %, tools/kmd5)
   typedef const u32x4 __attribute__((aligned(1), address_space(1))) *gpiece;
-  constexpr uint32_t kSlot = 4 * kMd5StageBlocks;  // 16-B chunks per stage
-  constexpr int kDepth = 2;                       // stages in flight
+  constexpr uint32_t kSlot = 4 * kStage;  // 16-B chunks per stage (<= 16: one 16-lane group per message)
   // slot m (lane m's stage) at m * kPitch chunks: an odd pitch keeps both the
   // loaders' writes and the per-lane ds_read_b128 conflict-free, and every
   // address is a per-lane base plus an immediate offset
   constexpr uint32_t kPitch = kSlot + 1;
   __shared__ u32x4 lds[kMd5Waves][64 * kPitch];
-  __shared__ uint4 handoff[kMd5Waves][64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uni_u32(threadIdx.x >> 6);
   u32x4 *L = lds[wave];
-  uint4 *H = handoff[wave];
+  // the hand-off of window entries to free lanes uses the pad column: entry e
+  // at chunk e * kPitch + kSlot
+  u32x4 *H = L + kSlot;
   const uint64_t gw = (uint64_t)blockIdx.x * kMd5Waves + wave, W = (uint64_t)gridDim.x * kMd5Waves;
   const uint64_t p0 = n * gw / W, p1 = n * (gw + 1) / W;
   if (p0 >= p1) return;
@@ -276,11 +278,11 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
       // the first k window entries of the class go to the first k free lanes
       const bool mine = (wmask >> lane) & 1u;
       const uint32_t rj = lane_rank(wmask);
-      if (mine && rj < k) H[rj] = make_uint4((uint32_t)w_off, (uint32_t)(w_off >> 32), w_len, lane);
+      if (mine && rj < k) H[rj * kPitch] = u32x4{(uint32_t)w_off, (uint32_t)(w_off >> 32), w_len, lane};
       __builtin_amdgcn_wave_barrier();
       const uint32_t r = lane_rank(need);
       if (!act && r < k) {
-        const uint4 h = H[r];
+        const u32x4 h = H[r * kPitch];
         msg = (uint32_t)(wbase - p0) + h.w;
         p = (uint64_t)(uintptr_t)base + (((uint64_t)h.y << 32) | h.x);
         nfull = h.z >> 6;
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
       t.nb = 0;
     } else if (nfull) {
       src = p;
-      t.nb = nfull < (uint32_t)kMd5StageBlocks ? nfull : (uint32_t)kMd5StageBlocks;
+      t.nb = nfull < (uint32_t)kStage ? nfull : (uint32_t)kStage;
       p += 64u * t.nb;
       nfull -= t.nb;
     } else {
@@ -322,14 +324,15 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
       act = false;
     }
   };
-  // kSlot wave-instructions per stage; each covers 4 messages x kSlot chunks
-  const uint32_t pj = 16u * (lane & (kSlot - 1));  // this lane's piece offset in every stage
-  auto issue = [&](u32x4(&R)[kSlot], uint64_t src, uint32_t nb) {
+  // 16 wave-instructions per stage; each covers 4 messages x kSlot chunks
+  // (lanes 16r + j, j < kSlot; with kSlot < 16 the other lanes re-read a piece)
+  const uint32_t pj = 16u * (lane & 15u);  // this lane's piece offset in every stage
+  auto issue = [&](u32x4(&R)[16], uint64_t src, uint32_t nb) {
     // the owner's last valid piece offset: pieces past the stage's blocks
     // re-read it (nb == 0: src is the tail workspace, offset 0)
     const uint32_t cap = nb ? 64u * nb - 16u : 0u;
 #pragma unroll
-    for (uint32_t q = 0; q < kSlot; q++) {
+    for (uint32_t q = 0; q < 16; q++) {
       const uint32_t m = 4u * q + (lane >> 4);
       const uint64_t t = ((uint64_t)shfl32((uint32_t)(src >> 32), m) << 32) | shfl32((uint32_t)src, m);
       const uint32_t mc = shfl32(cap, m);
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   uint32_t st[4] = {0, 0, 0, 0};
   auto compress_stage = [&](const Stage &t) {
     if (t.first) md5_init(st);
-    for (uint32_t b = 0; b < (uint32_t)kMd5StageBlocks; b++) {
+    for (uint32_t b = 0; b < (uint32_t)kStage; b++) {
       if (b < t.nb) {
         uint32_t M[16];
 #pragma unroll
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     }
     if (t.fin) *reinterpret_cast<uint4 *>(out16 + (p0 + t.msg) * 16) = make_uint4(st[0], st[1], st[2], st[3]);
   };
-  u32x4 R[kDepth][kSlot];
+  u32x4 R[kDepth][16];
   Stage T[kDepth];
 #pragma unroll
   for (int d = 0; d < kDepth; d++) {
@@ -370,7 +373,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     if (!__ballot(T[d].nb != 0)) return false;
     // pieces -> LDS: chunk j of slot m at m * kPitch + j
 #pragma unroll
-    for (uint32_t q = 0; q < kSlot; q++) L[(4u * q + (lane >> 4)) * kPitch + (lane & (kSlot - 1))] = R[d][q];
+    for (uint32_t q = 0; q < 16; q++)
+      if ((lane & 15u) < kSlot) L[(4u * q + (lane >> 4)) * kPitch + (lane & 15u)] = R[d][q];
     __builtin_amdgcn_wave_barrier();
     const Stage cur = T[d];
     uint64_t src;
@@ -380,8 +384,13 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     __builtin_amdgcn_wave_barrier();
     return true;
   };
-  static_assert(kDepth == 2, "the loop below alternates two register sets");
-  while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{})) {
+  static_assert(kDepth == 1 || kDepth == 2, "one register set, or two used alternately");
+  if constexpr (kDepth == 2) {
+    while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{})) {
+    }
+  } else {
+    while (step(std::integral_constant<int, 0>{})) {
+    }
   }
 }
 

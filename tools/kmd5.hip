@@ -369,8 +369,9 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int NV = 5;
-  const char *names[NV] = {"v1", "v1 loads", "v1 alu", "prod", "prod main"};
+  const int NV = 9;
+  const char *names[NV] = {"v1", "v1 loads", "v1 alu", "prod", "prod main", "S4 d2", "S3 d1 3WG", "S3 d2 3WG",
+                           "S3 d1 2WG"};
   uint8_t *ws;
   CK(hipMalloc(&ws, hc::md5_workspace_bytes(N)));
   for (auto &k : cases) {
@@ -396,10 +397,18 @@ int main(int argc, char **argv) {
                              tails, o);
           break;
         case 3: CK(hc::launch_md5(buf, doff, dlen, 0, 0, N, ws, o, cus, s)); break;
-        default:  // the main kernel alone, on the tail slots k_md5_v1_tail wrote (same format)
+        case 4:  // the main kernel alone, on the tail slots k_md5_v1_tail wrote (same format)
           hipLaunchKernelGGL((hc::k_md5<true, true>), dim3((unsigned)pgrid), dim3(256), 0, s, buf, doff, dlen,
                              (uint64_t)0, 0u, N, tails, o);
           break;
+#define KV(S, D, G)                                                                                              \
+  hipLaunchKernelGGL((hc::k_md5<true, true, S, D>), dim3((unsigned)std::min<uint64_t>((N + 1023) / 1024, cus * G)), \
+                     dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N, tails, o)
+        case 5: KV(4, 2, 2); break;
+        case 6: KV(3, 1, 3); break;
+        case 7: KV(3, 2, 3); break;
+        default: KV(3, 1, 2); break;
+#undef KV
       }
     };
     run(0, ref);
