@@ -195,7 +195,7 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-template <bool kOff, bool kLen, int kStage = kMd5StageBlocks, int kDepth = 1>
+template <bool kOff, bool kLen, int kStage = kMd5StageBlocks, int kDepth = 1, bool kTable = true>
 __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restrict__ base,
                                                         const uint64_t *__restrict__ offs,
                                                         const uint32_t *__restrict__ lens, uint64_t stride,
@@ -331,12 +331,29 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     // the owner's last valid piece offset: pieces past the stage's blocks
     // re-read it (nb == 0: src is the tail workspace, offset 0)
     const uint32_t cap = nb ? 64u * nb - 16u : 0u;
+    if constexpr (kTable) {
+      // every lane posts {src, cap} in the pad column of its slot (the
+      // hand-off is done by now); a loader reads the 16 entries it serves,
+      // broadcast within its 16-lane group: 1 + 16 LDS instructions instead
+      // of 48 ds_bpermute
+      __builtin_amdgcn_wave_barrier();
+      H[lane * kPitch] = u32x4{(uint32_t)src, (uint32_t)(src >> 32), cap, 0u};
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (uint32_t q = 0; q < 16; q++) {
-      const uint32_t m = 4u * q + (lane >> 4);
-      const uint64_t t = ((uint64_t)shfl32((uint32_t)(src >> 32), m) << 32) | shfl32((uint32_t)src, m);
-      const uint32_t mc = shfl32(cap, m);
-      R[q] = *(gpiece)(t + (pj < mc ? pj : mc));
+      for (uint32_t q = 0; q < 16; q++) {
+        const u32x4 e = H[(4u * q + (lane >> 4)) * kPitch];
+        const uint64_t t = ((uint64_t)e.y << 32) | e.x;
+        R[q] = *(gpiece)(t + (pj < e.z ? pj : e.z));
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++) {
+        const uint32_t m = 4u * q + (lane >> 4);
+        const uint64_t t = ((uint64_t)shfl32((uint32_t)(src >> 32), m) << 32) | shfl32((uint32_t)src, m);
+        const uint32_t mc = shfl32(cap, m);
+        R[q] = *(gpiece)(t + (pj < mc ? pj : mc));
+      }
     }
   };
   uint32_t st[4] = {0, 0, 0, 0};

@@ -370,7 +370,7 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int NV = 8;
-  const char *names[NV] = {"v1", "v1 loads", "v1 alu", "prod", "prod main", "S4 d2", "v1 alu 2w/SIMD",
+  const char *names[NV] = {"v1", "v1 loads", "v1 alu", "prod", "prod main", "bpermute", "v1 alu 2w/SIMD",
                            "v1 alu 3w/SIMD"};
   uint8_t *ws;
   CK(hipMalloc(&ws, hc::md5_workspace_bytes(N)));
@@ -404,7 +404,10 @@ int main(int argc, char **argv) {
 #define KV(S, D, G)                                                                                              \
   hipLaunchKernelGGL((hc::k_md5<true, true, S, D>), dim3((unsigned)std::min<uint64_t>((N + 1023) / 1024, cus * G)), \
                      dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N, tails, o)
-        case 5: KV(4, 2, 2); break;
+        case 5:
+          hipLaunchKernelGGL((hc::k_md5<true, true, 4, 1, false>), dim3((unsigned)pgrid), dim3(256), 0, s, buf, doff,
+                             dlen, (uint64_t)0, 0u, N, tails, o);
+          break;
         case 6:
           hipLaunchKernelGGL(hc::k_md5_diag<2>, dim3(cus * 2), dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N,
                              tails, o);
