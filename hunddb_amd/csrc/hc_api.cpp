@@ -288,6 +288,10 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
   // direct DMA: uniform, densely packed (stride == ulen, 16-B multiple) and already pinned
   const bool direct = !off && !len && stride == ulen && ulen > 0 && (ulen & 15u) == 0 &&
                       (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && is_pinned(base);
+  // span DMA: off/len records in pinned memory, in increasing order with small
+  // gaps (records packed back to back, e.g. a data component): one H2D copy of
+  // the byte span per chunk, no CPU gather
+  const bool span_ok = !direct && (off || len) && is_pinned(base);
   uint64_t i = 0, chunks = 0, moved = 0;
   int rc = HC_OK;
   auto retire = [&](Slot &s) -> int {
@@ -319,7 +323,45 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
         break;
       }
       packed_uniform = true;
+    } else if (span_ok && [&] {
+                 // plan [i, j) as one span; keep its 16-B phase when the bytes
+                 // before the first block belong to the caller's buffer
+                 const uint64_t lo = blk_off(off, stride, i);
+                 uint64_t ph = (reinterpret_cast<uintptr_t>(base) + lo) & 15u;
+                 if (lo < ph) ph = 0;
+                 uint64_t hi = lo, payload = 0;
+                 while (j < n && j - i < maxmsg) {
+                   const uint64_t o = blk_off(off, stride, j);
+                   const uint32_t l = blk_len(len, ulen, j);
+                   if (o < hi && j > i) break;  // overlap or out of order: end the span
+                   const uint64_t nhi = std::max<uint64_t>(hi, o + l);
+                   if (nhi - lo + ph > P.chunk) break;
+                   s.pin_off[j - i] = o - lo + ph;
+                   s.pin_len[j - i] = l;
+                   hi = nhi;
+                   payload += l;
+                   j++;
+                 }
+                 pos = hi - lo + ph;
+                 if (j == i || pos > payload + payload / 4 + (64u << 10)) {  // gaps: gather instead
+                   j = i;
+                   pos = 0;
+                   return false;
+                 }
+                 return hipMemcpyAsync(s.dbuf, base + lo - ph, pos, hipMemcpyHostToDevice, s.stream) == hipSuccess;
+               }()) {
+      const uint64_t nb = j - i;
+      packed_uniform = false;
+      if (hipMemcpyAsync(s.doff, s.pin_off, nb * 8, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+          hipMemcpyAsync(s.dlen, s.pin_len, nb * 4, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+        rc = HC_E_HIP;
+        break;
+      }
     } else {
+      if (j != i) {  // the span copy failed to enqueue
+        rc = HC_E_HIP;
+        break;
+      }
       // plan the chunk: blocks [i, j) packed at 16-B aligned offsets
       bool uniform = true;
       while (j < n && j - i < maxmsg) {

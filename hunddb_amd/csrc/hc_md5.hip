@@ -444,9 +444,10 @@ hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const int tgrid = (int)((n + 255) / 256 < (uint64_t)cus * 8 ? (n + 255) / 256 : (uint64_t)cus * 8);
-  // 2 workgroups (8 waves) per CU fit the LDS; a wave's range should give its
-  // 64 lanes several messages
-  uint64_t grid = (n + 64 * 4 * kMd5Waves - 1) / (64 * 4 * kMd5Waves);
+  // 2 workgroups (8 waves) per CU fit the LDS; below 512 workgroups' worth,
+  // one message per lane per wave range (a small batch -- one host staging
+  // chunk of ~7k records -- still spreads over the chip)
+  uint64_t grid = (n + 64 * kMd5Waves - 1) / (64 * kMd5Waves);
   if (grid > (uint64_t)cus * 2) grid = (uint64_t)cus * 2;
   const dim3 g((unsigned)grid), b(64 * kMd5Waves), tg(tgrid), tb(256);
 #define HC_MD5_LAUNCH(O, L)                                                                                 \

@@ -237,6 +237,53 @@ def test_host_entries(cuda, hc, oracle, golden):
     assert str(err) == "invalid block data" and fb == 1
 
 
+def test_host_span_dma_pinned(cuda, hc, oracle):
+    """off/len host batches in PINNED memory take the span-DMA path (one H2D
+    copy of the byte span per chunk, no CPU gather): records back to back at an
+    odd start, with small gaps, spanning several staging chunks; out-of-order
+    and widely gapped offsets fall back to the gather path.  Every word vs the
+    oracle; verify finds the corrupted block; md5 leaves vs the oracle."""
+    torch = cuda
+    from hunddb_amd import merkle as M
+    rng = np.random.default_rng(41)
+    n = 40_000
+    lens = rng.integers(0, 9000, n).astype(np.uint32)
+    gaps = np.where(rng.random(n) < 0.1, rng.integers(1, 40, n), 0).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    off += 3
+    total = int(off[-1] + lens[-1]) + 64
+    t = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    host = t.numpy()
+    host[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    assert total > 2 * (64 << 20)  # several staging chunks
+    want = oracle.crc32_messages(host, off, lens)
+    assert (hc.crc32_messages(host, off, lens) == want).all()
+    assert (hc.crc32_blocks(host, off=off, lens=lens) == oracle.crc32_blocks(host, off=off, lens=lens)).all()
+    perm = rng.permutation(n)  # out of order: gather path
+    assert (hc.crc32_messages(host, off[perm], lens[perm]) == want[perm]).all()
+    wide = off * 3 // 2  # gaps of a third: gather path
+    keep = wide + lens < total
+    assert (hc.crc32_messages(host, wide[keep], lens[keep]) ==
+            oracle.crc32_messages(host, wide[keep], lens[keep])).all()
+    mw = np.empty((n, 16), np.uint8)
+    oracle.lib().oc_md5_messages(host.ctypes.data, off.ctypes.data, lens.ctypes.data, mw.ctypes.data, n)
+    assert (M.md5_records(host, off, lens) == mw).all()
+    # 4 KiB blocks back to back in pinned memory, given as off/len: stamp, verify, corrupt
+    nb = 20_000
+    tb = torch.empty(nb * 4096, dtype=torch.uint8, pin_memory=True)
+    blocks = tb.numpy()
+    blocks[:] = rng.integers(0, 256, blocks.size, dtype=np.uint8)
+    boff = np.arange(nb, dtype=np.uint64) * 4096
+    blen = np.full(nb, 4096, np.uint32)
+    hc.stamp_blocks(blocks, off=boff, lens=blen)
+    err, bm, fb = hc.verify_blocks(blocks, off=boff, lens=blen)
+    assert err is None and fb == -1
+    blocks[4096 * 17_777 + 1000] ^= 0x80
+    err, bm, fb = hc.verify_blocks(blocks, off=boff, lens=blen)
+    assert str(err) == "CRC mismatch in block" and fb == 17_777
+
+
 def test_add_crcs_to_data_gpu(cuda, hc, oracle):
     """AddCRCsToData (crc_util.go:41-64) over multi-hundred-block inputs runs on the GPU."""
     rng = np.random.default_rng(12)

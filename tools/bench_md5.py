@@ -8,6 +8,8 @@ CheckIntegrity (lsm/sstable/sstable.go:2352-2411) on device-resident records.
            4096-B records (uniform stride).  Rate = record bytes / launch time.
   levels   NewMerkleTree(leaves, true) parents (k_merkle_level per level) over
            --leaves leaves.  Rate = leaves / s.
+  host     --host-records log-uniform records in pinned HOST memory through
+           hc_md5_messages (PCIe-inclusive).
   cpu      hashlib.md5 (OpenSSL) on one host core over a sample of the
            record workload.
 
@@ -48,7 +50,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
-    ap.add_argument("--only", default="", help="run only this part: loguniform | 4096 | levels")
+    ap.add_argument("--only", default="", help="run only this part: loguniform | 4096 | levels | host")
+    ap.add_argument("--host-records", type=int, default=500_000)
     args = ap.parse_args()
 
     import torch
@@ -63,6 +66,33 @@ def main():
         leaves_4096(args, torch, crc, M, dev)
     if args.only in ("", "levels"):
         levels(args, torch, crc, M, dev, rng)
+    if args.only in ("", "host"):
+        host_records(args, torch, M, rng)
+
+
+def host_records(args, torch, M, rng):
+    """CheckIntegrity from host memory: records in pinned host memory through
+    hc_md5_messages (pinned staging, H2D, k_md5_tail + k_md5, D2H of the
+    digests, overlapped).  PCIe-inclusive rate = record bytes / wall time."""
+    n = args.host_records
+    lens = np.minimum(np.exp(rng.uniform(np.log(64), np.log(65536), n)), 65536).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(off[-1] + lens[-1])
+    t = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    buf = t.numpy()
+    buf[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    M.md5_records(buf, off[:1000], lens[:1000])  # warm the pipeline
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = M.md5_records(buf, off, lens)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    for i in rng.integers(0, n, 500):
+        assert out[i].tobytes() == hashlib.md5(buf[int(off[i]):int(off[i]) + int(lens[i])]).digest()
+    print(json.dumps({"bench": "md5_host_pinned", "records": n, "bytes": total, "best_s": round(best, 4),
+                      "GBps": round(total / best / 1e9, 2)}), flush=True)
 
 
 def leaves_loguniform(args, torch, crc, M, dev, rng):
