@@ -262,9 +262,10 @@ bool is_pinned(const void *p) {
 
 thread_local uint64_t t_host_bytes = 0;  // bytes moved by the last host batch (stats)
 
-// Runs CRCs of host blocks on the GPU; results into crc_out[0..n).  Blocks
-// larger than one staging slot are rejected (HC_E_ARG): the on-disk block
-// sizes are 4-16 KiB (utils/config/config.go:137, README.md:191,255).
+// Runs CRCs of host blocks on the GPU; results into crc_out[0..n).  A block
+// or message larger than one staging slot (HC_CHUNK_MB, 64 MiB) is hashed on
+// its own (oversize): on-disk blocks are 4-16 KiB (utils/config/config.go:137,
+// README.md:191,255), but GetCRC / md5.Sum take records of any size.
 // md5_out != nullptr: MD5 digests of whole messages instead (row f4; crc_out unused).
 constexpr uint64_t kMd5MaxPerChunk = 262144;  // bounds the per-message MD5 workspace of a slot
 int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
@@ -303,6 +304,35 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     else
       std::memcpy(crc_out + s.i0, s.pin_crc, s.nb * 4);
     return HC_OK;
+  };
+  // A block or message larger than a staging slot (records are uint32-sized):
+  // its own device buffer, copied and hashed synchronously on the slot's stream.
+  auto oversize = [&](Slot &s, uint64_t k) -> int {
+    const uint64_t o = blk_off(off, stride, k);
+    const uint32_t l = blk_len(len, ulen, k);
+    uint8_t *d = nullptr;
+    int r = HC_OK;
+    if (hipMallocAsync(reinterpret_cast<void **>(&d), (size_t)l + 16, s.stream) != hipSuccess) return HC_E_NOMEM;
+    if (hipMemcpyAsync(d, base + o, l, hipMemcpyHostToDevice, s.stream) != hipSuccess) r = HC_E_HIP;
+    if (r == HC_OK && md5) {
+      if (launch_md5(d, nullptr, nullptr, l, l, 1, s.dtail, s.dmd5, g_dev[dev].cus, s.stream) != hipSuccess ||
+          hipMemcpyAsync(s.pin_md5, s.dmd5, 16, hipMemcpyDeviceToHost, s.stream) != hipSuccess)
+        r = HC_E_HIP;
+    } else if (r == HC_OK) {
+      r = dispatch(dev, d, nullptr, nullptr, l, l, 1, s.dcrc, nullptr, nullptr, flags, s.stream, l);
+      if (r == HC_OK && hipMemcpyAsync(s.pin_crc, s.dcrc, 4, hipMemcpyDeviceToHost, s.stream) != hipSuccess)
+        r = HC_E_HIP;
+    }
+    if (hipFreeAsync(d, s.stream) != hipSuccess && r == HC_OK) r = HC_E_HIP;
+    if (hipStreamSynchronize(s.stream) != hipSuccess && r == HC_OK) r = HC_E_HIP;
+    if (r == HC_OK) {
+      if (md5)
+        std::memcpy(md5_out + 16 * k, s.pin_md5, 16);
+      else
+        crc_out[k] = s.pin_crc[0];
+      moved += l;
+    }
+    return r;
   };
   while (i < n && rc == HC_OK) {
     Slot &s = P.slot[chunks % kSlots];
@@ -374,9 +404,10 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
         pos = need;
         j++;
       }
-      if (j == i) {
-        rc = HC_E_ARG;  // a single block larger than the staging slot
-        break;
+      if (j == i) {  // one block/message larger than a staging slot: on its own
+        if ((rc = oversize(s, i)) != HC_OK) break;
+        i++;
+        continue;
       }
       const uint64_t nb = j - i;
       // gather into pinned staging on copy_threads threads

@@ -104,6 +104,17 @@ def test_md5_uniform_stride(cuda, oracle, hc):
         assert (out.cpu().numpy().reshape(-1, 16) == want).all(), ulen
 
 
+def test_host_records_larger_than_staging(cuda, oracle, hc):
+    """Records over the 64 MiB staging slot (md5.Sum / GetCRC take any size):
+    hashed on their own between ordinary records, host memory."""
+    rng = np.random.default_rng(9)
+    lens = np.array([100, (80 << 20) + 13, 5000, 70 << 20, 0, 333], np.uint32)
+    buf, off, ln = _packed(rng, lens, pad=1)
+    got = M.md5_records(buf, off, ln)
+    assert (got == _oracle_md5(oracle, buf, off, ln)).all()
+    assert (hc.crc32_messages(buf, off, ln) == oracle.crc32_messages(buf, off, ln)).all()
+
+
 def test_md5_host_batch(cuda, oracle):
     """hc_md5_messages: host records through the pinned pipeline (several
     chunks: more records than one slot's 262144)."""
