@@ -280,8 +280,9 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
   const uint64_t maxmsg = md5 ? std::min<uint64_t>(P.maxblk, kMd5MaxPerChunk) : P.maxblk;
   if (md5)
     for (auto &sl : P.slot)
-      if (!sl.dtail && (hipMalloc(reinterpret_cast<void **>(&sl.dtail), md5_workspace_bytes(maxmsg)) != hipSuccess ||
-                        hipMalloc(reinterpret_cast<void **>(&sl.dmd5), maxmsg * 16) != hipSuccess ||
+      if (!sl.dmd5 && ((md5_workspace_bytes(maxmsg) &&
+                        hipMalloc(reinterpret_cast<void **>(&sl.dtail), md5_workspace_bytes(maxmsg)) != hipSuccess) ||
+                       hipMalloc(reinterpret_cast<void **>(&sl.dmd5), maxmsg * 16) != hipSuccess ||
                         hipHostMalloc(reinterpret_cast<void **>(&sl.pin_md5), maxmsg * 16, hipHostMallocDefault) !=
                             hipSuccess))
         return HC_E_NOMEM;

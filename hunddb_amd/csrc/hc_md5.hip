@@ -5,9 +5,6 @@
 //
 // MD5 (RFC 1321) chains 64-byte blocks, so one message is one sequential
 // chain: the parallelism is across messages, one lane per message.
-//   * k_md5_tail (thread per message): writes each message's padded tail
-//     blocks (its last len % 64 bytes, 0x80, zeros, the bit length) into a
-//     128-byte slot of the workspace.
 //   * k_md5 (lane per message): lanes take messages as they
 //     free up, longest length class first; message bytes reach the lanes in
 //     stages of up to 4 blocks, fetched by coalesced 256-byte pieces and
@@ -82,96 +79,22 @@ __device__ __forceinline__ void md5_init(uint32_t (&st)[4]) {
 __device__ __forceinline__ uint32_t uni_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ---------------------------------------------------------------------------
-// Thread per message: the 128-byte tail slot = the message's last len % 64 data
-// bytes, 0x80, zeros and the 64-bit little-endian bit length at byte 56 (tail
-// < 56 bytes: one block) or 120 (two blocks).  The data bytes come from the
-// aligned 16-byte chunks that hold them (at most 5; an aligned chunk holding
-// a message byte never leaves that byte's page; chunks past the tail re-read
-// the last one), funnel-shifted per lane.  The second block is written only
-// when the message needs it (len % 64 >= 56).
-template <bool kOff, bool kLen>
-__global__ __launch_bounds__(256) void k_md5_tail(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-                                                  const uint32_t *__restrict__ lens, uint64_t stride, uint32_t ulen,
-                                                  uint64_t n, uint8_t *__restrict__ tails) {
-  for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t o;
-    uint32_t l;
-    if constexpr (kOff)
-      o = offs[m];
-    else
-      o = m * stride;
-    if constexpr (kLen)
-      l = lens[m];
-    else
-      l = ulen;
-    const uint32_t r = l & 63u;
-    const uintptr_t tp = (uintptr_t)base + o + (l & ~63u);
-    const uint32_t sh = (uint32_t)(tp & 15u);
-    const uint32_t nc = r ? (sh + r + 15) >> 4 : 0u;  // aligned chunks holding the tail bytes (<= 5)
-    uint32_t D[21];
-#pragma unroll
-    for (int j = 0; j < 21; j++) D[j] = 0;
-    if (nc) {
-#pragma unroll
-      for (int j = 0; j < 5; j++) {
-        const uint4 v = *reinterpret_cast<const uint4 *>((tp - sh) + 16u * ((uint32_t)j < nc ? (uint32_t)j : nc - 1u));
-        D[4 * j] = v.x;
-        D[4 * j + 1] = v.y;
-        D[4 * j + 2] = v.z;
-        D[4 * j + 3] = v.w;
-      }
-    }
-    // dword k of the tail = alignbyte(D[q + k + 1], D[q + k], sh & 3), q = sh / 4
-    const uint32_t q = sh >> 2, b = sh & 3u;
-    auto pick = [&](int k) {  // D[q + k], q in 0..3
-      const uint32_t x = (q & 1u) ? D[k + 1] : D[k], y = (q & 1u) ? D[k + 3] : D[k + 2];
-      return (q & 2u) ? y : x;
-    };
-    uint32_t w[32];
-    uint32_t lo = pick(0);
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const uint32_t hi = pick(i + 1);
-      uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, b);
-      lo = hi;
-      const int32_t nb = (int32_t)r - 4 * i;  // tail bytes in this word
-      v &= nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
-      v |= (uint32_t)i == (r >> 2) ? (0x80u << (8 * (r & 3u))) : 0u;
-      w[i] = v;
-    }
-#pragma unroll
-    for (int i = 16; i < 32; i++) w[i] = 0;
-    const uint64_t bits = (uint64_t)l * 8;
-    const bool two = r >= 56;
-    w[14] = two ? w[14] : (uint32_t)bits;
-    w[15] = two ? w[15] : (uint32_t)(bits >> 32);
-    w[30] = two ? (uint32_t)bits : 0u;
-    w[31] = two ? (uint32_t)(bits >> 32) : 0u;
-    uint4 *dst = reinterpret_cast<uint4 *>(tails + m * 128);
-#pragma unroll
-    for (int k = 0; k < 4; k++) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-    if (two) {
-#pragma unroll
-      for (int k = 4; k < 8; k++) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Lane per message, blocks staged by coalesced loads through LDS.
 //
 // A lane consumes its message in stages of up to 4 blocks (256 B) and ends it
-// with a stage from its tail slot (k_md5_tail, 1-2 blocks).  The 64 stages of
-// a wave are fetched by 16 wave-instructions, each covering 4 messages x 256
-// contiguous bytes (16 lanes x 16 B per message): HBM sees >= 128-B pieces,
-// not the 64 scattered half-lines of a lane-per-message load (1.8 vs 5.5-6.2
-// TB/s in tools/kmd5's probes).  The pieces go to the wave's LDS image (slot m
-// = the stage of lane m, odd pitch: conflict-free writes and per-lane
-// ds_read_b128 at immediate offsets); the next stage is in flight while one
-// is compressed (kDepth 2 -- two in flight -- measured no faster: the kernel
-// is VALU-bound at 2 waves per SIMD, tools/kmd5).  Pieces past a stage's
-// blocks re-read its last piece: no load leaves a message's full blocks or
-// its tail slot.  kStage 3 (3 workgroups per CU) measured slower.
+// with a tail stage: the aligned 16-B chunks holding its last len % 64 bytes,
+// padded in the lane's LDS slot into 1-2 blocks (0x80, zeros, bit length; a
+// separate tail pass measured no faster).  The 64 stages of a wave are
+// fetched by 16 wave-instructions, each covering 4 messages x 256 contiguous
+// bytes (16 lanes x 16 B per message): HBM sees >= 128-B pieces, not the 64
+// scattered half-lines of a lane-per-message load (1.8 vs 5.5-6.2 TB/s in
+// tools/kmd5's probes).  The pieces go to the wave's LDS image (slot m = the
+// stage of lane m, odd pitch: conflict-free writes and per-lane ds_read_b128
+// at immediate offsets); two stages are in flight while one is compressed
+// (kDepth 1 measures within noise of 2: the kernel is VALU-bound at 2 waves
+// per SIMD, tools/kmd5).  Pieces past a stage's last valid one
+// re-read it: no load leaves a message's full blocks or the aligned chunks
+// of its tail.  kStage 3 (3 workgroups per CU) measured slower.
 //
 // Free lanes take messages from 64-entry metadata windows (lane j holds
 // message wbase + j; the next window is prefetched), by ballot rank through
@@ -195,12 +118,11 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-template <bool kOff, bool kLen, int kStage = kMd5StageBlocks, int kDepth = 1, bool kTable = true>
+template <bool kOff, bool kLen, int kStage = kMd5StageBlocks, int kDepth = 2, bool kTable = true>
 __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restrict__ base,
                                                         const uint64_t *__restrict__ offs,
                                                         const uint32_t *__restrict__ lens, uint64_t stride,
-                                                        uint32_t ulen, uint64_t n, const uint8_t *__restrict__ tails,
-                                                        uint8_t *__restrict__ out16) {
+                                                        uint32_t ulen, uint64_t n, uint8_t *__restrict__ out16) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   // stage pieces are addressed as integers: name the global address space, or
   // they become flat loads, which also count on lgkmcnt (the LDS waits of the
@@ -255,7 +177,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   bool act = false, fresh = false;
   uint32_t msg = 0;  // message index - p0 (a wave's range is < 2^32 messages)
   uint64_t p = 0;  // address of the message's next full block
-  uint32_t nfull = 0, ntail = 0;
+  uint32_t nfull = 0, ntail = 0, mlen = 0;
   auto assign = [&]() {
     uint64_t need = __ballot(!act);
     if (!need || !more) return;
@@ -287,6 +209,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
         p = (uint64_t)(uintptr_t)base + (((uint64_t)h.y << 32) | h.x);
         nfull = h.z >> 6;
         ntail = (h.z & 63u) < 56 ? 1u : 2u;
+        mlen = h.z;
         act = true;
         fresh = true;
       }
@@ -296,41 +219,53 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     }
   };
   // Stages are planned kDepth ahead of the one being compressed: the lane's
-  // next blocks of its message (src, nb), or its tail slot (fin: the digest
-  // is complete after it; the lane is free for the next message at once).
+  // next blocks of its message (src, nb), or its tail (fin: the digest is
+  // complete after it; the lane is free for the next message at once).
   struct Stage {
     uint32_t msg;
     uint32_t nb;  // blocks, 0 = none
     bool first, fin;
+    uint32_t tinfo, tlen;  // tail stage: 16-B phase | tail bytes << 4; message length
   };
-  auto plan = [&](Stage &t, uint64_t &src) {
+  // src / cap: the stage's first piece and the offset of its last valid one
+  // (pieces past it re-read it)
+  auto plan = [&](Stage &t, uint64_t &src, uint32_t &cap) {
     assign();
     t.first = fresh;
     fresh = false;
     t.fin = false;
     t.msg = msg;
+    t.tinfo = 0;
+    t.tlen = 0;
     if (!act) {
-      src = (uint64_t)(uintptr_t)tails;
+      src = (uint64_t)(uintptr_t)out16;
+      cap = 0;
       t.nb = 0;
     } else if (nfull) {
       src = p;
       t.nb = nfull < (uint32_t)kStage ? nfull : (uint32_t)kStage;
+      cap = 64u * t.nb - 16u;
       p += 64u * t.nb;
       nfull -= t.nb;
     } else {
-      src = (uint64_t)(uintptr_t)tails + (p0 + msg) * 128;
       t.nb = ntail;
       t.fin = true;
       act = false;
+      // the tail bytes come as the aligned 16-B chunks that hold them (an
+      // aligned chunk holding a message byte stays inside that byte's page);
+      // compress_stage pads them in place
+      const uint32_t r = mlen & 63u, ph = (uint32_t)(p & 15u);
+      const uint32_t nck = r ? (ph + r + 15u) >> 4 : 0u;
+      src = nck ? (p & ~(uint64_t)15) : (uint64_t)(uintptr_t)out16;
+      cap = nck ? 16u * (nck - 1u) : 0u;
+      t.tinfo = ph | (r << 4);
+      t.tlen = mlen;
     }
   };
   // 16 wave-instructions per stage; each covers 4 messages x kSlot chunks
   // (lanes 16r + j, j < kSlot; with kSlot < 16 the other lanes re-read a piece)
   const uint32_t pj = 16u * (lane & 15u);  // this lane's piece offset in every stage
-  auto issue = [&](u32x4(&R)[16], uint64_t src, uint32_t nb) {
-    // the owner's last valid piece offset: pieces past the stage's blocks
-    // re-read it (nb == 0: src is the tail workspace, offset 0)
-    const uint32_t cap = nb ? 64u * nb - 16u : 0u;
+  auto issue = [&](u32x4(&R)[16], uint64_t src, uint32_t cap) {
     if constexpr (kTable) {
       // every lane posts {src, cap} in the pad column of its slot (the
       // hand-off is done by now); a loader reads the 16 entries it serves,
@@ -359,6 +294,42 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   uint32_t st[4] = {0, 0, 0, 0};
   auto compress_stage = [&](const Stage &t) {
     if (t.first) md5_init(st);
+    {
+      if (t.fin) {
+        // the padded tail blocks, built in the lane's own slot: the last
+        // len % 64 bytes (funnel-shifted out of the aligned chunks), 0x80,
+        // zeros, the bit length at byte 56 (or 120: a second block)
+        const uint32_t ph = t.tinfo & 15u, r = t.tinfo >> 4, sh = ph & 3u;
+        const uint32_t *Dw = reinterpret_cast<const uint32_t *>(L + lane * kPitch) + (ph >> 2);
+        uint32_t w[16];
+        uint32_t lo = Dw[0];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          const uint32_t hi = Dw[k + 1];
+          uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+          lo = hi;
+          const int32_t nbk = (int32_t)r - 4 * k;  // tail bytes in this word
+          v &= nbk >= 4 ? 0xFFFFFFFFu : (nbk <= 0 ? 0u : (1u << (8 * nbk)) - 1u);
+          v |= (uint32_t)k == (r >> 2) ? (0x80u << (8 * (r & 3u))) : 0u;
+          w[k] = v;
+        }
+        const uint64_t bits = (uint64_t)t.tlen * 8;
+        const bool two = r >= 56;
+        if (!two) {
+          w[14] = (uint32_t)bits;
+          w[15] = (uint32_t)(bits >> 32);
+        }
+        u32x4 *S = L + lane * kPitch;
+#pragma unroll
+        for (int k = 0; k < 4; k++) S[k] = u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+        if (two) {
+          S[4] = u32x4{0u, 0u, 0u, 0u};
+          S[5] = u32x4{0u, 0u, 0u, 0u};
+          S[6] = u32x4{0u, 0u, 0u, 0u};
+          S[7] = u32x4{0u, 0u, (uint32_t)bits, (uint32_t)(bits >> 32)};
+        }
+      }
+    }
     for (uint32_t b = 0; b < (uint32_t)kStage; b++) {
       if (b < t.nb) {
         uint32_t M[16];
@@ -380,8 +351,9 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
 #pragma unroll
   for (int d = 0; d < kDepth; d++) {
     uint64_t src;
-    plan(T[d], src);
-    issue(R[d], src, T[d].nb);
+    uint32_t cap;
+    plan(T[d], src, cap);
+    issue(R[d], src, cap);
   }
   // one step on register set d (a template argument, so R[d] stays in registers)
   auto step = [&](auto dc) -> bool {
@@ -395,8 +367,9 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     __builtin_amdgcn_wave_barrier();
     const Stage cur = T[d];
     uint64_t src;
-    plan(T[d], src);
-    issue(R[d], src, T[d].nb);  // in flight while the older stages are compressed
+    uint32_t cap;
+    plan(T[d], src, cap);
+    issue(R[d], src, cap);  // in flight while the older stages are compressed
     compress_stage(cur);
     __builtin_amdgcn_wave_barrier();
     return true;
@@ -438,23 +411,23 @@ __global__ void k_md5_empty(uint8_t *out16) {  // md5.Sum([]byte{}) (merkle_tree
 
 }  // namespace
 
-uint64_t md5_workspace_bytes(uint64_t n) { return n * 128; }
+uint64_t md5_workspace_bytes(uint64_t n) {
+  (void)n;
+  return 0;  // the tail blocks are built inside k_md5: no workspace
+}
 
 hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const int tgrid = (int)((n + 255) / 256 < (uint64_t)cus * 8 ? (n + 255) / 256 : (uint64_t)cus * 8);
+  (void)workspace;  // unused: md5_workspace_bytes() == 0
   // 2 workgroups (8 waves) per CU fit the LDS; below 512 workgroups' worth,
   // one message per lane per wave range (a small batch -- one host staging
   // chunk of ~7k records -- still spreads over the chip)
   uint64_t grid = (n + 64 * kMd5Waves - 1) / (64 * kMd5Waves);
   if (grid > (uint64_t)cus * 2) grid = (uint64_t)cus * 2;
-  const dim3 g((unsigned)grid), b(64 * kMd5Waves), tg(tgrid), tb(256);
-#define HC_MD5_LAUNCH(O, L)                                                                                 \
-  do {                                                                                                      \
-    hipLaunchKernelGGL((k_md5_tail<O, L>), tg, tb, 0, s, base, off, len, stride, ulen, n, workspace);       \
-    hipLaunchKernelGGL((k_md5<O, L>), g, b, 0, s, base, off, len, stride, ulen, n, workspace, out16);      \
-  } while (0)
+  const dim3 g((unsigned)grid), b(64 * kMd5Waves);
+#define HC_MD5_LAUNCH(O, L)                                                                                  \
+  hipLaunchKernelGGL((k_md5<O, L>), g, b, 0, s, base, off, len, stride, ulen, n, out16)
   if (off && len)
     HC_MD5_LAUNCH(true, true);
   else if (off)

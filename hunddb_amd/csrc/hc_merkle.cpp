@@ -150,7 +150,7 @@ int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const
   hipStream_t s = static_cast<hipStream_t>(stream);
   void *ws = workspace;
   int rc = HC_OK;
-  if (!ws && hipMallocAsync(&ws, md5_workspace_bytes(n), s) != hipSuccess) rc = HC_E_NOMEM;
+  if (!ws && md5_workspace_bytes(n) && hipMallocAsync(&ws, md5_workspace_bytes(n), s) != hipSuccess) rc = HC_E_NOMEM;
   if (rc == HC_OK && launch_md5(static_cast<const uint8_t *>(base), off, len, stride, ulen, n,
                                 static_cast<uint8_t *>(ws), out16, cus, s) != hipSuccess)
     rc = HC_E_HIP;

@@ -45,7 +45,7 @@ def md5_records(buf, off, lens) -> np.ndarray:
 
 
 def dev_md5_messages(buf, out16, off=None, lens=None, stride=0, ulen=0, n=None, workspace=None, stream=None):
-    """Device form (k_md5_tail + k_md5): digests of base[off(i):+len(i)] into the
+    """Device form (k_md5): digests of base[off(i):+len(i)] into the
     uint8 tensor out16 (n*16 bytes).  Asynchronous on `stream`."""
     if n is None:
         n = off.numel() if off is not None else buf.numel() // max(1, stride)

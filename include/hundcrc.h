@@ -194,9 +194,8 @@ int hc_md5_messages(const uint8_t *base, const uint64_t *off, const uint32_t *le
 /* Device form: message i = base[off(i) .. +len(i)) (off/len arrays or
  * i*stride / ulen, as hc_dev_crc32_blocks), digests into out16 (device,
  * 16-B aligned).  workspace: device memory of hc_md5_workspace_bytes(n)
- * bytes, 16-B aligned (the messages' padded tail blocks and the per-wave
- * schedule), or NULL to take it stream-ordered from the device pool.
- * Kernels k_md5_plan + k_md5 (lane per message). */
+ * bytes (currently 0: the kernel pads each message's tail itself), or NULL.
+ * Kernel k_md5 (lane per message). */
 uint64_t hc_md5_workspace_bytes(uint64_t n);
 int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                         uint32_t ulen, uint64_t n, uint8_t *out16, void *workspace, void *stream);

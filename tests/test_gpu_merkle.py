@@ -1,4 +1,4 @@
-"""Row f4 on the GPU: md5.Sum leaves (k_md5_tail + k_md5) and Merkle levels
+"""Row f4 on the GPU: md5.Sum leaves (k_md5) and Merkle levels
 (k_merkle_level) through the C ABI vs the oracle (oracle/oc_merkle.c, pinned
 to hashlib and merkle_tree_test.go's roots in test_merkle.py), bit-exact.
 

@@ -2,7 +2,7 @@
 """Row f4 benchmarks: the Merkle/MD5 data half of
 CheckIntegrity (lsm/sstable/sstable.go:2352-2411) on device-resident records.
 
-  leaves   md5.Sum of every record (k_md5_tail + k_md5, hc_dev_md5_messages):
+  leaves   md5.Sum of every record (k_md5, hc_dev_md5_messages):
            --records records, serialized sizes log-uniform 64 B .. 64 KiB
            (config 5's record sizes) packed back to back, unaligned; and
            4096-B records (uniform stride).  Rate = record bytes / launch time.
@@ -72,7 +72,7 @@ def main():
 
 def host_records(args, torch, M, rng):
     """CheckIntegrity from host memory: records in pinned host memory through
-    hc_md5_messages (pinned staging, H2D, k_md5_tail + k_md5, D2H of the
+    hc_md5_messages (span DMA or pinned staging, H2D, k_md5, D2H of the
     digests, overlapped).  PCIe-inclusive rate = record bytes / wall time."""
     n = args.host_records
     lens = np.minimum(np.exp(rng.uniform(np.log(64), np.log(65536), n)), 65536).astype(np.uint32)

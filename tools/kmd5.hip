@@ -9,7 +9,7 @@
 //               loading its own 64-B blocks; tail slots by k_md5_v1_tail
 //   v1 loads    v1's memory pattern, XOR fold instead of the compression
 //   v1 alu      v1's control flow and compression, no data loads
-//   prod        launch_md5: k_md5_tail + k_md5 (staged through LDS)
+//   prod        launch_md5: k_md5 (staged through LDS, tails padded in LDS)
 //   prod main   k_md5 alone
 // plus memory-pattern probes (4096-B records, XOR fold): each lane reading its
 // own record in 64..512-B chunks, and a wave reading 64 records in rotation
@@ -370,10 +370,10 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int NV = 8;
-  const char *names[NV] = {"v1", "v1 loads", "v1 alu", "prod", "prod main", "bpermute", "v1 alu 2w/SIMD",
-                           "v1 alu 3w/SIMD"};
+  const char *names[NV] = {"v1", "v1 loads", "v1 alu", "prod", "prod main", "bpermute", "S4 d1",
+                           "v1 alu 2w/SIMD"};
   uint8_t *ws;
-  CK(hipMalloc(&ws, hc::md5_workspace_bytes(N)));
+  CK(hipMalloc(&ws, hc::md5_workspace_bytes(N) + 16));
   for (auto &k : cases) {
     CK(hipMemcpy(doff, k.off.data(), N * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dlen, k.len.data(), N * 4, hipMemcpyHostToDevice));
@@ -399,21 +399,18 @@ int main(int argc, char **argv) {
         case 3: CK(hc::launch_md5(buf, doff, dlen, 0, 0, N, ws, o, cus, s)); break;
         case 4:  // the main kernel alone, on the tail slots k_md5_v1_tail wrote (same format)
           hipLaunchKernelGGL((hc::k_md5<true, true>), dim3((unsigned)pgrid), dim3(256), 0, s, buf, doff, dlen,
-                             (uint64_t)0, 0u, N, tails, o);
+                             (uint64_t)0, 0u, N, o);
           break;
 #define KV(S, D, G)                                                                                              \
   hipLaunchKernelGGL((hc::k_md5<true, true, S, D>), dim3((unsigned)std::min<uint64_t>((N + 1023) / 1024, cus * G)), \
-                     dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N, tails, o)
+                     dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N, o)
         case 5:
           hipLaunchKernelGGL((hc::k_md5<true, true, 4, 1, false>), dim3((unsigned)pgrid), dim3(256), 0, s, buf, doff,
-                             dlen, (uint64_t)0, 0u, N, tails, o);
+                             dlen, (uint64_t)0, 0u, N, o);
           break;
-        case 6:
-          hipLaunchKernelGGL(hc::k_md5_diag<2>, dim3(cus * 2), dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N,
-                             tails, o);
-          break;
+        case 6: KV(4, 1, 2); break;
         default:
-          hipLaunchKernelGGL(hc::k_md5_diag<2>, dim3(cus * 3), dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N,
+          hipLaunchKernelGGL(hc::k_md5_diag<2>, dim3(cus * 2), dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N,
                              tails, o);
           break;
 #undef KV
@@ -425,7 +422,7 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> a(N * 16), b(N * 16);
     CK(hipMemcpy(a.data(), ref, N * 16, hipMemcpyDeviceToHost));
     std::vector<uint64_t> mism(NV, 0);
-    for (int v = 3; v < 6; v++) {
+    for (int v = 3; v < 7; v++) {
       CK(hipMemset(out, 0, N * 16));
       run(v, out);
       CK(hipStreamSynchronize(s));
