@@ -420,10 +420,11 @@ hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s) {
   if (n == 0) return hipSuccess;
   (void)workspace;  // unused: md5_workspace_bytes() == 0
-  // 2 workgroups (8 waves) per CU fit the LDS; below 512 workgroups' worth,
-  // one message per lane per wave range (a small batch -- one host staging
-  // chunk of ~7k records -- still spreads over the chip)
-  uint64_t grid = (n + 64 * kMd5Waves - 1) / (64 * kMd5Waves);
+  // 2 workgroups (8 waves) per CU fit the LDS; a smaller batch gets 4 messages
+  // per lane per wave range (256 per wave): with heavy-tailed sizes, fewer and
+  // longer ranges balance better than more waves (200k log-uniform records:
+  // 1991 GB/s at 196 workgroups against 1284 at 512, profiles/r1/md5/dyn/)
+  uint64_t grid = (n + 256 * kMd5Waves - 1) / (256 * kMd5Waves);
   if (grid > (uint64_t)cus * 2) grid = (uint64_t)cus * 2;
   const dim3 g((unsigned)grid), b(64 * kMd5Waves);
 #define HC_MD5_LAUNCH(O, L)                                                                                  \

@@ -381,7 +381,7 @@ int main(int argc, char **argv) {
     const int grid = (int)((waves + 3) / 4);
     hipLaunchKernelGGL(hc::k_md5_v1_tail, dim3(cus * 8), dim3(256), 0, s, buf, doff, dlen, (uint64_t)0, 0u, N, tails);
     // k_md5's grid as launch_md5 sets it
-    const uint64_t pgrid = std::min<uint64_t>((N + 255) / 256, (uint64_t)cus * 2);
+    const uint64_t pgrid = std::min<uint64_t>((N + 1023) / 1024, (uint64_t)cus * 2);
     auto run = [&](int v, uint8_t *o) {
       switch (v) {
         case 0:
