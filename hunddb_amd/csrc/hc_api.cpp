@@ -187,12 +187,15 @@ struct Slot {
   bool busy = false;
   // MD5 batches (row f4), allocated on first use: tail workspace and digests
   uint8_t *dtail = nullptr, *dmd5 = nullptr, *pin_md5 = nullptr;
+  // span-DMA target (device only, HostPipe::span bytes), allocated on first use
+  uint8_t *dspan = nullptr;
 };
 
 struct HostPipe {
   int dev = -1;
   size_t chunk = 0;   // staging bytes per slot
   size_t maxblk = 0;  // metadata capacity per slot
+  size_t span = 0;    // span-DMA bytes per slot (device memory only: no pinned staging)
   Slot slot[kSlots];
   bool ok = false;
 
@@ -202,6 +205,10 @@ struct HostPipe {
     dev = d;
     chunk = (size_t)env_int("HC_CHUNK_MB", 64) << 20;
     maxblk = chunk / 64 + 1;
+    // span DMA needs no pinned staging, so its chunks can be larger: fewer,
+    // fuller kernels (the MD5 of one 64 MiB chunk of records is a few dozen
+    // waves -- too little parallelism to keep up with the copy)
+    span = std::max(chunk, (size_t)env_int("HC_SPAN_MB", 256) << 20);
     DeviceGuard g(dev);
     for (auto &s : slot) {
       if (hipHostMalloc(reinterpret_cast<void **>(&s.pin), chunk, hipHostMallocDefault) != hipSuccess ||
@@ -231,6 +238,7 @@ struct HostPipe {
       if (s.pin_len) (void)hipHostFree(s.pin_len);
       if (s.pin_crc) (void)hipHostFree(s.pin_crc);
       if (s.dbuf) (void)hipFree(s.dbuf);
+      if (s.dspan) (void)hipFree(s.dspan);
       if (s.doff) (void)hipFree(s.doff);
       if (s.dlen) (void)hipFree(s.dlen);
       if (s.dcrc) (void)hipFree(s.dcrc);
@@ -340,6 +348,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     if ((rc = retire(s)) != HC_OK) break;
     uint64_t j = i, pos = 0;
     bool packed_uniform;
+    uint8_t *dsrc = s.dbuf;  // the chunk's device copy
     uint32_t l0 = blk_len(len, ulen, i);
     if (direct) {
       j = std::min<uint64_t>(n, i + std::max<uint64_t>(1, P.chunk / ulen));
@@ -354,7 +363,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
         break;
       }
       packed_uniform = true;
-    } else if (span_ok && [&] {
+    } else if (span_ok && (s.dspan || hipMalloc(reinterpret_cast<void **>(&s.dspan), P.span) == hipSuccess) && [&] {
                  // plan [i, j) as one span; keep its 16-B phase when the bytes
                  // before the first block belong to the caller's buffer
                  const uint64_t lo = blk_off(off, stride, i);
@@ -366,7 +375,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
                    const uint32_t l = blk_len(len, ulen, j);
                    if (o < hi && j > i) break;  // overlap or out of order: end the span
                    const uint64_t nhi = std::max<uint64_t>(hi, o + l);
-                   if (nhi - lo + ph > P.chunk) break;
+                   if (nhi - lo + ph > P.span) break;
                    s.pin_off[j - i] = o - lo + ph;
                    s.pin_len[j - i] = l;
                    hi = nhi;
@@ -379,7 +388,8 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
                    pos = 0;
                    return false;
                  }
-                 return hipMemcpyAsync(s.dbuf, base + lo - ph, pos, hipMemcpyHostToDevice, s.stream) == hipSuccess;
+                 dsrc = s.dspan;
+                 return hipMemcpyAsync(s.dspan, base + lo - ph, pos, hipMemcpyHostToDevice, s.stream) == hipSuccess;
                }()) {
       const uint64_t nb = j - i;
       packed_uniform = false;
@@ -437,7 +447,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     const uint64_t nb = j - i;
     if (md5) {
       const bool u = packed_uniform;
-      if (launch_md5(s.dbuf, u ? nullptr : s.doff, u ? nullptr : s.dlen, l0, l0, nb, s.dtail, s.dmd5,
+      if (launch_md5(dsrc, u ? nullptr : s.doff, u ? nullptr : s.dlen, l0, l0, nb, s.dtail, s.dmd5,
                      g_dev[dev].cus, s.stream) != hipSuccess ||
           hipMemcpyAsync(s.pin_md5, s.dmd5, nb * 16, hipMemcpyDeviceToHost, s.stream) != hipSuccess) {
         rc = HC_E_HIP;
@@ -446,8 +456,8 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
       t_last = hc_launch_info{"k_md5", 0, nb, pos, 0, 256, 0};
     } else {
       rc = packed_uniform
-               ? dispatch(dev, s.dbuf, nullptr, nullptr, l0, l0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos)
-               : dispatch(dev, s.dbuf, s.doff, s.dlen, 0, 0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos);
+               ? dispatch(dev, dsrc, nullptr, nullptr, l0, l0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos)
+               : dispatch(dev, dsrc, s.doff, s.dlen, 0, 0, nb, s.dcrc, nullptr, nullptr, flags, s.stream, pos);
       if (rc != HC_OK) break;
       if (hipMemcpyAsync(s.pin_crc, s.dcrc, nb * 4, hipMemcpyDeviceToHost, s.stream) != hipSuccess) {
         rc = HC_E_HIP;
