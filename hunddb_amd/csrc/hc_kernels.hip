@@ -120,14 +120,28 @@ __device__ __forceinline__ void lane0_atomic_umin64(unsigned long long *p, uint6
 // ring depth (rows in flight per wave = kRing-1 while one is hashed), load
 // cache policy (0 plain, 1 nontemporal), block order (0: each wave owns a
 // contiguous run of blocks; 1: block b goes to wave b % W -- uniform layout
-// only) and kNull (timing-only build: rows are XOR-folded instead of
-// CRC'd, to measure the memory ceiling of exactly this access pattern).
-template <int W_, int R_, int P_, int O_, bool N_ = false>
+// only), kNull (timing-only build: rows are XOR-folded instead of
+// CRC'd, to measure the memory ceiling of exactly this access pattern),
+// kStage (rows land in a per-wave ring of kRing 1 KiB LDS slots by LDS-DMA,
+// global_load_lds_dwordx4, instead of a VGPR ring) and kS4Rep (replicas of
+// the 4-byte shift tables: fewer replicas leave LDS room for the ring; 0 =
+// no table, the shift is a 32x32 GF(2) mat-vec on the VALU).
+template <int W_, int R_, int P_, int O_, bool N_ = false, bool S_ = false, int S4_ = 4>
 struct FastCfg {
   static constexpr int kWaves = W_, kRing = R_, kPolicy = P_, kOrder = O_;
-  static constexpr bool kNull = N_;
+  static constexpr bool kNull = N_, kStage = S_;
+  static constexpr int kS4Rep = S4_;
+  static constexpr uint32_t kS4Bytes = 4096u * S4_;  // 0: s4 shift on the VALU
+  static constexpr uint32_t kRingBytes = S_ ? (uint32_t)W_ * R_ * kRowBytes : 0u;
+  static constexpr uint32_t kLdsBytes = kLdsMainBytes + kS4Bytes + kRingBytes;
+  static_assert(kLdsBytes <= 163840u, "LDS budget: 160 KiB per CU");
+  static_assert(S4_ == 0 || S4_ == 1 || S4_ == 2 || S4_ == 4, "s4 replicas");
+  static_assert(!S_ || (P_ == 0 || P_ == 1), "LDS-DMA rows: plain or nt policy");
 };
-using DefaultFastCfg = FastCfg<kFastWaves, 4, 1, 0>;  // kbench r1: nt loads +17%, ring 4 best
+// kbench: nt loads +17 %, ring 4 best; interleaved block order (block b ->
+// wave b % W, uniform layouts) 0-7 % over contiguous runs, never slower
+// (profiles/r1/glds/)
+using DefaultFastCfg = FastCfg<kFastWaves, 4, 1, 1>;
 
 // Row load, 16 B per lane.  Policy 0: plain global_load_dwordx4; 1: the same
 // with the nontemporal (nt) bit; 2..5: buffer_load_dwordx4 with cache-policy
@@ -148,6 +162,15 @@ __device__ __forceinline__ uint4 load_row(const uint8_t *row, uint32_t lane) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Row load by LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at
+// slot + 16 l; the LDS base is wave-uniform (M0).  Policy 1 sets nt.
+template <int kPolicy>
+__device__ __forceinline__ void dma_row(const uint8_t *row, uint8_t *slot, uint32_t lane) {
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(row + lane * 16u), (lds_void_t *)slot, 16, 0,
+                                   kPolicy ? 2 : 0);
+}
+
 template <bool kUniform, class Cfg>
 __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
@@ -156,13 +179,25 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
   constexpr int kWaves = Cfg::kWaves, kThreads = kWaves * 64, kRing = Cfg::kRing;
   constexpr bool kInterleave = kUniform && Cfg::kOrder == 1;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  constexpr uint32_t kS4R = Cfg::kS4Rep;
+  // tables and the row ring are separate LDS variables: their accesses carry
+  // distinct alias scopes, so hipcc's waitcnt pass does not wait for the
+  // in-flight row DMA before a table lookup
+  __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsMainBytes + Cfg::kS4Bytes) / 4];
+  // kS4R == 0: columns of the 4-byte shift (bit i of byte j -> s4[j][1 << (i % 8)]),
+  // wave-uniform
+  uint32_t s4col[32];
+  if constexpr (kS4R == 0) {
+#pragma unroll
+    for (int i = 0; i < 32; i++) s4col[i] = uni(tables->s4[i >> 3][1u << (i & 7)]);
+  }
+  __shared__ __attribute__((aligned(16))) uint8_t ring_lds[Cfg::kStage ? Cfg::kRingBytes : 16];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
 
   // Fill the replicated tables.  Main region address of (table k, byte v,
   // replica r) = (k>>1)<<16 | v<<8 | (k&1)<<7 | r<<2; s4 region address
-  // = kLdsMainBytes + k*4096 + v*16 + (r&3)*4.
+  // = kLdsMainBytes + (k*256 + v)*4*kS4R + (r%kS4R)*4.
   const uint32_t *tg = &tables->tg[0][0];
   for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kThreads) {
     const uint32_t a = q * 16;
@@ -171,11 +206,7 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
   }
   const uint32_t *s4 = &tables->s4[0][0];
-  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kThreads) {
-    const uint32_t v = s4[q];
-    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
-        make_uint4(v, v, v, v);
-  }
+  for (uint32_t q = tid; q < 1024u * kS4R; q += kThreads) lds[kLdsMainBytes / 4 + q] = s4[q / kS4R];
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
@@ -184,7 +215,7 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 
   const uint32_t r4 = (lane & 31u) << 2;
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
-  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  const uint32_t S4base = kLdsMainBytes + (kS4R ? (lane % (kS4R ? kS4R : 1)) << 2 : 0u);
   const bool msg = (flags & kFlagMessages) != 0;
 
   // c <- shift(c, 1024) ^ w : four conflict-free lookups, one v_perm each.
@@ -197,10 +228,12 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
     return xor3(xor3(t0, t1, t2), t3, w);
   };
   auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
-    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
-    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
-    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
-    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    if constexpr (kS4R == 0) return matvec32(s4col, x) ^ w;
+    constexpr uint32_t E = 4u * kS4R, T = 1024u * kS4R;  // entry, table strides
+    const uint32_t t0 = lds_u32(lds, S4base + (x & 255u) * E);
+    const uint32_t t1 = lds_u32(lds, S4base + T + ((x >> 8) & 255u) * E);
+    const uint32_t t2 = lds_u32(lds, S4base + 2 * T + ((x >> 16) & 255u) * E);
+    const uint32_t t3 = lds_u32(lds, S4base + 3 * T + (x >> 24) * E);
     return xor3(xor3(t0, t1, t2), t3, w);
   };
 
@@ -323,8 +356,15 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
   };
   // The load is unconditional (past the wave's last row it re-reads that row,
   // tagged invalid) so hipcc's wait counting stays exact: vmcnt(kRing-1).
-  auto load_next = [&](Tag &t) -> uint4 {
-    const uint4 v = load_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, lane);
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  uint8_t *const wring = ring_lds + (Cfg::kStage ? wave * (uint32_t)(kRing * kRowBytes) : 0u);
+  auto load_next = [&](Tag &t, int slot) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if constexpr (Cfg::kStage) {
+      dma_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, wring + slot * kRowBytes, lane);
+    } else {
+      v = load_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, lane);
+    }
     t.valid = pvalid;
     t.blk = pb;
     t.ptr = pptr;
@@ -350,7 +390,7 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
   uint4 ring[kRing];
   Tag tag[kRing];
 #pragma unroll
-  for (int u = 0; u < kRing; u++) ring[u] = load_next(tag[u]);
+  for (int u = 0; u < kRing; u++) ring[u] = load_next(tag[u], u);
 
   // ---- consumer --------------------------------------------------------------
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
@@ -361,7 +401,23 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
       // consume slot u, then refill it (same registers: no copies, kRing-1
       // rows stay in flight while this one is hashed)
       const Tag t = tag[u];
-      uint4 v = ring[u];
+      uint4 v;
+      if constexpr (Cfg::kStage) {
+        // slot u's DMA is the oldest of the kRing in flight; the slot read is
+        // inline asm (invisible to hipcc's waitcnt pass, which would wait
+        // vmcnt(0) for the DMA before a visible LDS read); the slot is
+        // refilled as soon as it is in VGPRs, before the row is hashed
+        __builtin_amdgcn_s_waitcnt((kRing - 1) | (7 << 4) | (15 << 8));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 r;
+        const uint32_t la =
+            (uint32_t)(uintptr_t)(lds_void_t *)(wring + u * kRowBytes) + lane * 16u;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(la) : "memory");
+        v = make_uint4(r.x, r.y, r.z, r.w);
+        load_next(tag[u], u);
+      } else {
+        v = ring[u];
+      }
       if (t.row == 0) {
         if (lane == 0) {
           stored = v.x;
@@ -377,7 +433,7 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
         c2 = row_step(c2, v.z);
         c3 = row_step(c3, v.w);
       }
-      ring[u] = load_next(tag[u]);
+      if constexpr (!Cfg::kStage) ring[u] = load_next(tag[u], u);
       if (t.row + 1 == t.rows) {
         uint32_t crc;
         if constexpr (Cfg::kNull) {
@@ -403,7 +459,11 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
         // block, further first_bad atomics cannot lower the minimum (and on a
         // batch of all-bad blocks would serialise every wave on one address)
         if (first_bad && uni(stored) != crc) reported = true;
-        if (!tag[(u + 1) % kRing].valid) return;  // the wave's last block is done
+        if (!tag[(u + 1) % kRing].valid) {  // the wave's last block is done
+          // no LDS-DMA may land after the workgroup's LDS is released
+          if constexpr (Cfg::kStage) __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+          return;
+        }
       }
     }
   }

@@ -81,6 +81,62 @@ Variant fast_variant(const char *name, int grid_mult = 1) {
   return v;
 }
 
+
+// LDS-staged streaming (the north star's "block staged in LDS"), timing-only:
+// each wave streams its contiguous run of 1 KiB rows through a private ring of
+// R LDS slots filled by global_load_lds_dwordx4 (LDS-DMA, no VGPR
+// destination), reads each slot back with ds_read_b128 and XOR-folds it.
+// The slot read is inline asm so hipcc's waitcnt pass does not see an LDS
+// read aliasing the in-flight DMA (it would emit vmcnt(0) before every read);
+// the counted vmcnt(R-1) is explicit.  Rows past the wave's end are clamped
+// to its last row (read again, folded in: timing only).
+typedef __attribute__((address_space(3))) void lds_void_t;
+template <int W, int R, int AUX>
+__global__ __launch_bounds__(W * 64) void k_glds_null(const uint8_t *base, uint64_t nrows, uint32_t *out) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[W * R * 1024];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * W + wave, NW = (uint64_t)gridDim.x * W;
+  const uint64_t r0 = nrows * gw / NW, r1 = nrows * (gw + 1) / NW;
+  uint8_t *myring = ring + wave * (R * 1024);
+  uint32_t acc = 0;
+  if (r0 < r1) {
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+      const uint64_t rr = r0 + u < r1 ? r0 + u : r1 - 1;
+      __builtin_amdgcn_global_load_lds((const void *)(base + rr * 1024 + lane * 16),
+                                       (lds_void_t *)(myring + u * 1024), 16, 0, AUX);
+    }
+    for (uint64_t k = r0; k < r1; k += R) {
+#pragma unroll
+      for (int u = 0; u < R; u++) {
+        __builtin_amdgcn_s_waitcnt((R - 1) | (7 << 4) | (15 << 8));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v;
+        const uint32_t la = (uint32_t)(uintptr_t)(lds_void_t *)(myring + u * 1024) + lane * 16;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(la) : "memory");
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        const uint64_t nr = k + u + R < r1 ? k + u + R : r1 - 1;
+        __builtin_amdgcn_global_load_lds((const void *)(base + nr * 1024 + lane * 16),
+                                         (lds_void_t *)(myring + u * 1024), 16, 0, AUX);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+  }
+  out[(size_t)blockIdx.x * W * 64 + threadIdx.x] = acc;
+}
+
+template <int W, int R, int AUX>
+Variant glds_variant(const char *name, const uint8_t *buf, uint64_t nrows, uint32_t *scratch, int wg_per_cu) {
+  Variant v;
+  v.name = name;
+  v.check = false;
+  v.run = [=](const hc::Batch &, int cus, hipStream_t st) {
+    hipLaunchKernelGGL((k_glds_null<W, R, AUX>), dim3(cus * wg_per_cu), dim3(W * 64), 0, st, buf, nrows, scratch);
+  };
+  return v;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -131,14 +187,24 @@ int main(int argc, char **argv) {
 
   using namespace hc;
   std::vector<Variant> vs;
-  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt (prod)"));
-  vs.push_back(arrays_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt, off/len arrays path", doff, dlen));
-  vs.push_back(fast_variant<FastCfg<16, 3, 1, 0>>("w16 r3 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 5, 1, 0>>("w16 r5 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1>>("w16 r4 nt inter"));
-  vs.push_back(fast_variant<FastCfg<16, 4, 4, 0>>("w16 r4 buf sc1|nt"));
-  vs.push_back(fast_variant<FastCfg<12, 4, 1, 0>>("w12 r4 nt"));
-  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0, true>>("NULL w16 r4 nt"));
+  // production first (the reference output), then the orders A/B/A/B
+  vs.push_back(fast_variant<DefaultFastCfg>("w16 r4 nt (prod)"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt contiguous"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1>>("w16 r4 nt interleaved"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt contiguous (again)"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1>>("w16 r4 nt interleaved (again)"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 0, true>>("NULL w16 r4 nt contiguous"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1, true>>("NULL w16 r4 nt interleaved"));
+  // LDS-staged rows (LDS-DMA ring; tables leave room for 24 KiB of ring)
+  vs.push_back(fast_variant<FastCfg<12, 2, 1, 0, false, true, 2>>("LDS-DMA w12 r2 nt s4x2"));
+  vs.push_back(fast_variant<FastCfg<12, 2, 1, 1, false, true, 2>>("LDS-DMA w12 r2 nt s4x2 interleaved"));
+  vs.push_back(fast_variant<FastCfg<16, 2, 1, 1, false, true, 0>>("LDS-DMA w16 r2 nt s4 VALU interleaved"));
+  vs.push_back(fast_variant<FastCfg<16, 2, 1, 0, false, true, 0>>("LDS-DMA w16 r2 nt s4 VALU contiguous"));
+  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1, false, false, 0>>("w16 r4 nt s4 VALU interleaved"));
+  vs.push_back(fast_variant<FastCfg<16, 2, 1, 1, true, true, 0>>("NULL LDS-DMA w16 r2 nt interleaved"));
+  vs.push_back(fast_variant<FastCfg<8, 3, 1, 0, true, true, 2>>("NULL LDS-DMA w8 r3 nt"));
+  const uint64_t nrows = N * B / 1024;
+  vs.push_back(glds_variant<8, 3, 2>("NULL glds LDS-staged w8 r3 nt", buf, nrows, scratch, 1));
   for (int pol = 0; pol < 2; pol++) {
     Variant v;
     v.name = pol ? "REF grid-stride read nt, 8x256/CU" : "REF grid-stride read, 8x256/CU";
