@@ -21,6 +21,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -74,7 +75,8 @@ def pmc_traffic(args):
     if not exe:
         return None, "rocprofv3 not found"
     out = {}
-    kern = {"frame": "k_frame", "unframe": "k_unframe"}.get(WORKLOADS[args.workload][1], "k_crc_fast")
+    # the streaming kernel: k_crc_uni (uniform 4/8/16 KiB blocks) or k_crc_fast
+    kern = {"frame": "k_frame", "unframe": "k_unframe"}.get(WORKLOADS[args.workload][1], "k_crc_(uni|fast)")
     tmp = tempfile.mkdtemp(prefix="hc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
              "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off"]
@@ -96,7 +98,7 @@ def pmc_traffic(args):
         for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if kern in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    if re.search(kern, row.get("Kernel_Name", "")) and row.get("Counter_Name") == ctr:
                         vals.append(float(row["Counter_Value"]))
         if not vals:
             return None, f"no {ctr} rows"

@@ -146,7 +146,11 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
   if (!off && !len) {
     const bool fast = ulen >= 1024 && (ulen & 1023u) == 0 &&
                       (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (stride & 15u) == 0;
-    if (fast) {
+    if (fast && (ulen & 4095u) == 0) {  // 4/8/16 KiB blocks: groups of 4 rows
+      e = launch_uni(b, fast_grid, s);
+      info.kernel = "k_crc_uni";
+      info.fast_blocks = n;
+    } else if (fast) {
       e = launch_fast(b, true, fast_grid, s);
       info.fast_blocks = n;
     } else {

@@ -40,6 +40,8 @@ constexpr uint32_t kFastLdsBytes = kLdsMainBytes + kLdsS4Bytes;
 // uniform_fast: the host proved every block satisfies the streaming kernel's
 // layout contract (16-B aligned start, length a positive multiple of 1024).
 hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s);
+// uniform batch, 16-B aligned base/stride, ulen a positive multiple of 4096
+hipError_t launch_uni(const Batch &b, int grid, hipStream_t s);
 // only_nonfast: process only blocks the streaming kernel skips.
 hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s);
 // Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B blocks.

@@ -43,7 +43,7 @@ def test_zero_payload_known_answers(cuda, hc, golden):
         buf = torch.zeros(1000 * B, dtype=torch.uint8, device="cuda")
         got = dev_crc(torch, hc, buf, 1000, stride=B, ulen=B)
         assert (got == want).all(), B
-        assert hc.last_launch()["kernel"] == "k_crc_fast"
+        assert hc.last_launch()["kernel"] == "k_crc_uni"
 
 
 def test_config1_golden(cuda, hc, golden):
@@ -122,6 +122,51 @@ def test_general_lengths_and_alignment(cuda, hc, oracle):
     want = oracle.crc32_blocks(host, off=off, lens=lens, threads=16)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (bad[:10], lens[bad[:10]], off[bad[:10]] % 16)
+
+
+@pytest.mark.parametrize("size,gap", [(1024, 0), (3072, 16), (5120, 0), (4096, 0), (4096, 16),
+                                      (12288, 0), (20480, 48)])
+def test_uniform_kernel_routes(cuda, hc, oracle, size, gap):
+    """Uniform aligned batches: lengths that are multiples of 4 KiB take
+    k_crc_uni (groups of 4 rows), other multiples of 1 KiB k_crc_fast; both
+    bit-exact in block mode (CRC, stamp, verify with corruption) and in
+    whole-message mode, including batches smaller than one block per wave."""
+    torch = cuda
+    stride = size + gap
+    want_kernel = "k_crc_uni" if size % 4096 == 0 else "k_crc_fast"
+    for n in (1, 7, 4095, 40_000):
+        host = np.random.default_rng(size * 7 + n).integers(0, 256, n * stride, dtype=np.uint8)
+        buf = torch.from_numpy(host).cuda()
+        got = dev_crc(torch, hc, buf, n, stride=stride, ulen=size)
+        assert hc.last_launch()["kernel"] == want_kernel
+        want = oracle.crc32_blocks(host, stride=stride, ulen=size, nblocks=n, threads=16)
+        assert (got == want).all(), (size, gap, n)
+        off = np.arange(n, dtype=np.uint64) * stride
+        lens = np.full(n, size, dtype=np.uint32)
+        got = dev_crc(torch, hc, buf, n, stride=stride, ulen=size, flags=hc.HC_F_MESSAGES)
+        assert hc.last_launch()["kernel"] == want_kernel
+        assert (got == oracle.crc32_messages(host, off, lens, threads=16)).all(), (size, gap, n)
+    # stamp in place, verify clean, corrupt, verify again (last n = 40000)
+    hc.dev_crc32_blocks(buf, None, stride=stride, ulen=size, nblocks=n, flags=hc.HC_F_STAMP)
+    stamped = buf.cpu().numpy()
+    words = np.stack([stamped[i * stride:i * stride + 4] for i in range(n)]).copy().view("<u4").reshape(-1)
+    assert (words == want).all()
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(buf, None, stride=stride, ulen=size, nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == 2**63 - 1 and int(bm.abs().sum().item()) == 0
+    rng = np.random.default_rng(size + gap)
+    victims = np.sort(rng.choice(n, 97, replace=False))
+    pos = victims.astype(np.int64) * stride + rng.integers(0, size, victims.size)
+    buf[torch.from_numpy(pos).cuda()] ^= 0x10
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(buf, None, stride=stride, ulen=size, nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == int(victims[0])
+    bits = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    assert np.array_equal(np.nonzero(bits)[0], victims)
 
 
 def test_uniform_nonconforming_goes_general(cuda, hc, oracle):
@@ -618,7 +663,7 @@ def test_config4_full_size_sampled_and_sharded(cuda, hc, oracle):
     hc.dev_fill_blocks(buf, seed, stride=B, ulen=B, nblocks=n)
     whole = torch.empty(n, dtype=torch.int32, device="cuda")
     hc.dev_crc32_blocks(buf, whole, stride=B, ulen=B, nblocks=n)
-    assert hc.last_launch()["kernel"] == "k_crc_fast"
+    assert hc.last_launch()["kernel"] == "k_crc_uni"
     parts = torch.empty(n, dtype=torch.int32, device="cuda")
     for r in range(8):
         lo, hi = shard.index_range(n, 8, r)

@@ -137,6 +137,18 @@ Variant glds_variant(const char *name, const uint8_t *buf, uint64_t nrows, uint3
   return v;
 }
 
+template <int kW, bool kNullV = false>
+Variant uni_variant(const char *name) {
+  Variant v;
+  v.name = name;
+  v.check = !kNullV;
+  v.run = [](const hc::Batch &b, int cus, hipStream_t s) {
+    hipLaunchKernelGGL((hc::k_crc_uni<kW, kNullV>), dim3(cus), dim3(kW * 64), 0, s, b.base, b.stride, b.ulen,
+                       b.flags, b.nblocks, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+  };
+  return v;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -190,17 +202,17 @@ int main(int argc, char **argv) {
   // production first (the reference output), then the orders A/B/A/B
   vs.push_back(fast_variant<DefaultFastCfg>("w16 r4 nt (prod)"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt contiguous"));
+  vs.push_back(uni_variant<16>("k_crc_uni w16"));
+  vs.push_back(uni_variant<16, true>("NULL k_crc_uni w16"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 1>>("w16 r4 nt interleaved"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 0>>("w16 r4 nt contiguous (again)"));
+  vs.push_back(uni_variant<16>("k_crc_uni w16 (again)"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 1>>("w16 r4 nt interleaved (again)"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 0, true>>("NULL w16 r4 nt contiguous"));
   vs.push_back(fast_variant<FastCfg<16, 4, 1, 1, true>>("NULL w16 r4 nt interleaved"));
   // LDS-staged rows (LDS-DMA ring; tables leave room for 24 KiB of ring)
   vs.push_back(fast_variant<FastCfg<12, 2, 1, 0, false, true, 2>>("LDS-DMA w12 r2 nt s4x2"));
-  vs.push_back(fast_variant<FastCfg<12, 2, 1, 1, false, true, 2>>("LDS-DMA w12 r2 nt s4x2 interleaved"));
   vs.push_back(fast_variant<FastCfg<16, 2, 1, 1, false, true, 0>>("LDS-DMA w16 r2 nt s4 VALU interleaved"));
-  vs.push_back(fast_variant<FastCfg<16, 2, 1, 0, false, true, 0>>("LDS-DMA w16 r2 nt s4 VALU contiguous"));
-  vs.push_back(fast_variant<FastCfg<16, 4, 1, 1, false, false, 0>>("w16 r4 nt s4 VALU interleaved"));
   vs.push_back(fast_variant<FastCfg<16, 2, 1, 1, true, true, 0>>("NULL LDS-DMA w16 r2 nt interleaved"));
   vs.push_back(fast_variant<FastCfg<8, 3, 1, 0, true, true, 2>>("NULL LDS-DMA w8 r3 nt"));
   const uint64_t nrows = N * B / 1024;
