@@ -110,6 +110,7 @@ def _lib():
             "hc_dev_crc32_blocks": (I, [I, P, P, P, U64, U32, U64, P, P, P, U32, P]),
             "hc_dev_verify_prepare": (I, [I, P, P, U64, P]),
             "hc_dev_fill_blocks": (I, [I, P, P, P, U64, U32, U64, U64, P]),
+            "hc_dev_fill_range": (I, [I, P, P, P, U64, U32, U64, U64, U64, P]),
             "hc_dev_add_crcs": (I, [I, P, U64, P, P, P]),
             "hc_read_from_disk": (I, [P, U64, U32, U64, U64, P, P, P]),
             "hc_dev_read_blocks": (I, [I, P, U64, U32, P, P, P, P, P]),
@@ -117,6 +118,7 @@ def _lib():
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_device_count": (I, []),
+            "hc_host_pipelines": (I, []),
             "hc_md5": (None, [P, S, P]),
             "hc_md5_messages": (I, [P, P, P, U64, P]),
             "hc_dev_md5_messages": (I, [I, P, P, P, U64, U32, U64, P, P, P]),
@@ -395,6 +397,17 @@ def dev_fill_blocks(buf, seed, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOC
         raise HundCRCError(rc, "dev_fill_blocks")
 
 
+def dev_fill_range(buf, seed, first_block, nblocks, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE,
+                   stream=None):
+    """Fill a rank's shard: buffer block i = global block first_block + i of the
+    seeded synthetic batch (hc_dev_fill_range)."""
+    dev = buf.device.index if buf.device.index is not None else 0
+    rc = _lib().hc_dev_fill_range(dev, buf.data_ptr(), _tptr(off), _tptr(lens), stride, ulen, int(first_block),
+                                  int(nblocks), seed & ((1 << 64) - 1), _stream_ptr(stream))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_fill_range")
+
+
 def dev_add_crcs(src, dst=None, crc_out=None, n=None, stream=None):
     """Fused AddCRCsToData (crc_util.go:41-64) on device tensors: frame the first
     `n` bytes of uint8 `src` (default: all) into stamped 4096-byte blocks at `dst`
@@ -446,6 +459,11 @@ def last_launch() -> dict:
 
 def device_count() -> int:
     return int(_lib().hc_device_count())
+
+
+def host_pipelines() -> int:
+    """Host-batch pipelines alive in this process (bounded by HC_MAX_PIPES)."""
+    return int(_lib().hc_host_pipelines())
 
 
 def debug_tables() -> np.ndarray:

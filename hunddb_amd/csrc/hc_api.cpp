@@ -9,6 +9,8 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -146,22 +148,24 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
   if (!off && !len) {
     const bool fast = ulen >= 1024 && (ulen & 1023u) == 0 &&
                       (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (stride & 15u) == 0;
-    if (fast && (ulen & 4095u) == 0) {  // 4/8/16 KiB blocks: groups of 4 rows
-      e = launch_uni(b, fast_grid, s);
-      info.kernel = "k_crc_uni";
+    if (fast && (ulen & 4095u) == 0) {  // 4/8/16 KiB blocks: groups of 4 rows, handed out per CU
+      e = launch_grp(b, fast_grid, s);
+      info.kernel = "k_crc_grp";
       info.fast_blocks = n;
     } else if (fast) {
       e = launch_fast(b, true, fast_grid, s);
       info.fast_blocks = n;
     } else {
-      e = launch_general(b, false, gen_grid, s);
+      e = launch_general(b, 0, gen_grid, s);
       info.kernel = "k_crc_any";
       info.general_blocks = n;
     }
   } else {
-    e = launch_fast(b, false, fast_grid, s);
-    if (e == hipSuccess) e = launch_general(b, true, gen_grid, s);
-    info.kernel = "k_crc_fast+k_crc_any";
+    // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk
+    // size, utils/config/config.go:137); the k_crc_any sweep does the rest
+    e = launch_grp(b, fast_grid, s);
+    if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
+    info.kernel = "k_crc_grp+k_crc_any";
     info.fast_blocks = n;  // routing is decided on the device per block
   }
   t_last = info;
@@ -258,7 +262,65 @@ struct HostPipe {
   ~HostPipe() { release(); }
 };
 
-thread_local HostPipe t_pipe;
+// Process-wide pool of pipelines, at most HC_MAX_PIPES (default 4) alive: a
+// host batch leases one for the duration of the call and returns it.  cgo runs
+// calls on arbitrary, long-lived OS threads, so per-thread pipelines (each
+// ~240 MiB pinned + ~1 GiB of device buffers) would grow with the thread
+// count; here extra concurrent callers wait for a free pipeline instead.
+// Pipelines are never destroyed (the pool outlives every caller; process exit
+// releases the memory), so no HIP call runs during static destruction.
+class PipePool {
+ public:
+  static PipePool &get() {
+    static PipePool *p = new PipePool;
+    return *p;
+  }
+  HostPipe *acquire(int dev) {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      for (size_t k = 0; k < idle_.size(); k++)  // an idle pipeline already on this device
+        if (idle_[k]->ok && idle_[k]->dev == dev) return take(k);
+      if (live_ < cap_) {
+        live_++;
+        return new HostPipe;
+      }
+      if (!idle_.empty()) return take(0);  // re-initialised on `dev` by the caller
+      cv_.wait(lk);
+    }
+  }
+  void release(HostPipe *p) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      idle_.push_back(p);
+    }
+    cv_.notify_one();
+  }
+  int live() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return live_;
+  }
+
+ private:
+  PipePool() : cap_(std::max(1, env_int("HC_MAX_PIPES", 4))) {}
+  HostPipe *take(size_t k) {
+    HostPipe *p = idle_[k];
+    idle_.erase(idle_.begin() + (long)k);
+    return p;
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<HostPipe *> idle_;
+  int live_ = 0;
+  const int cap_;
+};
+
+struct PipeLease {  // RAII: one pipeline for one host batch
+  HostPipe *p;
+  explicit PipeLease(int dev) : p(PipePool::get().acquire(dev)) {}
+  ~PipeLease() { PipePool::get().release(p); }
+  PipeLease(const PipeLease &) = delete;
+  PipeLease &operator=(const PipeLease &) = delete;
+};
 
 inline uint64_t blk_off(const uint64_t *off, uint64_t stride, uint64_t i) { return off ? off[i] : i * stride; }
 inline uint32_t blk_len(const uint32_t *len, uint32_t ulen, uint64_t i) { return len ? len[i] : ulen; }
@@ -285,7 +347,8 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
   const int dev = default_device();
   int st = init_device(dev);
   if (st != HC_OK) return st;
-  HostPipe &P = t_pipe;
+  PipeLease lease(dev);
+  HostPipe &P = *lease.p;
   if ((st = P.init(dev)) != HC_OK) return st;
   DeviceGuard g(dev);
   const bool md5 = md5_out != nullptr;
@@ -355,13 +418,14 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     uint8_t *dsrc = s.dbuf;  // the chunk's device copy
     uint32_t l0 = blk_len(len, ulen, i);
     if (direct) {
-      j = std::min<uint64_t>(n, i + std::max<uint64_t>(1, P.chunk / ulen));
+      if (ulen > P.chunk) {  // a block larger than a staging slot: on its own
+        if ((rc = oversize(s, i)) != HC_OK) break;
+        i++;
+        continue;
+      }
+      j = std::min<uint64_t>(n, i + P.chunk / ulen);
       j = std::min<uint64_t>(j, i + maxmsg);
       pos = (j - i) * (uint64_t)ulen;
-      if (pos > P.chunk) {
-        rc = HC_E_ARG;
-        break;
-      }
       if (hipMemcpyAsync(s.dbuf, base + i * stride, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
         rc = HC_E_HIP;
         break;
@@ -429,7 +493,9 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
       const int th = (int)std::min<uint64_t>((uint64_t)copy_threads, std::max<uint64_t>(1, pos >> 22));
       parallel_for(th, [&](int t) {
         const uint64_t a = nb * t / th, b = nb * (t + 1) / th;
-        if (!off && !len && stride == ulen) {  // contiguous source: one memcpy per thread
+        // contiguous source AND contiguous staging (pin_off[k] = k*ulen only when
+        // ulen is a 16-B multiple): one memcpy per thread
+        if (!off && !len && stride == ulen && (ulen & 15u) == 0) {
           if (b > a) std::memcpy(s.pin + s.pin_off[a], base + (i + a) * stride, (b - a) * (uint64_t)ulen);
         } else {
           for (uint64_t k = a; k < b; k++)
@@ -526,10 +592,17 @@ int hc_device_count(void) {
 // ---- drop-ins ---------------------------------------------------------------
 uint32_t hc_crc32_ieee(const uint8_t *p, size_t n) {
   if (n == 0) return 0;
-  if (force_gpu()) {
+  if (force_gpu() && n <= 0xFFFFFFFFu) {
+    // HC_FORCE_GPU is a test mode: a broken GPU path must not pass on the CPU.
+    // GetCRC has no error channel (crc_util.go:15), so report and abort.
     uint64_t o = 0;
     uint32_t l = (uint32_t)n, c = 0;
-    if (n <= 0xFFFFFFFFu && host_batch(p, &o, &l, 0, 0, 1, &c, kFlagMessages) == HC_OK) return c;
+    const int rc = host_batch(p, &o, &l, 0, 0, 1, &c, kFlagMessages);
+    if (rc != HC_OK) {
+      std::fprintf(stderr, "hundcrc: HC_FORCE_GPU GetCRC failed: %s\n", hc_strerror(rc));
+      std::abort();
+    }
+    return c;
   }
   return hc::cpu_crc32_update(0, p, n);
 }
@@ -564,14 +637,24 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
     std::memcpy(blk + HC_CRC_SIZE, src + s, e - s);
     if (e - s < kPayloadPerBlock) std::memset(blk + HC_CRC_SIZE + (e - s), 0, kPayloadPerBlock - (e - s));
   }
-  // CRCs: one GPU batch for multi-block outputs, host for a single block
+  // CRCs: one GPU batch for multi-block outputs, host for a single block.
+  // AddCRCsToData cannot fail in Go (crc_util.go:41-64), so a host with no
+  // gfx950 (HC_E_NODEV) computes the CRCs on the host path below (hc_cpu.cpp,
+  // product code) instead of failing; any other GPU error is returned, and
+  // HC_FORCE_GPU (test mode) never takes the host path.
   static const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", 256);
+  bool on_gpu = false;
   if (nb >= gpu_min || (force_gpu() && nb > 0)) {
     std::vector<uint32_t> crc(nb);
     int rc = host_batch(dst, nullptr, nullptr, HC_BLOCK_SIZE, HC_BLOCK_SIZE, nb, crc.data(), 0);
-    if (rc != HC_OK) return (size_t)-1;
-    for (size_t b = 0; b < nb; b++) std::memcpy(dst + b * HC_BLOCK_SIZE, &crc[b], 4);
-  } else {
+    if (rc == HC_OK) {
+      for (size_t b = 0; b < nb; b++) std::memcpy(dst + b * HC_BLOCK_SIZE, &crc[b], 4);
+      on_gpu = true;
+    } else if (rc != HC_E_NODEV || force_gpu()) {
+      return (size_t)-1;
+    }
+  }
+  if (!on_gpu) {
     for (size_t b = 0; b < nb; b++) {
       uint8_t *blk = dst + b * HC_BLOCK_SIZE;
       const uint32_t c = hc::cpu_crc32_update(0, blk + HC_CRC_SIZE, kPayloadPerBlock);
@@ -814,8 +897,8 @@ int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad, 
              : HC_E_HIP;
 }
 
-int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32_t *len,
-                       uint64_t stride, uint32_t ulen, uint64_t nblocks, uint64_t seed, void *stream) {
+int hc_dev_fill_range(int device, void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                      uint32_t ulen, uint64_t first_block, uint64_t nblocks, uint64_t seed, void *stream) {
   if (nblocks == 0) return HC_OK;
   if (!base) return HC_E_ARG;
   int st = init_device(device);
@@ -823,10 +906,17 @@ int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32
   DeviceGuard g(device);
   int grid = (int)std::min<uint64_t>((nblocks + 3) / 4, (uint64_t)g_dev[device].cus * 16);
   return launch_fill(static_cast<uint8_t *>(base), off, len, stride, ulen, nblocks, seed, grid,
-                     static_cast<hipStream_t>(stream)) == hipSuccess
+                     static_cast<hipStream_t>(stream), first_block) == hipSuccess
              ? HC_OK
              : HC_E_HIP;
 }
+
+int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32_t *len,
+                       uint64_t stride, uint32_t ulen, uint64_t nblocks, uint64_t seed, void *stream) {
+  return hc_dev_fill_range(device, base, off, len, stride, ulen, 0, nblocks, seed, stream);
+}
+
+int hc_host_pipelines(void) { return PipePool::get().live(); }
 
 int hc_last_launch(hc_launch_info *info) {
   if (!info) return HC_E_ARG;

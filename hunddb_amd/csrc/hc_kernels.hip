@@ -604,6 +604,251 @@ __global__ __launch_bounds__(kWaves * 64) void k_crc_uni(const uint8_t *base, ui
 }
 
 // ---------------------------------------------------------------------------
+// k_crc_grp: the streaming kernel for blocks of 4 KiB multiples with the
+// k_crc_uni group structure, for uniform batches and off/len batches alike,
+// with the blocks dealt to waves by a per-workgroup hand-out.
+//   * Workgroup g owns the chunks of C = 2^lg_chunk consecutive blocks
+//     c*G + g (G = grid): all workgroups sweep memory together, and the CRC
+//     words / bitmap bits of one chunk are written by one CU (one XCD's L2:
+//     a 128-B line of crc_out is 32 blocks).
+//   * Inside the workgroup the blocks are handed out one at a time by an LDS
+//     counter (ds_add_rtn, lane 0, once per block, its value used one block
+//     later).  Mixed 4/8/16 KiB batches (configs[2]) then keep every wave of a
+//     CU busy to the end; a static deal leaves per-wave byte totals ~3 % apart
+//     (sd), and the slowest wave sets the kernel time.
+//   * off/len metadata of the block after next is read by a buffer load issued
+//     before each iteration's first row refill, so it is complete by the time
+//     the next refill's row has been waited for (in-order vmcnt): no wait of
+//     its own, no scalar load in flight across the LDS lookups.  It is issued
+//     every iteration (the same entry again between block ends) so no VMEM
+//     instruction sits behind a branch.
+//   * A block that is not 16-B aligned or whose length is not a positive
+//     multiple of 4096 costs one group of dummy rows (re-reads of the current
+//     group, never stored) and is left to k_crc_any (fast_mask 4095).
+template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false>
+__global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ lens, uint64_t stride,
+                                                         uint32_t ulen, uint32_t flags, uint64_t nblocks,
+                                                         uint32_t lg_chunk, uint32_t rot,
+                                                         uint32_t *__restrict__ crc_out,
+                                                         uint32_t *__restrict__ bad_bitmap,
+                                                         unsigned long long *__restrict__ first_bad,
+                                                         const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) = make_uint4(v, v, v, v);
+  }
+  if (tid == 0) s_next = 3 * kFastWaves;  // indices 0 .. 3W-1 are dealt statically below
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+
+  const uint32_t r4 = (lane & 31u) << 2;
+  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
+  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (kNull) return c ^ w;
+    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
+    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
+    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
+    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
+    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
+    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
+    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+
+  const uint32_t wave = uni(tid >> 6);
+  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint32_t cmask = (1u << lg_chunk) - 1u;
+  // k-th block of this workgroup's sequence; rot staggers where each
+  // workgroup enters its chunks (rot = 0: in order)
+  const uint32_t rotw = (uint32_t)wg * rot;
+  auto blk_of = [&](uint32_t k) -> uint64_t {
+    return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | ((k + rotw) & cmask);
+  };
+  const bool msg = (flags & kFlagMessages) != 0;
+
+  // metadata -> (group pointer, group count, skip)
+  struct Blk {
+    uint64_t i;
+    const uint8_t *p;
+    uint32_t groups;
+    bool valid, skip;
+  };
+  auto make_blk = [&](uint64_t i, uint64_t o, uint32_t l) {
+    Blk r;
+    r.i = i;
+    r.valid = i < nblocks;
+    r.p = base + o;
+    r.groups = l >> 12;
+    r.skip = kArrays && (((((uintptr_t)base + o) & 15u) != 0) || (l & 4095u) != 0 || l == 0);
+    return r;
+  };
+  auto meta_sync = [&](uint64_t i) {  // prologue only
+    if constexpr (!kArrays) return make_blk(i, i * stride, ulen);
+    const uint64_t ic = i < nblocks ? i : 0;
+    return make_blk(i, offs[ic], lens[ic]);
+  };
+  // the block after next: its metadata as a buffer load (vmcnt-ordered)
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 m_o = {0, 0};
+  uint32_t m_l = 0;
+  auto meta_issue = [&](uint64_t i) {
+    if constexpr (kArrays) {
+      const uint64_t ic = i < nblocks ? i : 0;  // (wave-uniform) descriptors based at the entry
+      const __amdgpu_buffer_rsrc_t ro =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(offs + ic), 0, 8, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rl =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(lens + ic), 0, 4, 0x00020000);
+      m_o = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(ro, 0, 0, 0));
+      m_l = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, 0, 0, 0);
+    }
+  };
+
+  uint32_t k0 = wave, k1 = kFastWaves + wave, k2 = 2 * kFastWaves + wave;
+  const uint64_t i0 = blk_of(k0);
+  if (i0 >= nblocks) return;
+  Blk cur = meta_sync(i0);
+  Blk n1 = meta_sync(blk_of(k1));
+  uint64_t i2 = blk_of(k2);
+  uint32_t k3v = 0;                        // VGPR: the LDS hand-out result, read one block end later
+  uint32_t kstat = 3 * kFastWaves + wave;  // static deal (kDyn = false: timing comparison only)
+  meta_issue(i2);
+  // the group the row registers hold; a skipped first block reads 4 KiB of the
+  // constant image instead (always mapped, never consumed)
+  const uint8_t *gp = cur.skip ? reinterpret_cast<const uint8_t *>(tables) : cur.p;
+  static_assert(sizeof(DeviceTables) >= 4096, "dummy group reads 4 KiB of the table image");
+  uint32_t g = 0, gc = cur.skip ? 1u : cur.groups;
+  uint4 q0 = load_row<1>(gp, lane), q1 = load_row<1>(gp + 1024, lane), q2 = load_row<1>(gp + 2048, lane),
+        q3 = load_row<1>(gp + 3072, lane);
+  if constexpr (kDyn) {
+    if (lane == 0) k3v = atomicAdd(&s_next, 1u);
+  }
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
+  uint64_t reported = ~0ull;  // wave-uniform: lowest block this wave has put into first_bad
+  for (;;) {
+    const bool last = g + 1 == gc;
+    // refills: this block's next group, or the next block's first group (a
+    // skipped or missing next block: this group again, never consumed)
+    const uint8_t *np = !last ? gp + 4096 : ((n1.valid && !n1.skip) ? n1.p : gp);
+    if (g == 0) {
+      uint4 v = q0;
+      if (lane == 0) {
+        stored = v.x;
+        v.x = msg ? (v.x ^ 0xFFFFFFFFu) : w0;
+      }
+      c0 = v.x;
+      c1 = v.y;
+      c2 = v.z;
+      c3 = v.w;
+    } else {
+      c0 = row_step(c0, q0.x);
+      c1 = row_step(c1, q0.y);
+      c2 = row_step(c2, q0.z);
+      c3 = row_step(c3, q0.w);
+    }
+    // consumer's next block (the rows the refills below fetch)
+    const Blk nxt = n1;
+    if (last) {
+      // n1 <- n2 (its metadata arrived with the row just waited for), n2 <- hand-out
+      if constexpr (kArrays) {
+        const uint64_t o = ((uint64_t)uni(m_o.y) << 32) | (uint64_t)uni(m_o.x);
+        n1 = make_blk(i2, o, uni(m_l));
+      } else {
+        n1 = make_blk(i2, i2 * stride, ulen);
+      }
+      uint32_t k3;
+      if constexpr (kDyn) {
+        k3 = uni(k3v);
+        if (lane == 0) k3v = atomicAdd(&s_next, 1u);
+      } else {
+        k3 = kstat;
+        kstat += kFastWaves;
+      }
+      i2 = blk_of(k3);
+    }
+    // kPin: keep each refill right after its row's hash (hipcc otherwise pairs
+    // them, two rows late)
+    auto pin = [&] {
+      if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
+    };
+    meta_issue(i2);
+    q0 = load_row<1>(np, lane);
+    pin();
+    c0 = row_step(c0, q1.x);
+    c1 = row_step(c1, q1.y);
+    c2 = row_step(c2, q1.z);
+    c3 = row_step(c3, q1.w);
+    pin();
+    q1 = load_row<1>(np + 1024, lane);
+    pin();
+    c0 = row_step(c0, q2.x);
+    c1 = row_step(c1, q2.y);
+    c2 = row_step(c2, q2.z);
+    c3 = row_step(c3, q2.w);
+    pin();
+    q2 = load_row<1>(np + 2048, lane);
+    pin();
+    c0 = row_step(c0, q3.x);
+    c1 = row_step(c1, q3.y);
+    c2 = row_step(c2, q3.z);
+    c3 = row_step(c3, q3.w);
+    pin();
+    q3 = load_row<1>(np + 3072, lane);
+    pin();
+    if (last) {  // block cur is complete
+      if (!cur.skip) {
+        uint32_t crc;
+        if constexpr (kNull) {
+          crc = wave_xor(c0 ^ c1 ^ c2 ^ c3);
+        } else {
+          const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
+          crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        }
+        const uint64_t b = cur.i;
+        if (crc_out) lane0_store_u32(crc_out + b, crc);
+        if (flags & kFlagStamp) lane0_store_u32(const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(cur.p)), crc);
+        const bool bad = uni(stored) != crc;
+        if (first_bad && bad) {
+          if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+          // one atomic per wave in practice: a wave's later bad blocks can only
+          // lower first_bad when they come before its earlier ones (rotated chunks)
+          if (b < reported) lane0_atomic_umin64(first_bad, b);
+          reported = b < reported ? b : reported;
+        }
+      }
+      if (!nxt.valid) return;
+      cur = nxt;
+      g = 0;
+      gc = cur.skip ? 1u : cur.groups;
+      gp = np;
+    } else {
+      g++;
+      gp = np;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // General kernel (k_crc_any): any alignment, any length (incl. < 4 bytes),
 // block or whole-message mode.  One wave per block, 16 waves per CU, the same
 // replicated LDS tables and per-lane Horner streams as the streaming kernel.
@@ -666,11 +911,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_range(const void *p, uint3
 template <int kBatch, int kVar = 0>
 __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
-    uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, int only_nonfast,
+    uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = uni(tid >> 6);
+  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
+  const uint64_t b0 = uni64(nblocks * gw / W), b1 = uni64(nblocks * (gw + 1) / W);
+  // fast_mask != 0 (the sweep after a streaming kernel): look for work before
+  // the 144 KiB table fill -- a batch the streaming kernel fully covered costs
+  // one metadata read per block and no fill (kbench2: 10 us -> a few)
+  if (fast_mask) {
+    bool any = false;
+    for (uint64_t g0 = b0; g0 < b1 && !any; g0 += 64) {
+      const uint64_t j = g0 + lane;
+      const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
+      const uint32_t lj = j < b1 ? (lens ? lens[j] : ulen) : 0;
+      const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & fast_mask) == 0 && lj != 0;
+      any = __ballot(j < b1 && !fast) != 0;
+    }
+    if (!__syncthreads_or(any)) return;
+  }
   const uint32_t *tg = &tables->tg[0][0];
   for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
     const uint32_t a = q * 16;
@@ -708,11 +971,6 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
     return xor3(xor3(t0, t1, t2), t3, w);
   };
-
-  const uint32_t wave = uni(tid >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
-  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
-  const uint64_t b0 = uni64(nblocks * gw / W), b1 = uni64(nblocks * (gw + 1) / W);
 
   // ---- message cursor ------------------------------------------------------
   // The metadata of 64 messages g .. g+63 sits one per lane (one coalesced
@@ -761,8 +1019,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       wo_hi = (uint32_t)(oj >> 32);
       wl = lj;
       asm volatile("" : "+v"(wo_lo), "+v"(wo_hi), "+v"(wl));
-      const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & 1023u) == 0 && lj != 0;
-      todo = __ballot(j < b1 && !(only_nonfast && fast));
+      // fast_mask != 0: the streaming kernel of this batch took the 16-B aligned
+      // blocks whose length is a positive multiple of fast_mask + 1
+      const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & fast_mask) == 0 && lj != 0;
+      todo = __ballot(j < b1 && !(fast_mask && fast));
     }
   };
 
@@ -930,16 +1190,18 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 // stored with one coalesced 16-B store per lane and hashed exactly like a
 // block of the streaming kernel (W0 in place of bytes 0..3).  Lane 0 keeps
 // its row-0 chunk and stores it last, with the CRC in bytes 0..3.
-// kInter: interior block i goes to wave (i-1) % W (neighbouring waves frame
-// neighbouring blocks); otherwise each wave owns a contiguous run.  tools/kcopy
-// measured the interleaved read+write pattern 2-3 % faster.
-template <bool kInter>
+// Interior blocks are handed out like k_crc_grp's: workgroup g owns the chunks
+// of 2^lg_chunk consecutive blocks c*G + g and its waves take them one at a
+// time from an LDS counter (tools/kcopy2: a persistent read+write stream went
+// from 5.0-5.5 TB/s with static deals to 5.9 TB/s this way).
 __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
-                                                         uint8_t *__restrict__ dst, uint64_t nblk,
+                                                         uint8_t *__restrict__ dst, uint64_t nblk, uint32_t lg_chunk,
                                                          uint32_t *__restrict__ crc_out,
                                                          const DeviceTables *__restrict__ tables) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) s_next = 2 * kFastWaves;
   const uint32_t *tg = &tables->tg[0][0];
   for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
     const uint32_t a = q * 16;
@@ -981,7 +1243,6 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
   const uint32_t wave = uni(tid >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
   const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
-  const uint64_t b0 = uni64(nblk * gw / W), b1 = uni64(nblk * (gw + 1) / W);
 
   // CRC of one framed block from its 4 rows (lane 0's row-0 word 0 = W0) and the
   // store of lane 0's first 16 bytes with the CRC in front.
@@ -1041,30 +1302,33 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
     finish(b, c, keep);
   };
 
-  if (kInter ? gw == 0 : (b0 == 0 && b1 > 0)) edge_block(0);
-  if (nblk > 1 && (kInter ? gw == W - 1 : (b0 < nblk && b1 == nblk))) edge_block(nblk - 1);
+  if (gw == 0) edge_block(0);
+  if (nblk > 1 && gw == (W > 1 ? 1 : 0)) edge_block(nblk - 1);
 
   // Interior blocks 1 .. nblk-2: every row window [S0 + 1024r + 16l, +16) lies
   // inside src, so each lane reads its 16 output bytes with ONE unaligned
   // 16-byte load (gfx950 runs in unaligned-access mode) -- no funnel, no
   // masks -- and the next block's 4 rows are in flight while this one is hashed.
-  // this wave's interior blocks: i0, i0 + st, ... <= il (< i1)
-  const uint64_t i1 = nblk > 1 ? nblk - 1 : 0;
-  const uint64_t st = kInter ? W : 1;
-  const uint64_t i0 = kInter ? 1 + gw : (b0 > 1 ? b0 : 1);
-  const uint64_t ie = kInter ? i1 : (b1 < i1 ? b1 : i1);  // exclusive end
-  if (i0 >= ie) return;
-  const uint64_t il = i0 + (ie - 1 - i0) / st * st;
-  auto nxt = [&](uint64_t b) { return b < il ? b : il; };  // clamped: past the end re-read the last
-  auto load4 = [&](uint64_t b, u32x4 (&v)[4]) {
-    const uint8_t *S = src + b * kPay - 4 + 16u * lane;
+  // Interior index i (block i + 1) of the workgroup's k-th hand-out:
+  const uint64_t ni = nblk > 2 ? nblk - 2 : 0;
+  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint32_t cmask = (1u << lg_chunk) - 1u;
+  auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
+  uint64_t c = blk_of(wave);
+  if (c >= ni) return;
+  uint64_t n1 = blk_of(kFastWaves + wave);
+  uint32_t knv = 0;  // LDS hand-out result for the block after n1, read one block later
+  if (lane == 0) knv = atomicAdd(&s_next, 1u);
+  auto load4 = [&](uint64_t i, u32x4 (&v)[4]) {
+    const uint8_t *S = src + (i + 1) * kPay - 4 + 16u * lane;
 #pragma unroll
     for (int r = 0; r < 4; r++)
       v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * kRowBytes));
   };
-  auto frame = [&](uint64_t b, const u32x4 (&cur)[4]) {
+  auto frame = [&](uint64_t i, const u32x4 (&cur)[4]) {
+    const uint64_t b = i + 1;
     uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
-    uint32_t c[4];
+    uint32_t cc[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       u32x4 v = cur[r];
@@ -1075,29 +1339,36 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
       if (r == 0) v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : row_step(c[k], w[k]);
+      for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : row_step(cc[k], w[k]);
     }
-    const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+    const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
     const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
     // binary.LittleEndian.PutUint32(block[:4], crc): lane 0's ob is the block start
     lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);
     if (crc_out) lane0_store_u32(crc_out + b, crcv);
   };
+  auto advance = [&]() {  // c <- n1 <- the next hand-out
+    c = n1;
+    n1 = blk_of(uni(knv));
+    if (lane == 0) knv = atomicAdd(&s_next, 1u);
+  };
   // two register sets, alternating roles (no copies that would wait on the
-  // prefetch); unconditional loads: past the end a wave re-reads its last block
+  // prefetch); unconditional loads: past the end a wave re-reads its block.
   // The first block is peeled so that the loop header is entered with the same
   // VMEM sequence from both edges ([next rows loaded][4 row stores]); a
   // mismatch there makes the waitcnt pass wait for the stores as well.
   u32x4 A[4], B[4];
-  load4(i0, A);
-  load4(nxt(i0 + st), B);
-  frame(i0, A);
-  for (uint64_t b = i0 + st; b <= il; b += 2 * st) {
-    load4(nxt(b + st), A);
-    frame(b, B);
-    if (b + st > il) break;
-    load4(nxt(b + 2 * st), B);
-    frame(b + st, A);
+  load4(c, A);
+  load4(n1 < ni ? n1 : c, B);
+  frame(c, A);
+  while (n1 < ni) {
+    advance();
+    load4(n1 < ni ? n1 : c, A);
+    frame(c, B);
+    if (n1 >= ni) break;
+    advance();
+    load4(n1 < ni ? n1 : c, B);
+    frame(c, A);
   }
 }
 
@@ -1114,13 +1385,15 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // overlapping lane 1's store with identical bytes.
 template <uint32_t lg_groups>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
-                                                           uint8_t *__restrict__ out,
+                                                           uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
                                                            uint32_t *__restrict__ bad_bitmap,
                                                            unsigned long long *__restrict__ first_bad,
                                                            const DeviceTables *__restrict__ tables) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  if (tid == 0) s_next = 2 * kFastWaves;
   const uint32_t *tg = &tables->tg[0][0];
   for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
     const uint32_t a = q * 16;
@@ -1161,11 +1434,14 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
   const uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
   const uint32_t gmask = (1u << lg_groups) - 1u;
   const uint32_t wave = uni(tid >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
-  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
-  const uint64_t b0 = uni64(nblk * gw / W), b1 = uni64(nblk * (gw + 1) / W);
-  if (b0 >= b1) return;
-  const uint64_t p0 = b0 << lg_groups, p1 = b1 << lg_groups;  // 4 KiB groups of this wave
+  // blocks handed out as in k_crc_grp (chunks of 2^lg_chunk consecutive blocks
+  // per workgroup, one block at a time per wave from an LDS counter); a wave
+  // walks a block's 4 KiB groups in order
+  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint32_t cmask = (1u << lg_chunk) - 1u;
+  auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
+  const uint64_t bstart = blk_of(wave);
+  if (bstart >= nblk) return;
   auto load4 = [&](uint64_t p, u32x4 (&v)[4]) {
     const uint8_t *S = blocks + p * HC_FRAME_BLOCK + 16u * lane;
 #pragma unroll
@@ -1207,18 +1483,48 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
       }
     }
   };
+  // group stream of this wave: (block, group) pairs; the producer cursor runs
+  // one group ahead of the group being stored and hashed
+  uint64_t pb = bstart, nb = blk_of(kFastWaves + wave);
+  uint32_t pg = 0;
+  bool pv = true;
+  uint32_t knv = 0;  // LDS hand-out result for the block after nb, read one block later
+  if (lane == 0) knv = atomicAdd(&s_next, 1u);
+  auto padv = [&]() {  // producer -> next group of the stream (pv = false past the end)
+    if (pg < gmask) {
+      pg++;
+      return;
+    }
+    pb = nb;
+    pg = 0;
+    pv = pb < nblk;
+    nb = blk_of(uni(knv));
+    if (lane == 0) knv = atomicAdd(&s_next, 1u);
+  };
   // first group peeled: both edges into the loop header carry the same VMEM
-  // sequence (see k_frame)
+  // sequence (see k_frame); past the end a wave re-reads its current group
   u32x4 A[4], Bv[4];
-  load4(p0, A);
-  load4(p0 + 1 < p1 ? p0 + 1 : p1 - 1, Bv);
-  group(p0, A);
-  for (uint64_t p = p0 + 1; p < p1; p += 2) {
-    load4(p + 1 < p1 ? p + 1 : p1 - 1, A);
+  uint64_t p = bstart << lg_groups;
+  load4(p, A);
+  padv();
+  uint64_t q = pv ? (pb << lg_groups) + pg : p;
+  bool qv = pv;
+  load4(q, Bv);
+  group(p, A);
+  while (qv) {
+    p = q;
+    padv();
+    q = pv ? (pb << lg_groups) + pg : p;
+    qv = pv;
+    load4(q, A);
     group(p, Bv);
-    if (p + 1 >= p1) break;
-    load4(p + 2 < p1 ? p + 2 : p1 - 1, Bv);
-    group(p + 1, A);
+    if (!qv) break;
+    p = q;
+    padv();
+    q = pv ? (pb << lg_groups) + pg : p;
+    qv = pv;
+    load4(q, Bv);
+    group(p, A);
   }
 }
 
@@ -1231,14 +1537,17 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t blk, uint64
   return z ^ (z >> 31);
 }
 
+// Block blk of the buffer is block first + blk of the synthetic batch (a rank's
+// shard of a global batch holds exactly the bytes the whole batch has there).
 __global__ __launch_bounds__(256) void k_fill(uint8_t *base, const uint64_t *off, const uint32_t *len,
                                                uint64_t stride, uint32_t ulen, uint64_t n,
-                                               uint64_t seed) {
+                                               uint64_t seed, uint64_t first) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t W = (uint64_t)gridDim.x * 4;
-  for (uint64_t blk = (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6); blk < n; blk += W) {
-    const uint64_t o = off ? off[blk] : blk * stride;
-    const uint32_t l = len ? len[blk] : ulen;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6); i < n; i += W) {
+    const uint64_t o = off ? off[i] : i * stride;
+    const uint32_t l = len ? len[i] : ulen;
+    const uint64_t blk = first + i;
     uint8_t *p = base + o;
     if ((((uintptr_t)p) & 15u) == 0) {
       for (uint32_t w = 2 * lane; 8 * w + 16 <= l; w += 128) {
@@ -1286,10 +1595,29 @@ hipError_t launch_uni(const Batch &b, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s) {
+hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_any<4, 3>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                     b.ulen, b.flags, b.nblocks, only_nonfast ? 1 : 0, b.crc_out, b.bad_bitmap, b.first_bad,
-                     b.tables);
+                     b.ulen, b.flags, b.nblocks, fast_mask, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+  return hipGetLastError();
+}
+
+uint32_t grp_lg_chunk(uint64_t nblocks, int grid) {
+  // chunks of up to 32 consecutive blocks per workgroup, at least 4 chunks each
+  uint32_t lg = 5;
+  while (lg > 0 && (nblocks >> lg) < (uint64_t)grid * 4) lg--;
+  return lg;
+}
+
+hipError_t launch_grp(const Batch &b, int grid, hipStream_t s) {
+  const uint32_t lg = grp_lg_chunk(b.nblocks, grid), rot = 0;
+  if (b.off || b.len)
+    hipLaunchKernelGGL((k_crc_grp<true, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, rot, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables);
+  else
+    hipLaunchKernelGGL((k_crc_grp<false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, rot, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables);
   return hipGetLastError();
 }
 
@@ -1297,7 +1625,9 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
                         const DeviceTables *tables, int grid, hipStream_t s) {
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_frame<true>, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, crc_out, tables);
+  const uint64_t ni = nblk > 2 ? nblk - 2 : 1;
+  hipLaunchKernelGGL(k_frame, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, grp_lg_chunk(ni, grid), crc_out,
+                     tables);
   return hipGetLastError();
 }
 
@@ -1305,8 +1635,9 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
                           const DeviceTables *tables, int grid, hipStream_t s) {
   if (nblk == 0) return hipSuccess;
+  const uint32_t lgc = grp_lg_chunk(nblk, grid);
 #define HC_UNFRAME(L)                                                                                      \
-  hipLaunchKernelGGL((k_unframe<L>), dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, out, crc_out, bad_bitmap, \
+  hipLaunchKernelGGL((k_unframe<L>), dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, lgc, out, crc_out, bad_bitmap, \
                      first_bad, tables)
   if (lg_groups == 0)
     HC_UNFRAME(0);
@@ -1319,8 +1650,8 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
 }
 
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
-                       uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, s, base, off, len, stride, ulen, n, seed);
+                       uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s, uint64_t first) {
+  hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, s, base, off, len, stride, ulen, n, seed, first);
   return hipGetLastError();
 }
 

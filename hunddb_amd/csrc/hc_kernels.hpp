@@ -42,8 +42,15 @@ constexpr uint32_t kFastLdsBytes = kLdsMainBytes + kLdsS4Bytes;
 hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s);
 // uniform batch, 16-B aligned base/stride, ulen a positive multiple of 4096
 hipError_t launch_uni(const Batch &b, int grid, hipStream_t s);
-// only_nonfast: process only blocks the streaming kernel skips.
-hipError_t launch_general(const Batch &b, bool only_nonfast, int grid, hipStream_t s);
+// fast_mask != 0: process only the blocks a streaming kernel skipped, i.e. all
+// but the 16-B aligned ones whose length is a positive multiple of fast_mask+1
+// (1023: k_crc_fast; 4095: k_crc_grp).  0: every block.
+hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s);
+// k_crc_grp: 4 KiB-multiple blocks (uniform, or off/len with device-side
+// routing of the others to k_crc_any with fast_mask 4095), per-workgroup
+// dynamic hand-out of chunked blocks.
+uint32_t grp_lg_chunk(uint64_t nblocks, int grid);
+hipError_t launch_grp(const Batch &b, int grid, hipStream_t s);
 // Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B blocks.
 constexpr uint32_t HC_FRAME_BLOCK = 4096;
 hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
@@ -53,8 +60,9 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
 hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_groups, uint8_t *out,
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
                           const DeviceTables *tables, int grid, hipStream_t s);
+// synthetic workload: buffer block i = block first + i of the seeded batch
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
-                       uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s);
+                       uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s, uint64_t first = 0);
 // Row f4 (hc_md5.hip): MD5 of each message (16-B digests at out16; workspace
 // = md5_workspace_bytes(n) bytes of device memory: tail slots + schedule), and
 // the Merkle levels above n leaves stored at levels16 (layout:

@@ -26,8 +26,9 @@
  *     pinned staging and are synchronous.  _dev_ entries take device pointers
  *     and a hipStream_t (passed as void*; NULL = the library's per-thread
  *     stream) and are asynchronous on that stream.
- *   - Every function is re-entrant and thread-safe (no global mutable state on
- *     the call path besides lazily-initialised per-device constant tables).
+ *   - Every function is re-entrant and thread-safe.  Shared state: the lazily
+ *     initialised per-device constant tables and the bounded pool of host-batch
+ *     pipelines (hc_host_pipelines).
  *   - Return codes: >= 0 success / Go-level result; < 0 library error.
  *     No C++ exception ever crosses this ABI.
  */
@@ -74,7 +75,9 @@ size_t hc_add_crcs_size(size_t n);
 /* AddCRCsToData (crc_util.go:41-64): chunk src into 4092-byte payloads, each
  * in a zeroed 4096-byte block with its CRC in bytes [0:4).  dst is caller
  * memory of >= hc_add_crcs_size(n) bytes (Go: make([]byte, ...)).  Returns the
- * number of bytes written, or (size_t)-1 if dst_cap is too small. */
+ * number of bytes written, or (size_t)-1 if dst_cap is too small or a GPU
+ * batch fails.  Outputs of >= 256 blocks are CRC'd on the GPU; without a
+ * gfx950 device they are CRC'd on the host (the Go function cannot fail). */
 size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap);
 /* SizeAfterAddingCRCs (crc_util.go:69-74), float64-ceil semantics. */
 uint64_t hc_size_after_crcs(uint64_t n);
@@ -180,6 +183,11 @@ int hc_dev_verify_prepare(int device, uint32_t *bad_bitmap, int64_t *first_bad,
 int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32_t *len,
                        uint64_t stride, uint32_t ulen, uint64_t nblocks, uint64_t seed,
                        void *stream);
+/* The same for a shard of a global batch: buffer block i gets the bytes of
+ * global block first_block + i (word w = splitmix64(seed, first_block + i, w)),
+ * so N ranks filling index ranges hold exactly the one-GPU batch. */
+int hc_dev_fill_range(int device, void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                      uint32_t ulen, uint64_t first_block, uint64_t nblocks, uint64_t seed, void *stream);
 
 /* ---- row f4: Merkle/MD5 integrity of SSTable data ----------------------------
  * lsm/sstable/sstable.go:2287-2420 CheckIntegrity: md5.Sum of every record
@@ -241,6 +249,10 @@ int hc_debug_tables(void *out, size_t cap);
 /* Number of visible gfx950 devices (0 if none; never initialises a context
  * on a machine without GPUs). */
 int hc_device_count(void);
+/* Host-batch pipelines alive in this process (pinned staging + device buffers
+ * + streams).  Host entries lease one per call from a pool of at most
+ * HC_MAX_PIPES (default 4); further concurrent callers wait for a free one. */
+int hc_host_pipelines(void);
 
 #ifdef __cplusplus
 }

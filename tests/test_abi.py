@@ -204,9 +204,26 @@ def test_batch_entries_fail_loudly_without_gpu(hc):
     assert ei.value.code == -3
     with pytest.raises(hc.HundCRCError):
         hc.stamp_blocks(buf)
-    # multi-hundred-block AddCRCsToData is a GPU batch too
     with pytest.raises(hc.HundCRCError):
-        hc.AddCRCsToData(bytes(4092 * 300))
+        hc.verify_blocks(buf)
+
+
+def test_add_crcs_to_data_without_gpu(hc, oracle, monkeypatch):
+    """AddCRCsToData cannot fail in Go (crc_util.go:41-64): a multi-hundred-block
+    input, a GPU batch on a gfx950 host, is CRC'd on the host path (hc_cpu.cpp)
+    when no device exists -- byte-exact vs the oracle.  Under HC_FORCE_GPU (test
+    mode) the missing device is an error instead."""
+    if hc.device_count() > 0:
+        pytest.skip("a gfx950 device is present")
+    rng = np.random.default_rng(300)
+    src = rng.integers(0, 256, 4092 * 300 + 77, dtype=np.uint8).tobytes()
+    out = hc.AddCRCsToData(src)
+    want = np.zeros(len(out), dtype=np.uint8)
+    assert oracle.lib().oc_add_crcs_to_data(src, len(src), want.ctypes.data) == len(out)
+    assert bytes(out) == want.tobytes()
+    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    with pytest.raises(hc.HundCRCError):
+        hc.AddCRCsToData(src)
 
 
 def test_read_from_disk_host(hc, golden, oracle):

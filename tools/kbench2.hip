@@ -1,0 +1,226 @@
+// kbench2.hip — A/B harness for k_crc_grp (per-workgroup block hand-out,
+// chunked XCD-local block order) against the production kernels (one
+// process, interleaved rounds, HIP-event time per launch).  Not part of the
+// product; build: make -C tools kbench2.
+//
+//   ./kbench2 <mode> [nblocks=1000000] [rounds=8] [launches=5]
+//   mode: 4096 | 8192 | 16384 (uniform batch) | mixed (configs[2]: 4/8/16 KiB
+//         drawn as bench.py's mixed_sizes, packed, off/len) | offlen4k
+//
+// Every CRC variant's words are checked against the production output.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../hunddb_amd/csrc/hc_kernels.hip"
+
+#define CK(x)                                                                                \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) {                                                                  \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(2);                                                                          \
+    }                                                                                        \
+  } while (0)
+
+namespace {
+
+uint64_t splitmix_h(uint64_t seed, uint64_t blk, uint64_t w) {
+  uint64_t z = seed + ((blk << 21) + w) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct Variant {
+  std::string name;
+  bool check;
+  std::function<void(hipStream_t)> run;
+  std::vector<float> ms;
+};
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  const std::string mode = argc > 1 ? argv[1] : "8192";
+  const uint64_t N = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1000000;
+  const int rounds = argc > 3 ? std::atoi(argv[3]) : 8;
+  const int launches = argc > 4 ? std::atoi(argv[4]) : 5;
+  const bool arrays = mode == "mixed" || mode == "offlen4k";
+  const uint32_t B = arrays ? 4096 : (uint32_t)std::atoi(mode.c_str());
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+
+  std::vector<uint64_t> ho(N);
+  std::vector<uint32_t> hl(N);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < N; i++) {
+    uint32_t l = B;
+    if (mode == "mixed") l = 4096u << (uint32_t)(splitmix_h(0x48756E64ull ^ 0x5A5A5A5A5A5A5A5Aull, i, (1u << 21) - 1) % 3);
+    ho[i] = total;
+    hl[i] = l;
+    total += l;
+  }
+  std::printf("device %s, %d CUs; mode %s: %llu blocks, %.3f GB\n", prop.gcnArchName, cus, mode.c_str(),
+              (unsigned long long)N, total / 1e9);
+  uint8_t *buf;
+  uint32_t *crc, *crc_ref;
+  uint64_t *doff;
+  uint32_t *dlen;
+  hc::DeviceTables *dt;
+  CK(hipMalloc(&buf, total));
+  CK(hipMalloc(&crc, N * 4));
+  CK(hipMalloc(&crc_ref, N * 4));
+  CK(hipMalloc(&doff, N * 8));
+  CK(hipMalloc(&dlen, N * 4));
+  CK(hipMalloc(&dt, sizeof(hc::DeviceTables)));
+  {
+    hc::DeviceTables h;
+    hc::build_device_tables(h);
+    CK(hipMemcpy(dt, &h, sizeof(h), hipMemcpyHostToDevice));
+  }
+  CK(hipMemcpy(doff, ho.data(), N * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dlen, hl.data(), N * 4, hipMemcpyHostToDevice));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  CK(hc::launch_fill(buf, doff, dlen, 0, 0, N, 0x48756E64, cus * 16, s));
+  CK(hipStreamSynchronize(s));
+
+  hc::Batch b{};
+  b.base = buf;
+  b.stride = B;
+  b.ulen = B;
+  b.nblocks = N;
+  b.tables = dt;
+  if (arrays) {
+    b.off = doff;
+    b.len = dlen;
+  }
+  const uint32_t lg5 = hc::grp_lg_chunk(N, cus);
+  using namespace hc;
+  std::vector<Variant> vs;
+  auto add = [&](const char *name, bool check, std::function<void(hipStream_t)> f) {
+    vs.push_back(Variant{name, check, f, {}});
+  };
+#define GRP(ARR, DYN, NUL, LG, ROT, ...)                                                                                   \
+  [&](hipStream_t st) {                                                                                          \
+    hipLaunchKernelGGL((k_crc_grp<ARR, DYN, NUL __VA_OPT__(,) __VA_ARGS__>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len,  \
+                       b.stride, b.ulen, b.flags, b.nblocks, (uint32_t)(LG), (uint32_t)(ROT), b.crc_out, b.bad_bitmap, b.first_bad, \
+                       b.tables);                                                                                \
+  }
+  // chunk sweep: HC_SWEEP=1 times k_crc_grp at lg_chunk 3..8 (C = 8 .. 256)
+  const bool sweep = std::getenv("HC_SWEEP") != nullptr;
+  if (!arrays) {
+    add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
+    if (sweep) {
+      add("grp pinned C=8", true, GRP(false, true, false, 3, 0, true));
+      add("grp pinned C=16", true, GRP(false, true, false, 4, 0, true));
+      add("grp pinned C=32", true, GRP(false, true, false, 5, 0, true));
+      add("grp pinned C=64", true, GRP(false, true, false, 6, 0, true));
+      add("grp pinned C=128", true, GRP(false, true, false, 7, 0, true));
+      add("grp pinned C=256", true, GRP(false, true, false, 8, 0, true));
+      add("grp pinned C=512", true, GRP(false, true, false, 9, 0, true));
+      add("grp pinned C=32 rot 13", true, GRP(false, true, false, 5, 13, true));
+      add("grp pinned C=64 rot 29", true, GRP(false, true, false, 6, 29, true));
+      add("grp pinned C=128 rot 53", true, GRP(false, true, false, 7, 53, true));
+      add("production launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+    } else {
+      add("grp pinned C=32", true, GRP(false, true, false, 5, 0, true));
+      add("grp pinned C=64", true, GRP(false, true, false, 6, 0, true));
+      add("grp pinned C=128", true, GRP(false, true, false, 7, 0, true));
+      add("grp C=32 (not pinned)", true, GRP(false, true, false, 5, 0));
+      add("uni (again)", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
+      add("grp pinned C=32 (again)", true, GRP(false, true, false, 5, 0, true));
+      add("grp pinned C=128 (again)", true, GRP(false, true, false, 7, 0, true));
+      add("NULL grp pinned C=32", false, GRP(false, true, true, 5, 0, true));
+    }
+  } else {
+    add("PROD k_crc_fast + k_crc_any(1023)", true, [&](hipStream_t st) {
+      launch_fast(b, false, cus, st);
+      launch_general(b, 1023, cus, st);
+    });
+#define GRPANY(LG, ROT)                        \
+  [&](hipStream_t st) {                     \
+    GRP(true, true, false, LG, ROT, true)(st); \
+    launch_general(b, 4095, cus, st);       \
+  }
+    if (sweep) {
+      add("grp pinned C=8 + any(4095)", true, GRPANY(3, 0));
+      add("grp pinned C=16 + any(4095)", true, GRPANY(4, 0));
+      add("grp pinned C=32 + any(4095)", true, GRPANY(5, 0));
+      add("grp pinned C=64 + any(4095)", true, GRPANY(6, 0));
+      add("grp pinned C=128 + any(4095)", true, GRPANY(7, 0));
+      add("grp pinned C=256 + any(4095)", true, GRPANY(8, 0));
+      add("grp pinned C=32 rot 13 + any", true, GRPANY(5, 13));
+      add("grp pinned C=64 rot 29 + any", true, GRPANY(6, 29));
+      add("grp pinned C=128 rot 53 + any", true, GRPANY(7, 53));
+      add("production launch_grp + any", true, [&](hipStream_t st) {
+        launch_grp(b, cus, st);
+        launch_general(b, 4095, cus, st);
+      });
+    } else {
+      add("grp pinned C=32 + any(4095)", true, GRPANY(5, 0));
+      add("grp pinned C=64 + any(4095)", true, GRPANY(6, 0));
+      add("grp pinned C=128 + any(4095)", true, GRPANY(7, 0));
+      add("grp pinned C=32 alone", true, GRP(true, true, false, 5, 0, true));
+      add("grp pinned C=32 + any (again)", true, GRPANY(5, 0));
+      add("any(4095) sweep alone (early exit)", false, [&](hipStream_t st) { launch_general(b, 4095, cus, st); });
+      add("NULL grp pinned C=32", false, GRP(true, true, true, 5, 0, true));
+    }
+  }
+
+  b.crc_out = crc_ref;
+  vs[0].run(s);
+  CK(hipStreamSynchronize(s));
+  std::vector<uint32_t> ref(N), got(N);
+  CK(hipMemcpy(ref.data(), crc_ref, N * 4, hipMemcpyDeviceToHost));
+  b.crc_out = crc;
+  int bad = 0;
+  for (auto &v : vs) {
+    if (v.check) {
+      CK(hipMemsetAsync(crc, 0, N * 4, s));
+      v.run(s);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(got.data(), crc, N * 4, hipMemcpyDeviceToHost));
+      if (got != ref) {
+        uint64_t k = 0;
+        while (k < N && got[k] == ref[k]) k++;
+        std::printf("MISMATCH in variant %s at block %llu (%08x vs %08x)\n", v.name.c_str(), (unsigned long long)k,
+                    got[k], ref[k]);
+        bad++;
+      }
+    } else {
+      v.run(s);
+    }
+  }
+  CK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; r++)
+    for (auto &v : vs)
+      for (int l = 0; l < launches; l++) {
+        CK(hipEventRecord(e0, s));
+        v.run(s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.ms.push_back(ms);
+      }
+  std::printf("%-40s %10s %10s %8s %8s\n", "variant", "med GB/s", "best GB/s", "med %pk", "med ms");
+  for (auto &v : vs) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2], best = v.ms[0];
+    std::printf("%-40s %10.1f %10.1f %7.2f%% %8.4f\n", v.name.c_str(), total / med / 1e6, total / best / 1e6,
+                total / med / 1e6 / 80.0, med);
+  }
+  return bad ? 3 : 0;
+}

@@ -1,0 +1,268 @@
+// kcopy2.hip — what read+write streams reach on this chip (the ceiling of
+// k_frame / k_unframe).  Not part of the product; build: make -C tools kcopy2.
+//
+//   ./kcopy2 [MiB=4096] [rounds=6] [launches=5]
+//
+// GB/s = (bytes read + bytes written) / HIP-event launch time, median over
+// interleaved rounds; "read" and "write" rows count their one stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                                \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) {                                                                  \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(2);                                                                          \
+    }                                                                                        \
+  } while (0)
+
+namespace {
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int kPol>
+__device__ __forceinline__ f4 ld(const f4 *p) {
+  if constexpr (kPol == 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <int kPol>
+__device__ __forceinline__ void st(f4 *p, f4 v) {
+  if constexpr (kPol == 1)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+// grid-stride float4 copy, U loads in flight per thread before the stores
+template <int U, int kLd, int kSt>
+__global__ __launch_bounds__(256) void k_copy(const f4 *__restrict__ src, f4 *__restrict__ dst, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = ld<kLd>(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; u++) st<kSt>(dst + i + u * stride, v[u]);
+  }
+  for (; i < n; i += stride) st<kSt>(dst + i, ld<kLd>(src + i));
+}
+
+// block-contiguous: workgroup w copies elements [w*per, (w+1)*per) in tiles of
+// 256 threads x U float4
+template <int U, int kLd, int kSt>
+__global__ __launch_bounds__(256) void k_copy_blk(const f4 *__restrict__ src, f4 *__restrict__ dst, size_t n) {
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  const size_t lo = (size_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  for (size_t t = lo + threadIdx.x; t < hi; t += 256 * U) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (t + u * 256 < hi) v[u] = ld<kLd>(src + t + u * 256);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (t + u * 256 < hi) st<kSt>(dst + t + u * 256, v[u]);
+  }
+}
+
+template <int U, int kLd>
+__global__ __launch_bounds__(256) void k_read(const f4 *__restrict__ src, size_t n, float *sink) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  f4 acc = {0, 0, 0, 0};
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+#pragma unroll
+    for (int u = 0; u < U; u++) acc += ld<kLd>(src + i + u * stride);
+  }
+  if (acc.x == 1234.5f) sink[0] = acc.y;
+}
+
+template <int kSt>
+__global__ __launch_bounds__(256) void k_write(f4 *__restrict__ dst, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const f4 v = {1.f, 2.f, 3.f, (float)threadIdx.x};
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) st<kSt>(dst + i, v);
+}
+
+// Persistent copy with the k_crc_grp hand-out: workgroup g owns the chunks of
+// 2^kLg consecutive 4 KiB pieces c*G + g; its waves take pieces one at a time
+// from an LDS counter (index prefetched one piece ahead).  A wave loads its
+// next piece (4 x 1 KiB rows) while it stores the current one.  kLdsKiB pads
+// the workgroup's LDS like the product kernels (occupancy).
+template <int kWaves, int kLg, int kLdsKiB, int kLd, int kSt>
+__global__ __launch_bounds__(kWaves * 64) void k_dyncopy(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                         uint64_t npieces, uint32_t *sink) {
+  __shared__ uint32_t lds_pad[kLdsKiB * 256 + 1];
+  __shared__ uint32_t ctr;
+  if (threadIdx.x == 0) ctr = 2 * kWaves;
+  if (sink[1] == 0xDEADu) lds_pad[threadIdx.x] = 1;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t G = gridDim.x, g = blockIdx.x;
+  auto piece = [&](uint32_t k) -> uint64_t {
+    return (((uint64_t)(k >> kLg) * G + g) << kLg) | (k & ((1u << kLg) - 1u));
+  };
+  uint64_t p = piece(wave), pn = piece(kWaves + wave);
+  if (p >= npieces) return;
+  uint32_t knv = 0;
+  if (lane == 0) knv = atomicAdd(&ctr, 1u);
+  auto load = [&](uint64_t q, f4 (&v)[4]) {
+    const f4 *S = reinterpret_cast<const f4 *>(src + q * 4096) + lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = ld<kLd>(S + r * 64);
+  };
+  auto store = [&](uint64_t q, const f4 (&v)[4]) {
+    f4 *D = reinterpret_cast<f4 *>(dst + q * 4096) + lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) st<kSt>(D + r * 64, v[r]);
+  };
+  f4 A[4], B[4];
+  load(p, A);
+  for (;;) {
+    bool vn = pn < npieces;
+    load(vn ? pn : p, B);
+    store(p, A);
+    if (!vn) return;
+    p = pn;
+    pn = piece(__builtin_amdgcn_readfirstlane(knv));
+    if (lane == 0) knv = atomicAdd(&ctr, 1u);
+    vn = pn < npieces;
+    load(vn ? pn : p, A);
+    store(p, B);
+    if (!vn) return;
+    p = pn;
+    pn = piece(__builtin_amdgcn_readfirstlane(knv));
+    if (lane == 0) knv = atomicAdd(&ctr, 1u);
+  }
+}
+
+// the same hand-out with static round-robin pieces (piece k of the workgroup
+// sequence to wave k % kWaves): isolates the dynamic part
+template <int kWaves, int kLg, int kLdsKiB, int kLd, int kSt>
+__global__ __launch_bounds__(kWaves * 64) void k_statcopy(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                          uint64_t npieces, uint32_t *sink) {
+  __shared__ uint32_t lds_pad[kLdsKiB * 256 + 1];
+  if (sink[1] == 0xDEADu) lds_pad[threadIdx.x] = 1;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t G = gridDim.x, g = blockIdx.x;
+  auto piece = [&](uint32_t k) -> uint64_t {
+    return (((uint64_t)(k >> kLg) * G + g) << kLg) | (k & ((1u << kLg) - 1u));
+  };
+  uint32_t k = wave;
+  uint64_t p = piece(k);
+  if (p >= npieces) return;
+  f4 A[4];
+  for (;;) {
+    const f4 *S = reinterpret_cast<const f4 *>(src + p * 4096) + lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) A[r] = ld<kLd>(S + r * 64);
+    f4 *D = reinterpret_cast<f4 *>(dst + p * 4096) + lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) st<kSt>(D + r * 64, A[r]);
+    k += kWaves;
+    p = piece(k);
+    if (p >= npieces) return;
+  }
+}
+
+struct Variant {
+  std::string name;
+  double bytes;
+  std::function<void(hipStream_t)> run;
+  std::vector<float> ms;
+};
+}  // namespace
+
+int main(int argc, char **argv) {
+  const size_t mib = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 4096;
+  const int rounds = argc > 2 ? std::atoi(argv[2]) : 6;
+  const int launches = argc > 3 ? std::atoi(argv[3]) : 5;
+  const size_t bytes = mib << 20, n = bytes / 16;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  std::printf("device %s, %d CUs; %zu MiB per stream\n", prop.gcnArchName, cus, mib);
+  f4 *a, *b;
+  float *sink;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&b, bytes));
+  CK(hipMalloc(&sink, 256));
+  CK(hipMemset(a, 0x5A, bytes));  // non-zero data (DVFS: zeros clock higher)
+  CK(hipMemset(b, 0xA5, bytes));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  std::vector<Variant> vs;
+  const double rw = 2.0 * bytes;
+#define COPY(U, L, S, G) [=](hipStream_t st) { hipLaunchKernelGGL((k_copy<U, L, S>), dim3(G), dim3(256), 0, st, a, b, n); }
+#define BLK(U, L, S, G) [=](hipStream_t st) { hipLaunchKernelGGL((k_copy_blk<U, L, S>), dim3(G), dim3(256), 0, st, a, b, n); }
+  vs.push_back({"hipMemcpyAsync D2D", rw, [=](hipStream_t st) { CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, st)); }, {}});
+  vs.push_back({"gs copy U4 pl/pl 8x256/CU", rw, COPY(4, 0, 0, cus * 8), {}});
+  vs.push_back({"gs copy U4 nt/nt 8x256/CU", rw, COPY(4, 1, 1, cus * 8), {}});
+  vs.push_back({"gs copy U1 pl/pl 8x256/CU", rw, COPY(1, 0, 0, cus * 8), {}});
+  vs.push_back({"gs copy U8 pl/pl 8x256/CU", rw, COPY(8, 0, 0, cus * 8), {}});
+  vs.push_back({"gs copy U8 nt/nt 8x256/CU", rw, COPY(8, 1, 1, cus * 8), {}});
+  vs.push_back({"gs copy U4 pl/pl 4x256/CU", rw, COPY(4, 0, 0, cus * 4), {}});
+  vs.push_back({"gs copy U8 pl/pl 2x256/CU", rw, COPY(8, 0, 0, cus * 2), {}});
+  vs.push_back({"gs copy U1 pl/pl one thread per f4", rw, COPY(1, 0, 0, (unsigned)(n / 256)), {}});
+  vs.push_back({"blk copy U4 pl/pl 8x256/CU", rw, BLK(4, 0, 0, cus * 8), {}});
+  vs.push_back({"blk copy U8 nt/nt 8x256/CU", rw, BLK(8, 1, 1, cus * 8), {}});
+  vs.push_back({"blk copy U4 pl/nt 8x256/CU", rw, BLK(4, 0, 1, cus * 8), {}});
+  const uint64_t np = bytes / 4096;
+  const uint8_t *a8 = reinterpret_cast<const uint8_t *>(a);
+  uint8_t *b8 = reinterpret_cast<uint8_t *>(b);
+#define DYN(W, LG, LDS, L, S, G)                                                                          \
+  [=](hipStream_t st) {                                                                                   \
+    hipLaunchKernelGGL((k_dyncopy<W, LG, LDS, L, S>), dim3(G), dim3(W * 64), 0, st, a8, b8, np, (uint32_t *)sink); \
+  }
+#define STAT(W, LG, LDS, L, S, G)                                                                          \
+  [=](hipStream_t st) {                                                                                    \
+    hipLaunchKernelGGL((k_statcopy<W, LG, LDS, L, S>), dim3(G), dim3(W * 64), 0, st, a8, b8, np, (uint32_t *)sink); \
+  }
+  vs.push_back({"dyn copy w16 C=32 144KiB LDS nt/nt", rw, DYN(16, 5, 144, 1, 1, cus), {}});
+  vs.push_back({"dyn copy w16 C=32 144KiB LDS pl/pl", rw, DYN(16, 5, 144, 0, 0, cus), {}});
+  vs.push_back({"dyn copy w16 C=128 144KiB LDS nt/nt", rw, DYN(16, 7, 144, 1, 1, cus), {}});
+  vs.push_back({"dyn copy w16 C=8 144KiB LDS nt/nt", rw, DYN(16, 3, 144, 1, 1, cus), {}});
+  vs.push_back({"dyn copy w16 C=32 2/CU nt/nt", rw, DYN(16, 5, 1, 1, 1, cus * 2), {}});
+  vs.push_back({"dyn copy w8 C=32 4/CU nt/nt", rw, DYN(8, 5, 1, 1, 1, cus * 4), {}});
+  vs.push_back({"dyn copy w16 C=32 144KiB nt/pl", rw, DYN(16, 5, 144, 1, 0, cus), {}});
+  vs.push_back({"stat copy w16 C=32 144KiB LDS nt/nt", rw, STAT(16, 5, 144, 1, 1, cus), {}});
+  vs.push_back({"stat copy w16 C=1 144KiB LDS nt/nt", rw, STAT(16, 0, 144, 1, 1, cus), {}});
+  vs.push_back({"READ only gs U4 pl 8x256/CU", (double)bytes,
+                [=](hipStream_t st) { hipLaunchKernelGGL((k_read<4, 0>), dim3(cus * 8), dim3(256), 0, st, a, n, sink); }, {}});
+  vs.push_back({"READ only gs U4 nt 8x256/CU", (double)bytes,
+                [=](hipStream_t st) { hipLaunchKernelGGL((k_read<4, 1>), dim3(cus * 8), dim3(256), 0, st, a, n, sink); }, {}});
+  vs.push_back({"WRITE only gs pl 8x256/CU", (double)bytes,
+                [=](hipStream_t st) { hipLaunchKernelGGL((k_write<0>), dim3(cus * 8), dim3(256), 0, st, b, n); }, {}});
+  vs.push_back({"WRITE only gs nt 8x256/CU", (double)bytes,
+                [=](hipStream_t st) { hipLaunchKernelGGL((k_write<1>), dim3(cus * 8), dim3(256), 0, st, b, n); }, {}});
+  for (auto &v : vs) v.run(s);
+  CK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; r++)
+    for (auto &v : vs)
+      for (int l = 0; l < launches; l++) {
+        CK(hipEventRecord(e0, s));
+        v.run(s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.ms.push_back(ms);
+      }
+  std::printf("%-40s %10s %10s %8s\n", "variant", "med GB/s", "best GB/s", "med ms");
+  for (auto &v : vs) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2], best = v.ms[0];
+    std::printf("%-40s %10.1f %10.1f %8.4f\n", v.name.c_str(), v.bytes / med / 1e6, v.bytes / best / 1e6, med);
+  }
+  return 0;
+}
