@@ -6,15 +6,29 @@ HundDB's utils/crc CheckBlockIntegrity computes per block,
 /root/reference/utils/crc/crc_util.go:88-100), through the C ABI
 (hc_dev_crc32_blocks) into the hand-written gfx950 streaming kernel.
 
-Default workload (N=1): the north star, 1M x 8 KiB blocks (8.192 GB) resident
-in HBM, synthetic splitmix64 data.  With N ranks each rank owns its own 1M-block
-shard (partition by block index, no data-path collective): weak scaling.
-`--workload config4` runs 16M x 8 KiB split across the ranks (strong scaling).
+Workloads (synthetic splitmix64 data keyed by GLOBAL block index, generated in HBM):
+  N = 1, default   the north star, 1M x 8 KiB (8.192 GB), BASELINE.json's target config.
+  N > 1, default   configs[3] strong scaling: ONE global batch of 16M x 8 KiB
+                   (131 GB) split by block index (hunddb_amd.shard.index_range),
+                   rank r fills and hashes blocks [lo_r, hi_r) of it.  After the
+                   timed region the CRC words are all-gathered over RCCL and rank 0
+                   re-runs the WHOLE batch alone: `speedup_vs_1gpu` is that 1-GPU
+                   step time / the N-GPU step time on the same batch, and the
+                   gathered words must equal the 1-GPU words.
+  --workload       any of WORKLOADS below (configs[1], configs[2], 16 KiB, the
+                   framing kernels f1/f2, off/len metadata path).
 
-Prints ONE JSON line (rank 0) with value = whole-job GiB/s (all ranks' bytes /
-max-over-ranks wall time), the roofline of the dominant kernel (algorithmic
-bytes per launch / mean HIP-event launch time vs 8 TB/s) and the CPU
-baseline (the oracle's restatement of Go's crc32.ChecksumIEEE on host cores).
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts its N
+ranks itself (subprocesses with the torch.distributed.run environment, started
+before this process touches the GPU); under torch.distributed.run it is one rank.
+
+Prints ONE JSON line (rank 0): value = whole-job GiB/s (all ranks' bytes / the
+max-over-ranks wall time of the K timed steps), the roofline of the dominant
+kernel (algorithmic bytes per launch / mean HIP-event launch time vs 8 TB/s, PMC
+traffic from rocprofv3 child runs at N=1) and, at N=1, the CPU baseline (the
+oracle's restatement of Go's crc32.ChecksumIEEE on the host cores, 1 thread and
+all threads with the run-to-run spread, and system zlib's crc32 as a second,
+independent point).
 """
 import argparse
 import csv
@@ -32,8 +46,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+SEED = 0x48756E64
 WORKLOADS = {
-    # name: (blocks per rank or total, block bytes or "mixed", scaling)
+    # name: (blocks per rank (weak) or in total (strong), block bytes or kind, scaling)
     "northstar": (1_000_000, 8192, "weak"),
     "config2": (1_000_000, 4096, "weak"),
     "config3": (1_000_000, "mixed", "weak"),
@@ -48,23 +63,27 @@ WORKLOADS = {
     # config2's blocks described by off/len arrays (the per-block metadata path)
     "offlen4k": (1_000_000, "offlen4k", "weak"),
 }
+KERNEL_RE = {"frame": "k_frame", "unframe": "k_unframe"}  # else the streaming CRC kernel
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="northstar", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: northstar at N=1, config4 (strong scaling) at N>1")
     ap.add_argument("--blocks", type=int, default=0, help="override the block count")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc", choices=["auto", "on", "off"], default="auto",
                     help="collect FETCH_SIZE/WRITE_SIZE in rocprofv3 child runs (N=1 only)")
+    ap.add_argument("--ref1", choices=["auto", "on", "off"], default="auto",
+                    help="strong scaling: rank 0 re-runs the whole batch alone (speedup + word check)")
     ap.add_argument("--settle", type=float, default=0.5, help="untimed clock-settle seconds before warmup")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--json-out", default="")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # --------------------------------------------------------------------------
@@ -75,11 +94,10 @@ def pmc_traffic(args):
     if not exe:
         return None, "rocprofv3 not found"
     out = {}
-    # the streaming kernel: k_crc_uni (uniform 4/8/16 KiB blocks) or k_crc_fast
-    kern = {"frame": "k_frame", "unframe": "k_unframe"}.get(WORKLOADS[args.workload][1], "k_crc_(uni|fast)")
+    kern = KERNEL_RE.get(WORKLOADS[args.workload][1], "k_crc_(grp|uni|fast)")
     tmp = tempfile.mkdtemp(prefix="hc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
-             "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off"]
+             "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off", "--settle", "0"]
     if args.blocks:
         child += ["--blocks", str(args.blocks)]
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -115,8 +133,8 @@ def pmc_traffic(args):
 
 
 def mixed_sizes(seed, lo, n):
-    """Config-3 block sizes: 4096 << (splitmix64(seed ^ 0x5A.., i, 2^21-1) % 3),
-    the same draw as tests/golden/gen_golden.py."""
+    """Config-3 block sizes of global blocks lo .. lo+n-1: 4096 << (splitmix64(seed
+    ^ 0x5A.., i, 2^21-1) % 3), the same draw as tests/golden/gen_golden.py."""
     import numpy as np
     i = np.arange(lo, lo + n, dtype=np.uint64)
     with np.errstate(over="ignore"):
@@ -128,70 +146,124 @@ def mixed_sizes(seed, lo, n):
 
 
 # --------------------------------------------------------------------------
-def cpu_baseline_framing(kind, dev_src, budget_s):
-    """One host thread running the oracle's restatement of the reference loop
-    (Go runs each AddCRCsToData / ReadFromDisk call on one goroutine) over a
-    256 MB sample of the same data; bytes counted as in the GPU line (read +
-    written)."""
-    import ctypes
+# CPU baseline (rank 0, N = 1): the reference's CPU path timed on the host cores
+def _rate(fn, nbytes, seconds):
+    """GiB/s of fn() (nbytes per call) run back to back for >= seconds."""
+    fn()
+    t0, k = time.perf_counter(), 0
+    while True:
+        fn()
+        k += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return k * nbytes / dt / 2**30
+
+
+def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None):
+    """Go's crc32.ChecksumIEEE over block[4:len] of every sample block
+    (crc_util.go:16,94), three ways: the oracle's restatement of Go's amd64
+    algorithm (oracle/hc_oracle.c oc_crc32_go_amd64: PCLMULQDQ fold + slicing-by-8)
+    on `threads` threads (5 slices: median and spread) and on 1 thread, and
+    system zlib's crc32 (Python zlib, an independent implementation) on 1 thread.
+    The oracle's words for the sample are also compared with the GPU's."""
+    import zlib
+
     import numpy as np
+
+    from oracle import oracle as O
+    nbytes = int(lens.sum(dtype=np.uint64))
+    port = lambda t: O.crc32_blocks(sample, off=off, lens=lens, threads=t)  # noqa: E731
+    words = port(threads)
+    mv = memoryview(sample)
+    pairs = list(zip(off.tolist(), lens.tolist()))
+
+    def zl():
+        for o, n_ in pairs:
+            zlib.crc32(mv[o + 4:o + n_])
+    zl_ok = all(zlib.crc32(mv[o + 4:o + n_]) == int(words[k]) for k, (o, n_) in enumerate(pairs[:200]))
+    slices = [_rate(lambda: port(threads), nbytes, 0.1 * budget_s) for _ in range(5)]
+    one = _rate(lambda: port(1), nbytes, 0.25 * budget_s)
+    zrate = _rate(zl, nbytes, 0.25 * budget_s)
+    res = {"value": round(float(np.median(slices)), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "sample": f"{what}: {len(pairs)} blocks, {nbytes / 2**20:.0f} MiB copied from the GPU batch; "
+                     f"oracle/hc_oracle.c oc_crc32_go_amd64 restates Go 1.23 hash/crc32 amd64 "
+                     f"(PCLMULQDQ fold + slicing-by-8), pclmul={O.lib().oc_have_pclmul()}",
+           "spread": [round(min(slices), 3), round(max(slices), 3)],
+           "spread_note": f"min/max of 5 slices of {0.1 * budget_s:.1f} s on {threads} threads",
+           "single_thread": round(one, 3),
+           "zlib_single_thread": round(zrate, 3),
+           "zlib_note": f"system zlib {zlib.ZLIB_RUNTIME_VERSION} crc32 via Python, 1 thread; "
+                        f"same words as the oracle on the first 200 blocks: {zl_ok}"}
+    if gpu_words is not None:
+        res["matches_gpu"] = bool(np.array_equal(words, gpu_words))
+    return res
+
+
+def cpu_baseline_framing(kind, dev_src, threads, budget_s):
+    """The oracle's restatement of the reference loop over a 256 MB sample of
+    the same data (Go runs each AddCRCsToData / ReadFromDisk call on one
+    goroutine): 1 thread, and `threads` threads on disjoint slices; bytes
+    counted as in the GPU line (read + written)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
     from oracle import oracle as O
     L = O.lib()
     nblk = (256 << 20) // 4096
+    per_t = nblk // threads
     if kind == "frame":  # crc_util.go:41-64
         src = dev_src[: nblk * 4092].cpu().numpy()
         dst = np.empty(nblk * 4096, dtype=np.uint8)
-        run = lambda: L.oc_add_crcs_to_data(src.ctypes.data, src.size, dst.ctypes.data)  # noqa: E731
-        per = src.size + dst.size
+
+        def run(a, b):
+            L.oc_add_crcs_to_data(src.ctypes.data + a * 4092, (b - a) * 4092, dst.ctypes.data + a * 4096)
         what = f"oc_add_crcs_to_data over {src.size} B of payload (crc_util.go:41-64)"
     else:  # block_manager.go:189-242
         blocks = dev_src[: nblk * 4096].cpu().numpy()
         out = np.empty(nblk * 4092, dtype=np.uint8)
-        fo, bad = ctypes.c_uint64(0), ctypes.c_int64(0)
-        run = lambda: L.oc_read_from_disk(blocks.ctypes.data, blocks.size, 4096, 0, out.size,  # noqa: E731
-                                          out.ctypes.data, ctypes.byref(fo), ctypes.byref(bad))
-        per = blocks.size + out.size
+
+        def run(a, b):
+            fo, bad = ctypes.c_uint64(0), ctypes.c_int64(0)
+            L.oc_read_from_disk(blocks.ctypes.data + a * 4096, (b - a) * 4096, 4096, 0, (b - a) * 4092,
+                                out.ctypes.data + a * 4092, ctypes.byref(fo), ctypes.byref(bad))
         what = f"oc_read_from_disk over {nblk} stamped 4096-B blocks (block_manager.go:189-242)"
-    run()
-    t0, passes = time.perf_counter(), 0
-    while True:
-        run()
-        passes += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(passes * per / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{what}, {passes} passes in {dt:.1f} s, read+written bytes"}
+    nbytes = nblk * (4092 + 4096)
+    pool = ThreadPoolExecutor(threads)
+
+    def par():  # ctypes releases the GIL for the call
+        list(pool.map(lambda t: run(t * per_t, (t + 1) * per_t), range(threads)))
+    slices = [_rate(par, per_t * threads * (4092 + 4096), 0.1 * budget_s) for _ in range(5)]
+    one = _rate(lambda: run(0, nblk), nbytes, 0.4 * budget_s)
+    pool.shutdown()
+    return {"value": round(float(np.median(slices)), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{what}, read+written bytes",
+            "spread": [round(min(slices), 3), round(max(slices), 3)],
+            "spread_note": f"min/max of 5 slices of {0.1 * budget_s:.1f} s on {threads} threads",
+            "single_thread": round(one, 3)}
 
 
-def cpu_baseline(host_sample, block, threads, budget_s):
-    """The oracle's restatement of Go's amd64 crc32.ChecksumIEEE (CLMUL +
-    slicing-by-8) over the same blocks, on `threads` host threads."""
-    from oracle import oracle as O
-    n = host_sample.size // block
-    O.crc32_blocks(host_sample, stride=block, ulen=block, threads=threads)  # warm
-    t0 = time.perf_counter()
-    passes = 0
-    while True:
-        O.crc32_blocks(host_sample, stride=block, ulen=block, threads=threads)
-        passes += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    gib = passes * n * block / dt / 2**30
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x {block} B blocks copied from the GPU batch, {passes} passes in {dt:.1f} s; "
-                      f"oracle/hc_oracle.c oc_crc32_go_amd64 (restates Go 1.23 hash/crc32 amd64: "
-                      f"PCLMULQDQ fold + slicing-by-8), pclmul={O.lib().oc_have_pclmul()}"}
+# --------------------------------------------------------------------------
+def self_launch(argv, nproc, script=None):
+    """`bench.py --gpus N` without WORLD_SIZE: run N ranks (one per GPU) as child
+    processes with the torch.distributed.run environment; this process never
+    touches the GPU.  Returns the first failing rank's exit status or 0."""
+    from hunddb_amd import shard
+    cmd = [sys.executable, os.path.abspath(script or __file__)] + list(argv)
+    return shard.spawn_ranks(cmd, nproc)
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.child:
+        sys.exit(self_launch(sys.argv[1:] if argv is None else argv, args.gpus))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and "WORLD_SIZE" in os.environ:
-        args.gpus = world
+    args.gpus = world
+    if args.workload is None:
+        args.workload = "northstar" if world == 1 else "config4"
 
     traffic, pmc_note = None, "off"
     if not args.child and rank == 0 and world == 1 and args.pmc != "off":
@@ -209,10 +281,10 @@ def main():
     local_dev = local % max(1, ndev)  # (rehearsal: ranks may share a GPU)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
+    backend = os.environ.get("HC_DIST_BACKEND", "nccl")
     if world > 1:
         # RCCL (backend "nccl") over xGMI; HC_DIST_BACKEND=gloo rehearses the
         # N>1 path with several ranks sharing one GPU.
-        backend = os.environ.get("HC_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
@@ -223,36 +295,44 @@ def main():
         nblk = args.blocks
     if scaling == "strong":  # one global batch, partitioned by block index
         lo, hi = shard.index_range(nblk, world, rank)
-        my = hi - lo
-    else:  # every rank owns its own full-size shard (blocks rank*n .. rank*n+n-1)
-        lo, my = nblk * rank, nblk
+        total_blocks = nblk
+    else:  # every rank owns its own full-size shard: global blocks rank*n .. rank*n+n-1
+        lo, hi = nblk * rank, nblk * (rank + 1)
+        total_blocks = nblk * world
+    my = hi - lo
+    counts = [shard.index_range(nblk, world, r)[1] - shard.index_range(nblk, world, r)[0]
+              if scaling == "strong" else nblk for r in range(world)]
     stream = torch.cuda.current_stream()
-    seed = 0x48756E64
 
+    sample = None  # (host blocks, off, lens) for the CPU baseline
     if bsize == "mixed":
-        sizes = mixed_sizes(seed, lo, my)
+        sizes = mixed_sizes(SEED, lo, my)
         off = np.zeros(my, dtype=np.uint64)
         off[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
         total = int(off[-1]) + int(sizes[-1])
         doff = torch.from_numpy(off.view(np.int64)).to(dev)
         dlen = torch.from_numpy(sizes.view(np.int32)).to(dev)
         buf = torch.empty(total, dtype=torch.uint8, device=dev)
-        crc.dev_fill_blocks(buf, seed ^ rank, off=doff, lens=dlen, nblocks=my)
+        crc.dev_fill_range(buf, SEED, lo, my, off=doff, lens=dlen)
         kw = dict(off=doff, lens=dlen, nblocks=my)
         step_bytes = total
-        block_desc = "mixed 4/8/16 KiB"
+        block_desc = "mixed 4/8/16 KiB, off/len arrays"
+        k = int(np.searchsorted(off, 512 << 20))
+        sample = (slice(0, int(off[k - 1]) + int(sizes[k - 1])), off[:k].copy(), sizes[:k].copy())
     elif bsize == "offlen4k":
         buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
-        crc.dev_fill_blocks(buf, seed ^ rank, stride=4096, ulen=4096, nblocks=my)
+        crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
         doff = torch.arange(my, dtype=torch.int64, device=dev) * 4096
         dlen = torch.full((my,), 4096, dtype=torch.int32, device=dev)
         kw = dict(off=doff, lens=dlen, nblocks=my)
         step_bytes = my * 4096
         block_desc = "4096 B via off/len arrays"
+        k = min(my, (512 << 20) // 4096)
+        sample = (slice(0, k * 4096), np.arange(k, dtype=np.uint64) * 4096, np.full(k, 4096, np.uint32))
     elif bsize == "frame":
         npay = my * 4092 - 1000  # ragged last block
         raw = torch.empty(npay + 1, dtype=torch.uint8, device=dev)
-        crc.dev_fill_blocks(raw, seed ^ rank, stride=npay + 1, ulen=npay + 1, nblocks=1)
+        crc.dev_fill_range(raw, SEED, lo, 1, stride=npay + 1, ulen=npay + 1)
         buf = raw[1:]  # payload at an odd address
         dst = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
         kw = None
@@ -260,7 +340,7 @@ def main():
         block_desc = "AddCRCsToData: 4092-B payload slices -> 4096-B stamped blocks"
     elif bsize == "unframe":
         buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
-        crc.dev_fill_blocks(buf, seed ^ rank, stride=4096, ulen=4096, nblocks=my)
+        crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
         crc.dev_crc32_blocks(buf, None, stride=4096, ulen=4096, nblocks=my, flags=crc.HC_F_STAMP)
         dst = torch.empty(my * 4092, dtype=torch.uint8, device=dev)
         bitmap = torch.empty((my + 31) // 32, dtype=torch.int32, device=dev)
@@ -271,52 +351,61 @@ def main():
         block_desc = "ReadFromDisk: verify 4096-B blocks + strip CRCs"
     else:
         buf = torch.empty(my * bsize, dtype=torch.uint8, device=dev)
-        crc.dev_fill_blocks(buf, seed ^ rank, stride=bsize, ulen=bsize, nblocks=my)
+        crc.dev_fill_range(buf, SEED, lo, my, stride=bsize, ulen=bsize)
         kw = dict(stride=bsize, ulen=bsize, nblocks=my)
         step_bytes = my * bsize
         block_desc = f"{bsize} B"
+        k = min(my, (512 << 20) // bsize)
+        sample = (slice(0, k * bsize), np.arange(k, dtype=np.uint64) * bsize, np.full(k, bsize, np.uint32))
     out = torch.empty(my, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
-    def step():
-        if kw is None:
-            crc.dev_add_crcs(buf, dst, crc_out=out, stream=stream)
-        elif kw == "unframe":
-            crc.dev_read_blocks(buf, 4096, out=dst, bad_bitmap=bitmap, first_bad=first_bad, stream=stream)
-        else:
-            crc.dev_crc32_blocks(buf, out, stream=stream, **kw)
+    def make_step(b, o, kw_):
+        def step():
+            if kw_ is None:
+                crc.dev_add_crcs(b, dst, crc_out=o, stream=stream)
+            elif kw_ == "unframe":
+                crc.dev_read_blocks(b, 4096, out=dst, crc_out=o, bad_bitmap=bitmap, first_bad=first_bad,
+                                    stream=stream)
+            else:
+                crc.dev_crc32_blocks(b, o, stream=stream, **kw_)
+        return step
 
-    # Clock settle (untimed): memory-bound launches of ~1 ms right after the fill
-    # run below the sustained clock; issue launches for >= args.settle seconds
-    # before the W warmup steps (MI355X_MICROARCH.md "DVFS give-back").
-    t_settle = time.perf_counter()
-    while time.perf_counter() - t_settle < args.settle:
-        for _ in range(8):
+    def timed(step, steps, warmup, barrier):
+        """Clock settle + warmup (untimed), then `steps` launches bracketed by a
+        barrier + synchronize on both sides; per-launch HIP events on the
+        launch stream.  Returns (wall seconds, mean launch seconds)."""
+        # memory-bound launches of ~1 ms right after the fill run below the
+        # sustained clock (MI355X_MICROARCH.md "DVFS give-back")
+        t_settle = time.perf_counter()
+        while time.perf_counter() - t_settle < args.settle:
+            for _ in range(8):
+                step()
+            torch.cuda.synchronize()
+        for _ in range(warmup):
             step()
         torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if barrier:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record(stream)
+            step()
+            ev[i][1].record(stream)
+        torch.cuda.synchronize()
+        if barrier:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        kern_ms = [a.elapsed_time(b) for a, b in ev]
+        return dt, sum(kern_ms) / len(kern_ms) / 1e3
+
+    step = make_step(buf, out, kw)
+    dt, mean_kern_s = timed(step, args.steps, args.warmup, world > 1)
     info = crc.last_launch()
 
-    # per-launch HIP events on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    mean_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
-
-    # max-over-ranks clock, summed bytes (RCCL all-reduce of 3 scalars, after the timed region)
+    # max-over-ranks clock, summed bytes (all-reduce of 3 scalars, after the timed region)
     dt, mean_kern_s, all_bytes = shard.job_timing(dt, mean_kern_s, float(step_bytes), device=dev)
     job_bytes = all_bytes * args.steps
 
@@ -324,6 +413,39 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+
+    # CRC words to rank 0 (RCCL all-gather of 4 B per block), then the same
+    # global batch on ONE GPU for the strong-scaling speedup and a word check
+    multi = None
+    if world > 1:
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        gathered = shard.gather_crcs(out, counts)
+        gather_s = time.perf_counter() - tg
+        ref1 = args.ref1 == "on" or (args.ref1 == "auto" and scaling == "strong")
+        if rank == 0:
+            multi = {"gathered_words": int(gathered.numel()), "gather_ms": round(gather_s * 1e3, 3)}
+            if ref1 and isinstance(kw, dict) and "stride" in kw and scaling == "strong":
+                del step, buf, out  # the shard (the step closure holds it too)
+                torch.cuda.empty_cache()
+                full = torch.empty(total_blocks * bsize, dtype=torch.uint8, device=dev)
+                crc.dev_fill_range(full, SEED, 0, total_blocks, stride=bsize, ulen=bsize)
+                outf = torch.empty(total_blocks, dtype=torch.int32, device=dev)
+                t1, k1 = timed(make_step(full, outf, dict(stride=bsize, ulen=bsize, nblocks=total_blocks)),
+                               args.steps, args.warmup, False)
+                same = bool(torch.equal(gathered.to(dev), outf))
+                multi.update({
+                    "ref_1gpu_ms_per_step": round(t1 / args.steps * 1e3, 4),
+                    "ref_1gpu_gib_s": round(total_blocks * bsize * args.steps / t1 / 2**30, 2),
+                    "speedup_vs_1gpu": round((t1 / args.steps) / (dt / args.steps), 3),
+                    "words_match_1gpu": same,
+                    "words_check": f"all {total_blocks} gathered CRC words == rank 0's 1-GPU run of the same "
+                                   f"global batch",
+                })
+                del full, outf
+                if not same:
+                    print("[bench] gathered CRC words differ from the 1-GPU run", file=sys.stderr)
+        dist.barrier()
 
     if rank == 0:
         gib_s = job_bytes / dt / 2**30
@@ -337,12 +459,15 @@ def main():
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
         cpu = None
-        if world == 1 and args.cpu_seconds > 0 and bsize in ("frame", "unframe"):
-            cpu = cpu_baseline_framing(bsize, buf, args.cpu_seconds)
-        elif world == 1 and args.cpu_seconds > 0 and bsize not in ("mixed", "offlen4k"):
-            sample_blocks = min(my, (512 << 20) // bsize)
-            host = buf[: sample_blocks * bsize].cpu().numpy()
-            cpu = cpu_baseline(host, bsize, args.cpu_threads, args.cpu_seconds)
+        if world == 1 and args.cpu_seconds > 0:
+            if bsize in ("frame", "unframe"):
+                cpu = cpu_baseline_framing(bsize, buf, args.cpu_threads, args.cpu_seconds)
+            elif sample is not None:
+                sl, soff, slen = sample
+                host = buf[sl].cpu().numpy()
+                cpu = cpu_baseline(host, soff, slen, args.cpu_threads, args.cpu_seconds,
+                                   f"{args.workload} ({block_desc})",
+                                   gpu_words=out[: len(soff)].cpu().numpy().view(np.uint32))
         res = {
             "metric": "GiB/s CRC32 over device-resident batched 4/8/16 KB blocks; % HBM peak",
             "value": round(gib_s, 2),
@@ -355,13 +480,19 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (splitmix64 keyed by block index, generated in HBM)",
-            "config": {"workload": args.workload, "blocks_per_gpu": my, "block_bytes": block_desc,
-                       "bytes_per_gpu_step": step_bytes, "parallelism": f"shard-by-block-index x{world}",
+            "data": "synthetic (splitmix64 keyed by global block index, generated in HBM)",
+            "config": {"workload": args.workload, "blocks_total": total_blocks, "blocks_per_gpu": my,
+                       "block_bytes": block_desc, "bytes_per_gpu_step": step_bytes,
+                       "parallelism": f"shard-by-block-index x{world}",
+                       "dist_backend": backend if world > 1 else None,
                        "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if multi is not None:
+            res["multi_gpu"] = multi
+            if "speedup_vs_1gpu" in multi:
+                res["speedup_vs_1gpu"] = multi["speedup_vs_1gpu"]
         line = json.dumps(res)
         print(line, flush=True)
         if args.json_out:

@@ -113,6 +113,8 @@ def _lib():
             "hc_dev_fill_range": (I, [I, P, P, P, U64, U32, U64, U64, U64, P]),
             "hc_dev_add_crcs": (I, [I, P, U64, P, P, P]),
             "hc_read_from_disk": (I, [P, U64, U32, U64, U64, P, P, P]),
+            "hc_read_from_disk_v": (I, [P, U64, U32, U64, U64, P, P, P, P, P]),
+            "hc_read_blocks_touched": (U64, [U32, U64, U64]),
             "hc_dev_read_blocks": (I, [I, P, U64, U32, P, P, P, P, P]),
             "hc_wal_replay": (I, [P, U64, U32, U64, U64, U64, P, U64, P, P, U64, P, P, P, P]),
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
@@ -227,20 +229,30 @@ def FixLastBlockCRC(data) -> Optional[CRCError]:
     return _err(_lib().hc_fix_last_block(p if n else None, n))
 
 
-def ReadFromDisk(blocks, block_size: int, start_offset: int, size: int):
+def ReadFromDisk(blocks, block_size: int, start_offset: int, size: int, verified=None):
     """lsm/block_manager/block_manager.go:189-242 minus the file I/O (row f1).
 
     `blocks`: the blocks from index start_offset // block_size on, as read (bytes
-    past its end read as zeros).  Every touched block is verified in one batch.
+    past its end read as zeros).  Every touched block is verified in one batch,
+    except those whose bit is set in `verified` (uint32 numpy array of
+    ceil(read_blocks_touched()/32) words: the block cache's verified bits); on
+    return `verified` also holds the blocks this call verified clean.
     Returns (payload, final_offset, None) or (None, 0, CRCError) like the Go
-    method; `last_bad_block()` gives the failing block's relative index."""
-    global _LAST_BAD
+    method; `last_bad_block()` gives the failing block's relative index and
+    `last_hashed()` how many blocks were hashed."""
+    global _LAST_BAD, _LAST_HASHED
     p, n, _k = _ro_ptr(blocks)
     out = ctypes.create_string_buffer(max(1, size))
-    fo, bad = ctypes.c_uint64(0), ctypes.c_int64(-1)
-    rc = _lib().hc_read_from_disk(p if n else None, n, block_size, start_offset, size, out,
-                                  ctypes.byref(fo), ctypes.byref(bad))
+    fo, bad, hashed = ctypes.c_uint64(0), ctypes.c_int64(-1), ctypes.c_uint64(0)
+    if verified is not None:
+        k = read_blocks_touched(block_size, start_offset, size)
+        if not (isinstance(verified, np.ndarray) and verified.dtype == np.uint32 and verified.size >= (k + 31) // 32):
+            raise ValueError(f"verified: uint32 array of >= {(k + 31) // 32} words")
+    vp = None if verified is None else verified.ctypes.data
+    rc = _lib().hc_read_from_disk_v(p if n else None, n, block_size, start_offset, size, vp, out,
+                                    ctypes.byref(fo), ctypes.byref(bad), ctypes.byref(hashed))
     _LAST_BAD = bad.value
+    _LAST_HASHED = hashed.value
     if rc < 0:
         raise HundCRCError(rc, "ReadFromDisk")
     if rc != HC_OK:
@@ -249,10 +261,21 @@ def ReadFromDisk(blocks, block_size: int, start_offset: int, size: int):
 
 
 _LAST_BAD = -1
+_LAST_HASHED = 0
 
 
 def last_bad_block() -> int:
     return _LAST_BAD
+
+
+def last_hashed() -> int:
+    """Blocks whose CRC the last ReadFromDisk computed (masked ones excluded)."""
+    return _LAST_HASHED
+
+
+def read_blocks_touched(block_size: int, start_offset: int, size: int) -> int:
+    """Blocks the ReadFromDisk loop touches (block_manager.go:195-235)."""
+    return int(_lib().hc_read_blocks_touched(block_size, start_offset, size))
 
 
 def wal_replay(blocks, block_size: int = BLOCK_SIZE, start_block: int = 0, start_offset: int = CRC_SIZE,

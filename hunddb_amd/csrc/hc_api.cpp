@@ -778,55 +778,94 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
                   bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes);
 }
 
-int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
-                      uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block) {
+uint64_t hc_read_blocks_touched(uint32_t block_size, uint64_t start_offset, uint64_t size) {
+  const uint64_t B = block_size;
+  if (B <= HC_CRC_SIZE || size == 0) return 0;
+  uint64_t boff = start_offset % B;
+  if (boff < HC_CRC_SIZE) boff = HC_CRC_SIZE;  // block_manager.go:198-201
+  const uint64_t first = B - boff;              // payload bytes of the first block
+  return size <= first ? 1 : 1 + (size - first + (B - 5)) / (B - 4);
+}
+
+int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                        uint64_t size, uint32_t *verified, uint8_t *out, uint64_t *final_offset, int64_t *bad_block,
+                        uint64_t *hashed) {
   if (bad_block) *bad_block = -1;
+  if (hashed) *hashed = 0;
   const uint64_t B = block_size;
   if (B <= HC_CRC_SIZE || (size && !out) || (avail && !blocks)) return HC_E_ARG;
   uint64_t boff = start_offset % B;
   if (boff < HC_CRC_SIZE) boff = HC_CRC_SIZE;  // block_manager.go:198-201
   // blocks touched by the loop at :207-235
-  const uint64_t first = B - boff;
-  const uint64_t k = size == 0 ? 0 : (size <= first ? 1 : 1 + (size - first + (B - 5)) / (B - 4));
-  // verify all k blocks in one batch (a9); the first failing block in order is
-  // the one the Go loop stops at
+  const uint64_t k = hc_read_blocks_touched(block_size, start_offset, size);
+  auto known_good = [&](uint64_t i) { return verified && ((verified[i >> 5] >> (i & 31)) & 1u); };
+  auto mark = [&](uint64_t i) {
+    if (verified) verified[i >> 5] |= 1u << (i & 31);
+  };
+  // Verify every touched block the caller has not already verified (its cache's
+  // verified bit, lru_cache.go:51-65 entries filled by ReadBlock :91-97) in ONE
+  // batch (a9); the first failing block in order is the one the Go loop stops at.
   const uint64_t nfull = std::min<uint64_t>(k, avail / B);
+  std::vector<uint64_t> todo;
+  todo.reserve(nfull);
+  for (uint64_t i = 0; i < nfull; i++)
+    if (!known_good(i)) todo.push_back(i);
   int64_t bad = -1;
-  int code = HC_OK;
   static const uint64_t gpu_min = (uint64_t)env_int("HC_READ_GPU_MIN_BLOCKS", 256);
-  if (nfull >= gpu_min || (force_gpu() && nfull > 0 && B <= 0xFFFFFFFFu)) {
-    std::vector<uint32_t> crc(nfull);
-    int rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nfull, crc.data(), 0);
+  const uint64_t nt = todo.size();
+  std::vector<uint8_t> ok(nt, 0);
+  if (nt && (nt >= gpu_min || force_gpu()) && B <= 0xFFFFFFFFu) {
+    std::vector<uint32_t> crc(nt);
+    int rc;
+    if (nt == nfull) {  // nothing masked: one uniform batch
+      rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nt, crc.data(), 0);
+    } else {
+      std::vector<uint64_t> off(nt);
+      std::vector<uint32_t> len(nt, (uint32_t)B);
+      for (uint64_t j = 0; j < nt; j++) off[j] = todo[j] * B;
+      rc = host_batch(blocks, off.data(), len.data(), 0, 0, nt, crc.data(), 0);
+    }
     if (rc != HC_OK) return rc;
-    for (uint64_t i = 0; i < nfull && bad < 0; i++) {
+    for (uint64_t j = 0; j < nt; j++) {
       uint32_t stored;
-      std::memcpy(&stored, blocks + i * B, 4);
-      if (stored != crc[i]) bad = (int64_t)i;
+      std::memcpy(&stored, blocks + todo[j] * B, 4);
+      ok[j] = stored == crc[j];
     }
   } else {
-    for (uint64_t i = 0; i < nfull && bad < 0; i++) {
+    for (uint64_t j = 0; j < nt; j++) {
+      const uint8_t *blk = blocks + todo[j] * B;
       uint32_t stored;
-      std::memcpy(&stored, blocks + i * B, 4);
-      if (stored != hc::cpu_crc32_update(0, blocks + i * B + HC_CRC_SIZE, B - HC_CRC_SIZE)) bad = (int64_t)i;
+      std::memcpy(&stored, blk, 4);
+      ok[j] = stored == hc::cpu_crc32_update(0, blk + HC_CRC_SIZE, B - HC_CRC_SIZE);
     }
   }
+  for (uint64_t j = 0; j < nt; j++) {
+    if (ok[j]) {
+      mark(todo[j]);
+    } else if (bad < 0) {
+      bad = (int64_t)todo[j];
+    }
+  }
+  uint64_t nhashed = nt;
   std::vector<uint8_t> tailbuf;
   if (bad < 0 && nfull < k) {
     // blocks past `avail`: ReadBlock returns a zero-extended short read (:130-146)
     tailbuf.assign(B, 0);
     for (uint64_t i = nfull; i < k && bad < 0; i++) {
+      if (known_good(i)) continue;
       std::fill(tailbuf.begin(), tailbuf.end(), 0);
       const uint64_t o = i * B;
       if (o < avail) std::memcpy(tailbuf.data(), blocks + o, std::min<uint64_t>(B, avail - o));
       uint32_t stored;
       std::memcpy(&stored, tailbuf.data(), 4);
+      nhashed++;
       if (stored != hc::cpu_crc32_update(0, tailbuf.data() + HC_CRC_SIZE, B - HC_CRC_SIZE)) bad = (int64_t)i;
     }
   }
+  if (hashed) *hashed = nhashed;
   if (bad >= 0) {
-    code = HC_ERR_CRC_MISMATCH;
     if (bad_block) *bad_block = bad;
-    return code;
+    return HC_ERR_CRC_MISMATCH;
   }
   // append blockData[blockOffset : blockOffset+bytesToRead] per block (:221-231)
   uint64_t produced = 0, rem = size;
@@ -843,6 +882,12 @@ int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size
   }
   if (final_offset) *final_offset = hc_size_after_crcs(hc_size_without_crcs(start_offset) + size);  // :237-239
   return HC_OK;
+}
+
+int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                      uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block) {
+  return hc_read_from_disk_v(blocks, avail, block_size, start_offset, size, nullptr, out, final_offset, bad_block,
+                             nullptr);
 }
 
 int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t *crc_out, void *stream) {

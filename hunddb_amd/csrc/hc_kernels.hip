@@ -28,6 +28,7 @@
 #include <cstdint>
 
 #include "hc_kernels.hpp"
+#include "hc_util.hpp"
 
 namespace hc {
 
@@ -629,8 +630,7 @@ template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ lens, uint64_t stride,
                                                          uint32_t ulen, uint32_t flags, uint64_t nblocks,
-                                                         uint32_t lg_chunk, uint32_t rot,
-                                                         uint32_t *__restrict__ crc_out,
+                                                         uint32_t lg_chunk, uint32_t *__restrict__ crc_out,
                                                          uint32_t *__restrict__ bad_bitmap,
                                                          unsigned long long *__restrict__ first_bad,
                                                          const DeviceTables *__restrict__ tables) {
@@ -679,12 +679,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   const uint32_t wave = uni(tid >> 6);
   const uint64_t G = gridDim.x, wg = blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
-  // k-th block of this workgroup's sequence; rot staggers where each
-  // workgroup enters its chunks (rot = 0: in order)
-  const uint32_t rotw = (uint32_t)wg * rot;
-  auto blk_of = [&](uint32_t k) -> uint64_t {
-    return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | ((k + rotw) & cmask);
-  };
+  // k-th block of this workgroup's sequence, increasing in k: the first one
+  // past the batch ends the wave (a per-workgroup rotation inside the chunks
+  // was measured -- no gain -- and would break that rule on a partial chunk)
+  auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
   const bool msg = (flags & kFlagMessages) != 0;
 
   // metadata -> (group pointer, group count, skip)
@@ -830,8 +828,8 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
         const bool bad = uni(stored) != crc;
         if (first_bad && bad) {
           if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
-          // one atomic per wave in practice: a wave's later bad blocks can only
-          // lower first_bad when they come before its earlier ones (rotated chunks)
+          // blocks arrive in increasing order: one atomic per wave (a batch of
+          // all-bad blocks would otherwise serialise every wave on one word)
           if (b < reported) lane0_atomic_umin64(first_bad, b);
           reported = b < reported ? b : reported;
         }
@@ -1194,6 +1192,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 // of 2^lg_chunk consecutive blocks c*G + g and its waves take them one at a
 // time from an LDS counter (tools/kcopy2: a persistent read+write stream went
 // from 5.0-5.5 TB/s with static deals to 5.9 TB/s this way).
+// kDepth: interior blocks in flight per wave (2: one prefetched while one is
+// framed; 3: two).  kNull: timing-only build, the CRC replaced by an XOR fold
+// (tools/kframe measures the memory pattern alone).
+template <int kDepth = 2, bool kNull = false>
 __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
                                                          uint8_t *__restrict__ dst, uint64_t nblk, uint32_t lg_chunk,
                                                          uint32_t *__restrict__ crc_out,
@@ -1201,7 +1203,7 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) s_next = 2 * kFastWaves;
+  if (tid == 0) s_next = kDepth * kFastWaves;
   const uint32_t *tg = &tables->tg[0][0];
   for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
     const uint32_t a = q * 16;
@@ -1339,36 +1341,68 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
       if (r == 0) v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : row_step(cc[k], w[k]);
+      for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : (kNull ? cc[k] ^ w[k] : row_step(cc[k], w[k]));
     }
-    const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
-    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    uint32_t crcv;
+    if constexpr (kNull) {
+      crcv = wave_xor(cc[0] ^ cc[1] ^ cc[2] ^ cc[3]);
+    } else {
+      const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
+      crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    }
     // binary.LittleEndian.PutUint32(block[:4], crc): lane 0's ob is the block start
     lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);
     if (crc_out) lane0_store_u32(crc_out + b, crcv);
   };
-  auto advance = [&]() {  // c <- n1 <- the next hand-out
-    c = n1;
-    n1 = blk_of(uni(knv));
+  auto nextb = [&]() {  // the next hand-out (requested one block earlier)
+    const uint64_t r = blk_of(uni(knv));
     if (lane == 0) knv = atomicAdd(&s_next, 1u);
+    return r;
   };
-  // two register sets, alternating roles (no copies that would wait on the
-  // prefetch); unconditional loads: past the end a wave re-reads its block.
-  // The first block is peeled so that the loop header is entered with the same
-  // VMEM sequence from both edges ([next rows loaded][4 row stores]); a
-  // mismatch there makes the waitcnt pass wait for the stores as well.
-  u32x4 A[4], B[4];
-  load4(c, A);
-  load4(n1 < ni ? n1 : c, B);
-  frame(c, A);
-  while (n1 < ni) {
-    advance();
-    load4(n1 < ni ? n1 : c, A);
-    frame(c, B);
-    if (n1 >= ni) break;
-    advance();
+  // Register sets with rotating roles (no copies that would wait on the
+  // prefetch); unconditional loads: past the end a wave re-reads a block it
+  // holds.  The first block is peeled so that the loop header is entered with
+  // the same VMEM sequence from both edges ([next rows loaded][4 row stores]);
+  // a mismatch there makes the waitcnt pass wait for the stores as well.
+  if constexpr (kDepth == 2) {
+    u32x4 A[4], B[4];
+    load4(c, A);
     load4(n1 < ni ? n1 : c, B);
     frame(c, A);
+    while (n1 < ni) {
+      c = n1;
+      n1 = nextb();
+      load4(n1 < ni ? n1 : c, A);
+      frame(c, B);
+      if (n1 >= ni) break;
+      c = n1;
+      n1 = nextb();
+      load4(n1 < ni ? n1 : c, B);
+      frame(c, A);
+    }
+  } else {
+    // loop invariant: B holds n1, C holds n2, A is free
+    uint64_t n2 = blk_of(2 * kFastWaves + wave);
+    u32x4 A[4], B[4], C[4];
+    load4(c, A);
+    load4(n1 < ni ? n1 : c, B);
+    load4(n2 < ni ? n2 : c, C);
+    frame(c, A);
+    while (n1 < ni) {
+      const uint64_t n3 = nextb();
+      load4(n3 < ni ? n3 : n1, A);
+      frame(n1, B);
+      if (n2 >= ni) break;
+      const uint64_t n4 = nextb();
+      load4(n4 < ni ? n4 : n2, B);
+      frame(n2, C);
+      if (n3 >= ni) break;
+      const uint64_t n5 = nextb();
+      load4(n5 < ni ? n5 : n3, C);
+      frame(n3, A);
+      n1 = n4;
+      n2 = n5;
+    }
   }
 }
 
@@ -1383,7 +1417,7 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
 // block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
 // overlapping lane 1's store with identical bytes.
-template <uint32_t lg_groups>
+template <uint32_t lg_groups, int kDepth = 2, bool kNull = false>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                            uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
@@ -1393,7 +1427,7 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) s_next = 2 * kFastWaves;
+  if (tid == 0) s_next = 2 * kFastWaves;  // two hand-outs per wave before the counter
   const uint32_t *tg = &tables->tg[0][0];
   for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
     const uint32_t a = q * 16;
@@ -1470,11 +1504,17 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
       }
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = (r == 0 && g == 0) ? w[k] : row_step(c[k], w[k]);
+      for (int k = 0; k < 4; k++)
+        c[k] = (r == 0 && g == 0) ? w[k] : (kNull ? c[k] ^ w[k] : row_step(c[k], w[k]));
     }
     if (g == gmask) {
-      const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-      const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      uint32_t crcv;
+      if constexpr (kNull) {
+        crcv = wave_xor(c[0] ^ c[1] ^ c[2] ^ c[3]);
+      } else {
+        const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+        crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      }
       if (crc_out) lane0_store_u32(crc_out + b, crcv);
       if (first_bad && crcv != stored) {  // wave-uniform
         if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
@@ -1503,28 +1543,57 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
   };
   // first group peeled: both edges into the loop header carry the same VMEM
   // sequence (see k_frame); past the end a wave re-reads its current group
-  u32x4 A[4], Bv[4];
+  auto pnext = [&](uint64_t fallback, bool &valid) {  // the producer's next group (or fallback)
+    padv();
+    valid = pv;
+    return pv ? (pb << lg_groups) + pg : fallback;
+  };
   uint64_t p = bstart << lg_groups;
-  load4(p, A);
-  padv();
-  uint64_t q = pv ? (pb << lg_groups) + pg : p;
-  bool qv = pv;
-  load4(q, Bv);
-  group(p, A);
-  while (qv) {
-    p = q;
-    padv();
-    q = pv ? (pb << lg_groups) + pg : p;
-    qv = pv;
-    load4(q, A);
-    group(p, Bv);
-    if (!qv) break;
-    p = q;
-    padv();
-    q = pv ? (pb << lg_groups) + pg : p;
-    qv = pv;
+  if constexpr (kDepth == 2) {
+    u32x4 A[4], Bv[4];
+    load4(p, A);
+    bool qv;
+    uint64_t q = pnext(p, qv);
     load4(q, Bv);
     group(p, A);
+    while (qv) {
+      p = q;
+      q = pnext(p, qv);
+      load4(q, A);
+      group(p, Bv);
+      if (!qv) break;
+      p = q;
+      q = pnext(p, qv);
+      load4(q, Bv);
+      group(p, A);
+    }
+  } else {
+    // loop invariant: Bv holds group q1, C holds q2, A is free
+    u32x4 A[4], Bv[4], C[4];
+    load4(p, A);
+    bool v1, v2, v3, v4, v5;
+    uint64_t q1 = pnext(p, v1);
+    load4(q1, Bv);
+    uint64_t q2 = pnext(p, v2);
+    load4(q2, C);
+    group(p, A);
+    while (v1) {
+      const uint64_t q3 = pnext(q1, v3);
+      load4(q3, A);
+      group(q1, Bv);
+      if (!v2) break;
+      const uint64_t q4 = pnext(q2, v4);
+      load4(q4, Bv);
+      group(q2, C);
+      if (!v3) break;
+      const uint64_t q5 = pnext(q3, v5);
+      load4(q5, C);
+      group(q3, A);
+      q1 = q4;
+      v1 = v4;
+      q2 = q5;
+      v2 = v5;
+    }
   }
 }
 
@@ -1601,22 +1670,29 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
   return hipGetLastError();
 }
 
-uint32_t grp_lg_chunk(uint64_t nblocks, int grid) {
-  // chunks of up to 32 consecutive blocks per workgroup, at least 4 chunks each
-  uint32_t lg = 5;
-  while (lg > 0 && (nblocks >> lg) < (uint64_t)grid * 4) lg--;
+uint32_t grp_lg_chunk(uint64_t nblocks, int grid, uint32_t block_bytes) {
+  // Chunk of C = 2^lg consecutive blocks per workgroup (tools/kbench2 sweeps,
+  // profiles/r2/sweep*: 1M blocks, C = 8 .. 512, four boxes): 8 and 16 KiB
+  // blocks run best at C = 128 (87-88 % of 8 TB/s), 4 KiB blocks at C = 64
+  // (84-85 %), mixed 4/8/16 KiB off/len batches (block_bytes 0) at C = 32-64.
+  // Small batches keep at least 4 chunks per workgroup.  HC_LG_CHUNK overrides
+  // (tuning sweeps only).
+  static const int forced = env_int("HC_LG_CHUNK", -1);
+  uint32_t lg = forced >= 0 ? (uint32_t)forced : (block_bytes >= 8192 ? 7u : 6u);
+  if (forced < 0)
+    while (lg > 0 && (nblocks >> lg) < (uint64_t)grid * 4) lg--;
   return lg;
 }
 
 hipError_t launch_grp(const Batch &b, int grid, hipStream_t s) {
-  const uint32_t lg = grp_lg_chunk(b.nblocks, grid), rot = 0;
+  const uint32_t lg = grp_lg_chunk(b.nblocks, grid, (b.off || b.len) ? 0u : b.ulen);
   if (b.off || b.len)
     hipLaunchKernelGGL((k_crc_grp<true, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
-                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, rot, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,
                        b.tables);
   else
     hipLaunchKernelGGL((k_crc_grp<false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
-                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, rot, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,
                        b.tables);
   return hipGetLastError();
 }
@@ -1626,7 +1702,7 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
   const uint64_t ni = nblk > 2 ? nblk - 2 : 1;
-  hipLaunchKernelGGL(k_frame, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, grp_lg_chunk(ni, grid), crc_out,
+  hipLaunchKernelGGL((k_frame<2>), dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, grp_lg_chunk(ni, grid, 4096), crc_out,
                      tables);
   return hipGetLastError();
 }
@@ -1635,7 +1711,7 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
                           const DeviceTables *tables, int grid, hipStream_t s) {
   if (nblk == 0) return hipSuccess;
-  const uint32_t lgc = grp_lg_chunk(nblk, grid);
+  const uint32_t lgc = grp_lg_chunk(nblk, grid, 4096u << lg_groups);
 #define HC_UNFRAME(L)                                                                                      \
   hipLaunchKernelGGL((k_unframe<L>), dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, lgc, out, crc_out, bad_bitmap, \
                      first_bad, tables)

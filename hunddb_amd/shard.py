@@ -8,6 +8,8 @@ collectives over xGMI; the same code runs on "gloo" for the CPU tests.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -32,7 +34,9 @@ def gather_crcs(local, counts, dst: int = 0, group=None):
     """Gather every rank's CRC words (torch int32 tensor) to `dst`, in rank order.
 
     `counts[r]` = number of blocks of rank r.  Returns the concatenated tensor on
-    `dst` and None elsewhere.  Variable sizes are padded to max(counts).
+    `dst` and None elsewhere.  Variable sizes are padded to max(counts).  RCCL
+    (backend "nccl") all-gathers device tensors over xGMI; gloo gathers host
+    copies (CPU tests, one-GPU rehearsals).
     """
     import torch
     import torch.distributed as dist
@@ -40,9 +44,11 @@ def gather_crcs(local, counts, dst: int = 0, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     m = max(counts)
-    pad = torch.zeros(m, dtype=local.dtype, device=local.device)
-    pad[: local.numel()] = local
-    if dist.get_backend(group) == "nccl":
+    nccl = dist.get_backend(group) == "nccl"
+    dev = local.device if nccl else torch.device("cpu")
+    pad = torch.zeros(m, dtype=local.dtype, device=dev)
+    pad[: local.numel()] = local.to(dev)
+    if nccl:
         bufs = [torch.empty_like(pad) for _ in range(world)]
         dist.all_gather(bufs, pad, group=group)
     else:
@@ -51,6 +57,53 @@ def gather_crcs(local, counts, dst: int = 0, group=None):
     if rank != dst:
         return None
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(cmd, nproc: int, port: int = 0, env=None, timeout=None) -> int:
+    """Start `nproc` copies of `cmd` (argv list), one per GPU, with the
+    torch.distributed.run environment (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for them.
+
+    The caller must not have touched the GPU (children are started with
+    subprocess, never by exec).  If a rank fails, the others are terminated.
+    Returns 0, or the first non-zero exit status."""
+    import subprocess
+    import time
+
+    port = port or free_port()
+    base = dict(os.environ if env is None else env)
+    procs = []
+    for r in range(nproc):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=e))
+    t0, rc = time.monotonic(), 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        if timeout is not None and time.monotonic() - t0 > timeout and live:
+            for q in live:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    return rc
 
 
 def job_timing(wall_s: float, kernel_s: float, local_bytes: float, device=None, group=None):

@@ -136,6 +136,20 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
  * `blocks`) of the first failing block -- the one the Go loop would stop at. */
 int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
                       uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block);
+/* Number of blocks ReadFromDisk(start_offset, size) touches (the loop of
+ * block_manager.go:203-235 with its CRC-field skip at :195-197). */
+uint64_t hc_read_blocks_touched(uint32_t block_size, uint64_t start_offset, uint64_t size);
+/* hc_read_from_disk with the block cache's verified bits (row f1): `verified`
+ * (optional; ceil(k/32) words, k = hc_read_blocks_touched, bit i = block i
+ * relative to `blocks`) marks blocks the caller already verified -- an LRU
+ * cache entry that was checked when it was read from disk or written by the
+ * engine (BlockManager.ReadBlock, block_manager.go:72-98; lru_cache.go:20-65)
+ * -- and they are NOT hashed again.  On return the bits of every block that
+ * this call verified clean are set too, so the cache can record them.
+ * *hashed (optional) = blocks whose CRC this call computed. */
+int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
+                        uint64_t size, uint32_t *verified, uint8_t *out, uint64_t *final_offset, int64_t *bad_block,
+                        uint64_t *hashed);
 
 /* WAL recovery (lsm/wal/wal.go:362-455 recoverMemtable + processBlockForRecovery,
  * row f3) over nblocks written WAL blocks of block_size bytes (every log's

@@ -143,13 +143,22 @@ struct ReadResult {
   uint64_t finalOffset = 0;
   Error err;
 };
+// `verified` (optional, ceil(ReadBlocksTouched/32) words): the block cache's
+// verified bits -- set bits are not hashed again; on return the blocks this
+// call verified clean are set as well (hc_read_from_disk_v).
+inline uint64_t ReadBlocksTouched(uint32_t blockSize, uint64_t startOffset, uint64_t size) {
+  return hc_read_blocks_touched(blockSize, startOffset, size);
+}
 inline ReadResult ReadFromDisk(ConstBytes blocks, uint32_t blockSize, uint64_t startOffset, uint64_t size,
-                               int64_t *badBlock = nullptr) {
+                               int64_t *badBlock = nullptr, std::vector<uint32_t> *verified = nullptr,
+                               uint64_t *hashed = nullptr) {
   ReadResult r;
   r.data.resize(size);
   int64_t bad = -1;
-  r.err = check(hc_read_from_disk(blocks.data(), blocks.size(), blockSize, startOffset, size, r.data.data(),
-                                  &r.finalOffset, &bad),
+  if (verified) verified->resize((ReadBlocksTouched(blockSize, startOffset, size) + 31) / 32, 0u);
+  r.err = check(hc_read_from_disk_v(blocks.data(), blocks.size(), blockSize, startOffset, size,
+                                    verified ? verified->data() : nullptr, r.data.data(), &r.finalOffset, &bad,
+                                    hashed),
                 "ReadFromDisk");
   if (badBlock) *badBlock = bad;
   if (r.err) {

@@ -19,6 +19,18 @@ import (
 	"unsafe"
 )
 
+// GPUAvailable reports whether a gfx950 device is visible (checked once at
+// init).  The utils/crc drop-ins work without one (single buffers and
+// AddCRCsToData run on the host CPU then); the batched helpers below
+// (CheckBlocksIntegrity, AddCRCToBlocks, ReadVerified*) return an error
+// instead, never a silent CPU fallback.  A deployment that relies on them
+// should check GPUAvailable at startup rather than discover it mid-flush.
+var GPUAvailable bool
+
+func init() {
+	GPUAvailable = C.hc_device_count() > 0
+}
+
 // BLOCK_SIZE keeps the typed-uint64 form and CRC_SIZE the untyped form of
 // crc_util.go:11-12 (CRC_SIZE is used in both int and uint64 contexts).
 const BLOCK_SIZE = 1024 * uint64(4)
@@ -35,10 +47,9 @@ func goErr(rc C.int) error {
 	if rc == C.HC_OK {
 		return nil
 	}
-	if rc < 0 { // library failure (no GPU for a batch, HIP error): never silent
-		panic("hundcrc: " + C.GoString(C.hc_strerror(rc)))
-	}
-	return errors.New(C.GoString(C.hc_strerror(rc))) // exact crc_util.go texts
+	// < 0: a library failure (no GPU for a batch, HIP error) -- an error value,
+	// never a silent fallback; >= 1: the exact crc_util.go texts
+	return errors.New(C.GoString(C.hc_strerror(rc)))
 }
 
 // GetCRC calculates CRC32 checksum over a byte array (crc_util.go:15).
@@ -51,12 +62,18 @@ func AddCRCToBlockData(data []byte) []byte {
 	if len(data) < CRC_SIZE {
 		return data
 	}
-	_ = goErr(C.hc_add_crc_block(ptr(data), C.size_t(len(data))))
+	// cannot fail on the host path; only HC_FORCE_GPU (test mode) reaches the GPU
+	if err := goErr(C.hc_add_crc_block(ptr(data), C.size_t(len(data)))); err != nil {
+		panic("hundcrc: AddCRCToBlockData: " + err.Error())
+	}
 	return data
 }
 
 // AddCRCsToData frames data into BLOCK_SIZE blocks with a CRC each (crc_util.go:41).
-// Multi-hundred-block inputs are CRC'd in one GPU batch.
+// Multi-hundred-block inputs are CRC'd in one GPU batch; on a host without a
+// gfx950 the library CRCs them on the CPU, so this cannot fail there, as the
+// reference cannot.  Only a HIP runtime error on a GPU host remains, and the
+// signature (no error result) leaves a panic as its report.
 func AddCRCsToData(serializedData []byte) []byte {
 	out := make([]byte, int(C.hc_add_crcs_size(C.size_t(len(serializedData)))))
 	if len(out) == 0 {
@@ -64,7 +81,7 @@ func AddCRCsToData(serializedData []byte) []byte {
 	}
 	w := C.hc_add_crcs(ptr(serializedData), C.size_t(len(serializedData)), ptr(out), C.size_t(len(out)))
 	if w == ^C.size_t(0) {
-		panic("hundcrc: AddCRCsToData failed")
+		panic("hundcrc: AddCRCsToData: GPU batch failed")
 	}
 	return out
 }
@@ -105,9 +122,9 @@ func CheckBlocksIntegrity(data []byte, blockSize int) (int, error) {
 
 // AddCRCToBlocks stamps every blockSize-byte block of data in one GPU batch
 // (flushBlock over a run of WAL blocks, wal.go:260-271).
-func AddCRCToBlocks(data []byte, blockSize int) {
+func AddCRCToBlocks(data []byte, blockSize int) error {
 	n := len(data) / blockSize
-	_ = goErr(C.hc_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize), C.uint64_t(n)))
+	return goErr(C.hc_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize), C.uint64_t(n)))
 }
 
 // ReadVerified is BlockManager.ReadFromDisk (block_manager.go:189-242) minus
@@ -121,6 +138,44 @@ func ReadVerified(raw []byte, blockSize uint16, startOffset, size uint64) ([]byt
 	var bad C.int64_t
 	rc := C.hc_read_from_disk(ptr(raw), C.uint64_t(len(raw)), C.uint32_t(blockSize),
 		C.uint64_t(startOffset), C.uint64_t(size), ptr(out), &final, &bad)
+	if err := goErr(rc); err != nil {
+		return nil, 0, err
+	}
+	return out, uint64(final), nil
+}
+
+// ReadBlocksTouched is the number of blocks ReadFromDisk(startOffset, size)
+// touches (block_manager.go:191-235): the length of ReadVerifiedCached's masks.
+func ReadBlocksTouched(blockSize uint16, startOffset, size uint64) int {
+	return int(C.hc_read_blocks_touched(C.uint32_t(blockSize), C.uint64_t(startOffset), C.uint64_t(size)))
+}
+
+// ReadVerifiedCached is ReadVerified with the block cache's verified bits
+// (row f1): verified[i] == true marks block i of raw (relative to
+// startOffset/blockSize) as already checked -- a cache entry verified when it
+// was read from disk or written by the engine -- so it is not hashed again.
+// On return verified[i] is also true for every block this call verified clean,
+// which the caller records in its cache entries.
+func ReadVerifiedCached(raw []byte, blockSize uint16, startOffset, size uint64, verified []bool) ([]byte, uint64, error) {
+	k := ReadBlocksTouched(blockSize, startOffset, size)
+	bits := make([]uint32, (k+31)/32)
+	for i := 0; i < k && i < len(verified); i++ {
+		if verified[i] {
+			bits[i>>5] |= 1 << uint(i&31)
+		}
+	}
+	out := make([]byte, size)
+	var final C.uint64_t
+	var bad C.int64_t
+	var bitsPtr *C.uint32_t
+	if len(bits) > 0 {
+		bitsPtr = (*C.uint32_t)(unsafe.Pointer(&bits[0]))
+	}
+	rc := C.hc_read_from_disk_v(ptr(raw), C.uint64_t(len(raw)), C.uint32_t(blockSize), C.uint64_t(startOffset),
+		C.uint64_t(size), bitsPtr, ptr(out), &final, &bad, nil)
+	for i := 0; i < k && i < len(verified); i++ {
+		verified[i] = bits[i>>5]>>uint(i&31)&1 == 1
+	}
 	if err := goErr(rc); err != nil {
 		return nil, 0, err
 	}

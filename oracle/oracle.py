@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 _DIR = os.path.dirname(os.path.abspath(__file__))
-_PATH = os.path.join(_DIR, "liboracle.so")
+# HC_ORACLE_LIB: load another build (the ASan/UBSan build of `make -C oracle asan`)
+_PATH = os.environ.get("HC_ORACLE_LIB") or os.path.join(_DIR, "liboracle.so")
 _L = None
 
 

@@ -96,6 +96,12 @@ static void cpu_tests() {
   int64_t badb = -2;
   auto rb = crc::ReadFromDisk(badimg, 4096, 0, 5 * 4092, &badb);
   EXPECT(rb.err && rb.err.Error_() == "CRC mismatch in block" && badb == 3 && rb.data.empty());
+  // the block cache's verified bits: block 3 masked (a verified cached copy) is
+  // trusted and not hashed; the other 4 are, and come back marked
+  std::vector<uint32_t> vbits(1, 1u << 3);
+  uint64_t hashed = 0;
+  auto rv = crc::ReadFromDisk(badimg, 4096, 0, 5 * 4092, &badb, &vbits, &hashed);
+  EXPECT(rv.err == nullptr && hashed == 4 && vbits[0] == 0x1Fu && crc::ReadBlocksTouched(4096, 0, 5 * 4092) == 5);
 
   // WalReplay (wal.go:362-455): one FULL record + a 2-fragment record
   std::vector<uint8_t> wal(3 * 4096, 0);

@@ -307,3 +307,63 @@ def test_device_entry_argument_checks(hc):
                            ctypes.byref(pb), ctypes.byref(po), None) == hc.HC_OK
     assert L.hc_wal_replay(None, 5, 4096, 0, 4, 0, None, 0, None, None, 0, ctypes.byref(nrec),
                            ctypes.byref(pb), ctypes.byref(po), None) == hc.HC_E_ARG
+
+
+def _read_mask_case(hc, oracle, n, B, seed):
+    """Stamped image of n blocks with two corrupt blocks; ReadFromDisk with the
+    block cache's verified bits (row f1): masked blocks are trusted and not
+    hashed, unmasked corrupt blocks are caught at their index, and the bits of
+    the blocks verified clean come back set."""
+    rng = np.random.default_rng(seed)
+    raw = rng.integers(0, 256, n * B, dtype=np.uint8)
+    raw.view(np.uint32).reshape(n, B // 4)[:, 0] = oracle.crc32_blocks(raw, stride=B, ulen=B)
+    c1, c2 = n // 8, (5 * n) // 8
+    bad = raw.copy()
+    bad[c1 * B + 100] ^= 1
+    bad[c2 * B + 9] ^= 0x80
+    start, size = 7, (n - 1) * (B - 4)
+    k = hc.read_blocks_touched(B, start, size)
+    assert k == n
+    words = (k + 31) // 32
+    # nothing masked: the first corrupt block stops the read, every block hashed
+    v = np.zeros(words, np.uint32)
+    got, fo, err = hc.ReadFromDisk(bad.tobytes(), B, start, size, verified=v)
+    assert str(err) == "CRC mismatch in block" and hc.last_bad_block() == c1 and hc.last_hashed() == n
+    bits = np.unpackbits(v.view(np.uint8), bitorder="little")[:k]
+    assert bits.sum() == n - 2 and bits[c1] == 0 and bits[c2] == 0  # verified-clean blocks recorded
+    # block c1 masked (the cache holds a verified copy): the read stops at c2
+    v = np.zeros(words, np.uint32)
+    v[c1 >> 5] |= np.uint32(1 << (c1 & 31))
+    got, fo, err = hc.ReadFromDisk(bad.tobytes(), B, start, size, verified=v)
+    assert hc.last_bad_block() == c2 and hc.last_hashed() == n - 1
+    # both masked plus every 3rd block: success, masked blocks not hashed, payload as the oracle's
+    v = np.zeros(words, np.uint32)
+    masked = sorted(set([c1, c2] + list(range(0, n, 3))))
+    for i in masked:
+        v[i >> 5] |= np.uint32(1 << (i & 31))
+    got, fo, err = hc.ReadFromDisk(bad.tobytes(), B, start, size, verified=v)
+    assert err is None and hc.last_hashed() == n - len(masked)
+    fixed = bad.copy()  # the same bytes with the two blocks re-stamped: the oracle accepts them
+    fixed.view(np.uint32).reshape(n, B // 4)[:, 0] = oracle.crc32_blocks(fixed, stride=B, ulen=B)
+    want, wfo, wrc, _ = oracle.read_from_disk(fixed.tobytes(), B, start, size)
+    assert wrc == 0 and got == want and fo == wfo
+    assert np.unpackbits(v.view(np.uint8), bitorder="little")[:k].sum() == n
+
+
+def test_read_from_disk_verified_mask_host(hc, oracle):
+    for B in (4096, 8192, 1500):
+        _read_mask_case(hc, oracle, 40, B, B)
+
+
+def test_read_blocks_touched_matches_loop(hc):
+    """hc_read_blocks_touched == the iteration count of block_manager.go:203-235."""
+    for B in (1024, 4096, 8192):
+        for start in (0, 1, 3, 4, 5, B - 1, B, B + 4, 3 * B + 77):
+            for size in (0, 1, B - 5, B - 4, B - 3, 2 * B, 10 * B + 3):
+                boff = max(start % B, 4)
+                blocks, rem = 0, size
+                while rem > 0:
+                    rem -= min(rem, B - boff)
+                    blocks += 1
+                    boff = 4
+                assert hc.read_blocks_touched(B, start, size) == blocks, (B, start, size)

@@ -807,3 +807,15 @@ print("ok")
     env = dict(os.environ, HC_CHUNK_MB="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+def test_read_from_disk_verified_mask_gpu_batch(cuda, hc, oracle):
+    """Row f1 with the cache's verified bits at GPU-batch size: the unmasked
+    blocks go to the GPU as one off/len batch, masked ones are not hashed."""
+    import importlib
+    sys_path_tests = os.path.dirname(os.path.abspath(__file__))
+    import sys
+    sys.path.insert(0, sys_path_tests)
+    ta = importlib.import_module("test_abi")
+    for B in (4096, 8192, 5000):
+        ta._read_mask_case(hc, oracle, 3000, B, B + 1)

@@ -103,16 +103,16 @@ int main(int argc, char **argv) {
     b.off = doff;
     b.len = dlen;
   }
-  const uint32_t lg5 = hc::grp_lg_chunk(N, cus);
+  const uint32_t lg5 = 5;
   using namespace hc;
   std::vector<Variant> vs;
   auto add = [&](const char *name, bool check, std::function<void(hipStream_t)> f) {
     vs.push_back(Variant{name, check, f, {}});
   };
-#define GRP(ARR, DYN, NUL, LG, ROT, ...)                                                                                   \
+#define GRP(ARR, DYN, NUL, LG, ...)                                                                                   \
   [&](hipStream_t st) {                                                                                          \
     hipLaunchKernelGGL((k_crc_grp<ARR, DYN, NUL __VA_OPT__(,) __VA_ARGS__>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len,  \
-                       b.stride, b.ulen, b.flags, b.nblocks, (uint32_t)(LG), (uint32_t)(ROT), b.crc_out, b.bad_bitmap, b.first_bad, \
+                       b.stride, b.ulen, b.flags, b.nblocks, (uint32_t)(LG), b.crc_out, b.bad_bitmap, b.first_bad, \
                        b.tables);                                                                                \
   }
   // chunk sweep: HC_SWEEP=1 times k_crc_grp at lg_chunk 3..8 (C = 8 .. 256)
@@ -120,59 +120,53 @@ int main(int argc, char **argv) {
   if (!arrays) {
     add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
     if (sweep) {
-      add("grp pinned C=8", true, GRP(false, true, false, 3, 0, true));
-      add("grp pinned C=16", true, GRP(false, true, false, 4, 0, true));
-      add("grp pinned C=32", true, GRP(false, true, false, 5, 0, true));
-      add("grp pinned C=64", true, GRP(false, true, false, 6, 0, true));
-      add("grp pinned C=128", true, GRP(false, true, false, 7, 0, true));
-      add("grp pinned C=256", true, GRP(false, true, false, 8, 0, true));
-      add("grp pinned C=512", true, GRP(false, true, false, 9, 0, true));
-      add("grp pinned C=32 rot 13", true, GRP(false, true, false, 5, 13, true));
-      add("grp pinned C=64 rot 29", true, GRP(false, true, false, 6, 29, true));
-      add("grp pinned C=128 rot 53", true, GRP(false, true, false, 7, 53, true));
+      add("grp pinned C=8", true, GRP(false, true, false, 3, true));
+      add("grp pinned C=16", true, GRP(false, true, false, 4, true));
+      add("grp pinned C=32", true, GRP(false, true, false, 5, true));
+      add("grp pinned C=64", true, GRP(false, true, false, 6, true));
+      add("grp pinned C=128", true, GRP(false, true, false, 7, true));
+      add("grp pinned C=256", true, GRP(false, true, false, 8, true));
+      add("grp pinned C=512", true, GRP(false, true, false, 9, true));
       add("production launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
     } else {
-      add("grp pinned C=32", true, GRP(false, true, false, 5, 0, true));
-      add("grp pinned C=64", true, GRP(false, true, false, 6, 0, true));
-      add("grp pinned C=128", true, GRP(false, true, false, 7, 0, true));
-      add("grp C=32 (not pinned)", true, GRP(false, true, false, 5, 0));
+      add("grp pinned C=32", true, GRP(false, true, false, 5, true));
+      add("grp pinned C=64", true, GRP(false, true, false, 6, true));
+      add("grp pinned C=128", true, GRP(false, true, false, 7, true));
+      add("grp C=32 (not pinned)", true, GRP(false, true, false, 5));
       add("uni (again)", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
-      add("grp pinned C=32 (again)", true, GRP(false, true, false, 5, 0, true));
-      add("grp pinned C=128 (again)", true, GRP(false, true, false, 7, 0, true));
-      add("NULL grp pinned C=32", false, GRP(false, true, true, 5, 0, true));
+      add("grp pinned C=32 (again)", true, GRP(false, true, false, 5, true));
+      add("grp pinned C=128 (again)", true, GRP(false, true, false, 7, true));
+      add("NULL grp pinned C=32", false, GRP(false, true, true, 5, true));
     }
   } else {
     add("PROD k_crc_fast + k_crc_any(1023)", true, [&](hipStream_t st) {
       launch_fast(b, false, cus, st);
       launch_general(b, 1023, cus, st);
     });
-#define GRPANY(LG, ROT)                        \
+#define GRPANY(LG)                             \
   [&](hipStream_t st) {                     \
-    GRP(true, true, false, LG, ROT, true)(st); \
+    GRP(true, true, false, LG, true)(st);      \
     launch_general(b, 4095, cus, st);       \
   }
     if (sweep) {
-      add("grp pinned C=8 + any(4095)", true, GRPANY(3, 0));
-      add("grp pinned C=16 + any(4095)", true, GRPANY(4, 0));
-      add("grp pinned C=32 + any(4095)", true, GRPANY(5, 0));
-      add("grp pinned C=64 + any(4095)", true, GRPANY(6, 0));
-      add("grp pinned C=128 + any(4095)", true, GRPANY(7, 0));
-      add("grp pinned C=256 + any(4095)", true, GRPANY(8, 0));
-      add("grp pinned C=32 rot 13 + any", true, GRPANY(5, 13));
-      add("grp pinned C=64 rot 29 + any", true, GRPANY(6, 29));
-      add("grp pinned C=128 rot 53 + any", true, GRPANY(7, 53));
+      add("grp pinned C=8 + any(4095)", true, GRPANY(3));
+      add("grp pinned C=16 + any(4095)", true, GRPANY(4));
+      add("grp pinned C=32 + any(4095)", true, GRPANY(5));
+      add("grp pinned C=64 + any(4095)", true, GRPANY(6));
+      add("grp pinned C=128 + any(4095)", true, GRPANY(7));
+      add("grp pinned C=256 + any(4095)", true, GRPANY(8));
       add("production launch_grp + any", true, [&](hipStream_t st) {
         launch_grp(b, cus, st);
         launch_general(b, 4095, cus, st);
       });
     } else {
-      add("grp pinned C=32 + any(4095)", true, GRPANY(5, 0));
-      add("grp pinned C=64 + any(4095)", true, GRPANY(6, 0));
-      add("grp pinned C=128 + any(4095)", true, GRPANY(7, 0));
-      add("grp pinned C=32 alone", true, GRP(true, true, false, 5, 0, true));
-      add("grp pinned C=32 + any (again)", true, GRPANY(5, 0));
+      add("grp pinned C=32 + any(4095)", true, GRPANY(5));
+      add("grp pinned C=64 + any(4095)", true, GRPANY(6));
+      add("grp pinned C=128 + any(4095)", true, GRPANY(7));
+      add("grp pinned C=32 alone", true, GRP(true, true, false, 5, true));
+      add("grp pinned C=32 + any (again)", true, GRPANY(5));
       add("any(4095) sweep alone (early exit)", false, [&](hipStream_t st) { launch_general(b, 4095, cus, st); });
-      add("NULL grp pinned C=32", false, GRP(true, true, true, 5, 0, true));
+      add("NULL grp pinned C=32", false, GRP(true, true, true, 5, true));
     }
   }
 
