@@ -13,12 +13,14 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
 
 #include "../hunddb_amd/csrc/hc_kernels.hip"
+#include "r1_kernels.hip"
 
 #define CK(x)                                                                                \
   do {                                                                                       \
@@ -52,8 +54,16 @@ int main(int argc, char **argv) {
   const uint64_t N = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1000000;
   const int rounds = argc > 3 ? std::atoi(argv[3]) : 8;
   const int launches = argc > 4 ? std::atoi(argv[4]) : 5;
-  const bool arrays = mode == "mixed" || mode == "offlen4k";
+  // general-kernel modes (k_crc_any): msg = config 5b (log-uniform 64 B - 64 KiB
+  // records packed back to back at an odd address, whole-message CRC), eq9815 =
+  // equal 9815-B records, blk4092 = 4092-B blocks in block mode (off/len)
+  const bool general = mode == "msg" || mode == "eq9815" || mode == "blk4092";
+  const bool arrays = mode == "mixed" || mode == "offlen4k" || general;
   const uint32_t B = arrays ? 4096 : (uint32_t)std::atoi(mode.c_str());
+  if (!arrays && (B == 0 || B % 4096 != 0)) {  // never launch a kernel outside its layout contract
+    std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
+    return 2;
+  }
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
@@ -61,13 +71,21 @@ int main(int argc, char **argv) {
   std::vector<uint64_t> ho(N);
   std::vector<uint32_t> hl(N);
   uint64_t total = 0;
+  if (general) total = 1;  // odd start
   for (uint64_t i = 0; i < N; i++) {
     uint32_t l = B;
     if (mode == "mixed") l = 4096u << (uint32_t)(splitmix_h(0x48756E64ull ^ 0x5A5A5A5A5A5A5A5Aull, i, (1u << 21) - 1) % 3);
+    if (mode == "msg") {  // log-uniform in [64, 65536]
+      const double u = (double)(splitmix_h(0x5B, i, 0) >> 11) / 9007199254740992.0;
+      l = (uint32_t)(64.0 * std::exp(u * std::log(1024.0)));
+    }
+    if (mode == "eq9815") l = 9815;
+    if (mode == "blk4092") l = 4092;
     ho[i] = total;
     hl[i] = l;
     total += l;
   }
+  total += 64;
   std::printf("device %s, %d CUs; mode %s: %llu blocks, %.3f GB\n", prop.gcnArchName, cus, mode.c_str(),
               (unsigned long long)N, total / 1e9);
   uint8_t *buf;
@@ -103,6 +121,7 @@ int main(int argc, char **argv) {
     b.off = doff;
     b.len = dlen;
   }
+  if (mode == "msg" || mode == "eq9815") b.flags = hc::kFlagMessages;
   const uint32_t lg5 = 5;
   using namespace hc;
   std::vector<Variant> vs;
@@ -117,7 +136,16 @@ int main(int argc, char **argv) {
   }
   // chunk sweep: HC_SWEEP=1 times k_crc_grp at lg_chunk 3..8 (C = 8 .. 256)
   const bool sweep = std::getenv("HC_SWEEP") != nullptr;
-  if (!arrays) {
+  if (general) {
+    add("r1 k_crc_any static runs", true, [&](hipStream_t st) { launch_general_static(b, 0, cus, st); });
+    add("k_crc_any dyn C=1 window", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 0); });
+    add("k_crc_any dyn C=2 windows", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 1); });
+    add("k_crc_any dyn C=4 windows", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 2); });
+    add("k_crc_any dyn C=16 windows", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 4); });
+    add("r1 static (again)", true, [&](hipStream_t st) { launch_general_static(b, 0, cus, st); });
+    add("PROD launch_general (dyn, 1 window)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
+    add("k_crc_any dyn C=4 (again)", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 2); });
+  } else if (!arrays) {
     add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
     if (sweep) {
       add("grp pinned C=8", true, GRP(false, true, false, 3, true));
@@ -139,9 +167,9 @@ int main(int argc, char **argv) {
       add("NULL grp pinned C=32", false, GRP(false, true, true, 5, true));
     }
   } else {
-    add("PROD k_crc_fast + k_crc_any(1023)", true, [&](hipStream_t st) {
+    add("r1 k_crc_fast + k_crc_any(1023)", true, [&](hipStream_t st) {
       launch_fast(b, false, cus, st);
-      launch_general(b, 1023, cus, st);
+      launch_general_static(b, 1023, cus, st);
     });
 #define GRPANY(LG)                             \
   [&](hipStream_t st) {                     \

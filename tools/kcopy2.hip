@@ -142,6 +142,82 @@ __global__ __launch_bounds__(kWaves * 64) void k_dyncopy(const uint8_t *__restri
   }
 }
 
+// k_dyncopy with the framing kernels' geometry: piece p reads 4 KiB at
+// src + p*sstride + soff and writes it to dst + p*dstride + doff, 16 B per lane
+// with unaligned (byte-aligned) vector loads / stores.  frame: sstride 4092,
+// soff odd, dstride 4096; unframe: sstride 4096, dstride 4092, doff -4.
+template <int kWaves, int kLg, int kLdsKiB>
+__global__ __launch_bounds__(kWaves * 64) void k_dyncopy_u(const uint8_t *__restrict__ src, uint64_t sstride,
+                                                           int64_t soff, uint8_t *__restrict__ dst, uint64_t dstride,
+                                                           int64_t doff, uint64_t npieces, uint32_t *sink) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  __shared__ uint32_t lds_pad[kLdsKiB * 256 + 1];
+  __shared__ uint32_t ctr;
+  if (threadIdx.x == 0) ctr = 2 * kWaves;
+  if (sink[1] == 0xDEADu) lds_pad[threadIdx.x] = 1;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t G = gridDim.x, g = blockIdx.x;
+  auto piece = [&](uint32_t k) -> uint64_t {
+    return (((uint64_t)(k >> kLg) * G + g) << kLg) | (k & ((1u << kLg) - 1u));
+  };
+  uint64_t p = piece(wave), pn = piece(kWaves + wave);
+  if (p >= npieces) return;
+  uint32_t knv = 0;
+  if (lane == 0) knv = atomicAdd(&ctr, 1u);
+  auto load = [&](uint64_t q, u32x4 (&v)[4]) {
+    const uint8_t *S = src + q * sstride + soff + 16 * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * 1024));
+  };
+  auto store = [&](uint64_t q, const u32x4 (&v)[4]) {
+    uint8_t *D = dst + q * dstride + doff + 16 * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) __builtin_nontemporal_store(v[r], reinterpret_cast<u32x4_u *>(D + r * 1024));
+  };
+  u32x4 A[4], B[4];
+  load(p, A);
+  for (;;) {
+    bool vn = pn < npieces;
+    load(vn ? pn : p, B);
+    store(p, A);
+    if (!vn) return;
+    p = pn;
+    pn = piece(__builtin_amdgcn_readfirstlane(knv));
+    if (lane == 0) knv = atomicAdd(&ctr, 1u);
+    vn = pn < npieces;
+    load(vn ? pn : p, A);
+    store(p, B);
+    if (!vn) return;
+    p = pn;
+    pn = piece(__builtin_amdgcn_readfirstlane(knv));
+    if (lane == 0) knv = atomicAdd(&ctr, 1u);
+  }
+}
+
+// non-persistent: one workgroup per kPer pieces (k_copy's "one element per
+// thread" shape with the framing geometry), no LDS
+template <int kPer>
+__global__ __launch_bounds__(256) void k_npcopy_u(const uint8_t *__restrict__ src, uint64_t sstride, int64_t soff,
+                                                  uint8_t *__restrict__ dst, uint64_t dstride, int64_t doff,
+                                                  uint64_t npieces) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t p = (uint64_t)blockIdx.x * 4 * kPer + (uint64_t)k * 4 + wave;
+    if (p >= npieces) return;
+    const uint8_t *S = src + p * sstride + soff + 16 * lane;
+    uint8_t *D = dst + p * dstride + doff + 16 * lane;
+    u32x4 v[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * 1024));
+#pragma unroll
+    for (int r = 0; r < 4; r++) __builtin_nontemporal_store(v[r], reinterpret_cast<u32x4_u *>(D + r * 1024));
+  }
+}
+
 // the same hand-out with static round-robin pieces (piece k of the workgroup
 // sequence to wave k % kWaves): isolates the dynamic part
 template <int kWaves, int kLg, int kLdsKiB, int kLd, int kSt>
@@ -232,6 +308,24 @@ int main(int argc, char **argv) {
   vs.push_back({"dyn copy w16 C=32 2/CU nt/nt", rw, DYN(16, 5, 1, 1, 1, cus * 2), {}});
   vs.push_back({"dyn copy w8 C=32 4/CU nt/nt", rw, DYN(8, 5, 1, 1, 1, cus * 4), {}});
   vs.push_back({"dyn copy w16 C=32 144KiB nt/pl", rw, DYN(16, 5, 144, 1, 0, cus), {}});
+  const uint64_t npu = np - 4;  // leave room for the 4092/4096 stride mismatch
+  const double rwu = 2.0 * npu * 4096;
+#define DYNU(SS, SO, DS, DO)                                                                                       \
+  [=](hipStream_t st) {                                                                                            \
+    hipLaunchKernelGGL((k_dyncopy_u<16, 6, 144>), dim3(cus), dim3(1024), 0, st, a8, (uint64_t)(SS), (int64_t)(SO), b8, \
+                       (uint64_t)(DS), (int64_t)(DO), npu, (uint32_t *)sink);                                      \
+  }
+#define NPU(SS, SO, DS, DO)                                                                                        \
+  [=](hipStream_t st) {                                                                                            \
+    hipLaunchKernelGGL((k_npcopy_u<1>), dim3((unsigned)((npu + 3) / 4)), dim3(256), 0, st, a8, (uint64_t)(SS),     \
+                       (int64_t)(SO), b8, (uint64_t)(DS), (int64_t)(DO), npu);                                     \
+  }
+  vs.push_back({"dyn copy_u aligned 4096/4096", rwu, DYNU(4096, 0, 4096, 0), {}});
+  vs.push_back({"dyn copy_u FRAME src 4092p+1 -> 4096p", rwu, DYNU(4092, 1, 4096, 0), {}});
+  vs.push_back({"dyn copy_u UNFRAME 4096p -> 4092p+12", rwu, DYNU(4096, 0, 4092, 12), {}});
+  vs.push_back({"nonpersist copy_u aligned", rwu, NPU(4096, 0, 4096, 0), {}});
+  vs.push_back({"nonpersist copy_u FRAME", rwu, NPU(4092, 1, 4096, 0), {}});
+  vs.push_back({"nonpersist copy_u UNFRAME", rwu, NPU(4096, 0, 4092, 12), {}});
   vs.push_back({"stat copy w16 C=32 144KiB LDS nt/nt", rw, STAT(16, 5, 144, 1, 1, cus), {}});
   vs.push_back({"stat copy w16 C=1 144KiB LDS nt/nt", rw, STAT(16, 0, 144, 1, 1, cus), {}});
   vs.push_back({"READ only gs U4 pl 8x256/CU", (double)bytes,
