@@ -3,6 +3,11 @@
 // applied per block the way /root/reference/utils/crc/crc_util.go:21-33 (stamp)
 // and :88-100 (verify) apply it.
 //
+// Kernels: k_crc_grp (the dominant streaming kernel: 4 KiB-multiple blocks,
+// uniform or off/len, blocks handed out per CU), k_crc_fast (uniform 1 KiB
+// multiples), k_crc_any (any length / alignment, whole-message CRC), k_frame
+// (fused AddCRCsToData), k_unframe (batched ReadFromDisk), k_fill.  The row
+// arithmetic they share, as in the streaming kernel k_crc_fast:
 // Streaming kernel (k_crc_fast), per wave = one block at a time:
 //   * A block of B bytes is B/1024 rows; row j is read by ONE coalesced
 //     global_load_dwordx4 (lane l gets bytes 1024j+16l .. +15).  No LDS
