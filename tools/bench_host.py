@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--mem", choices=["pinned", "pageable"], default="pinned")
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--blocks", type=int, default=1_000_000)
+    ap.add_argument("--bsize", type=int, default=8192, help="host8k: block bytes")
+    ap.add_argument("--verify", type=int, default=0, help="host8k: hc_verify_blocks instead of hc_crc32_blocks")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--check", type=int, default=1, help="spot-check results against a CPU CRC")
@@ -59,7 +61,8 @@ def main():
     res = {"mode": args.mode, "mem": args.mem}
 
     if args.mode == "host8k":
-        B, n = 8192, args.blocks
+        B, n = args.bsize, args.blocks
+        res.update(bsize=B, blocks=n, verify=args.verify, chunk_mb=int(os.environ.get("HC_CHUNK_MB", "64")))
         host, keep = host_array(n * B, args.mem)
         dev = torch.empty(n * B, dtype=torch.uint8, device="cuda")
         crc.dev_fill_blocks(dev, 0x48756E64, stride=B, ulen=B, nblocks=n)
@@ -74,11 +77,20 @@ def main():
         del dev
         crc.crc32_blocks(host, stride=B, ulen=B, nblocks=min(n, 1000))  # warm the pipeline
         times = []
+        if args.verify:  # stamp the host copy so that every block verifies clean
+            wv = want.view(np.uint8).reshape(n, 4)
+            host.reshape(n, B)[:, :4] = wv
         for _ in range(args.steps):
             t = time.perf_counter()
-            got = crc.crc32_blocks(host, stride=B, ulen=B, nblocks=n)
+            if args.verify:
+                err, bm, fb = crc.verify_blocks(host, stride=B, ulen=B, nblocks=n)
+            else:
+                got = crc.crc32_blocks(host, stride=B, ulen=B, nblocks=n)
             times.append(time.perf_counter() - t)
-        assert np.array_equal(got, want), "host-path CRCs differ from the device-resident path"
+        if args.verify:
+            assert err is None and fb == -1, (err, fb)
+        else:
+            assert np.array_equal(got, want), "host-path CRCs differ from the device-resident path"
         bytes_ = n * B
     elif args.mode == "config5":
         import walgen
