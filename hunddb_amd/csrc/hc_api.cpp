@@ -523,11 +523,14 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
         rc = HC_E_HIP;
         break;
       }
-      // plan the chunk: blocks [i, j) packed at 16-B aligned offsets
+      // plan the chunk: blocks [i, j) packed at 16-B aligned offsets, or back
+      // to back when the source is one contiguous run of equal blocks (then
+      // each gather thread copies one span; unaligned blocks go to k_crc_any)
       bool uniform = true;
+      const bool contig = !off && !len && stride == ulen;
       while (j < n && j - i < maxmsg) {
         const uint32_t l = blk_len(len, ulen, j);
-        const uint64_t need = (pos + l + 15) & ~uint64_t(15);
+        const uint64_t need = contig ? pos + l : (pos + l + 15) & ~uint64_t(15);
         if (need > P.chunk) break;
         s.pin_off[j - i] = pos;
         s.pin_len[j - i] = l;
@@ -543,16 +546,19 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
       const uint64_t nb = j - i;
       // gather into pinned staging on copy_threads threads
       const int th = (int)std::min<uint64_t>((uint64_t)copy_threads, std::max<uint64_t>(1, pos >> 22));
+      // streamed stores into staging (only the DMA engine reads it): neutral for
+      // block batches, +4-10 % for WAL replay, whose record copy-out competes
+      // for host memory bandwidth (profiles/r2/host_gather/)
       parallel_for(th, [&](int t) {
         const uint64_t a = nb * t / th, b = nb * (t + 1) / th;
-        // contiguous source AND contiguous staging (pin_off[k] = k*ulen only when
-        // ulen is a 16-B multiple): one memcpy per thread
-        if (!off && !len && stride == ulen && (ulen & 15u) == 0) {
-          if (b > a) std::memcpy(s.pin + s.pin_off[a], base + (i + a) * stride, (b - a) * (uint64_t)ulen);
+        // contiguous source AND contiguous staging (pin_off[k] = k*ulen): one copy per thread
+        if (contig) {
+          if (b > a) copy_nt(s.pin + s.pin_off[a], base + (i + a) * stride, (b - a) * (uint64_t)ulen);
         } else {
           for (uint64_t k = a; k < b; k++)
-            std::memcpy(s.pin + s.pin_off[k], base + blk_off(off, stride, i + k), s.pin_len[k]);
+            copy_nt(s.pin + s.pin_off[k], base + blk_off(off, stride, i + k), s.pin_len[k]);
         }
+        _mm_sfence();  // streamed staging bytes are visible to the DMA engine
       });
       packed_uniform = uniform && (l0 & 15u) == 0;  // then off = k*l0
       if (hipMemcpyAsync(s.dbuf, s.pin, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
@@ -690,14 +696,18 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
   const size_t out = hc_add_crcs_size(n);
   if (out > dst_cap || (n && (!src || !dst))) return (size_t)-1;
   const size_t nb = out / HC_BLOCK_SIZE;
+  const size_t nfull = n / kPayloadPerBlock;  // blocks whose 4092 payload bytes all come from src
   // framing: zeroed 4096-byte blocks, payload at [4:] (crc_util.go:48-60)
-  for (size_t b = 0; b < nb; b++) {
-    uint8_t *blk = dst + b * HC_BLOCK_SIZE;
-    const size_t s = b * kPayloadPerBlock, e = std::min(n, s + kPayloadPerBlock);
-    std::memset(blk, 0, HC_CRC_SIZE);
-    std::memcpy(blk + HC_CRC_SIZE, src + s, e - s);
-    if (e - s < kPayloadPerBlock) std::memset(blk + HC_CRC_SIZE + (e - s), 0, kPayloadPerBlock - (e - s));
-  }
+  auto frame = [&](size_t a, size_t b) {
+    for (size_t k = a; k < b; k++) {
+      uint8_t *blk = dst + k * HC_BLOCK_SIZE;
+      const size_t s = k * kPayloadPerBlock, e = std::min(n, s + kPayloadPerBlock);
+      std::memset(blk, 0, HC_CRC_SIZE);
+      std::memcpy(blk + HC_CRC_SIZE, src + s, e - s);
+      if (e - s < kPayloadPerBlock) std::memset(blk + HC_CRC_SIZE + (e - s), 0, kPayloadPerBlock - (e - s));
+    }
+  };
+
   // CRCs: one GPU batch for multi-block outputs, host for a single block.
   // AddCRCsToData cannot fail in Go (crc_util.go:41-64), so a host with no
   // gfx950 (HC_E_NODEV) computes the CRCs on the host path below (hc_cpu.cpp,
@@ -706,12 +716,48 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
   static const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", 256);
   bool on_gpu = false;
   if (nb >= gpu_min || (force_gpu() && nb > 0)) {
-    const int rc = host_batch(dst, nullptr, nullptr, HC_BLOCK_SIZE, HC_BLOCK_SIZE, nb, nullptr, 0, nullptr, nullptr, dst);
+    // The CRC of block k is ChecksumIEEE(src[4092k : 4092k+4092]) for every
+    // full block, so the GPU batch reads the SOURCE payload (4092-byte
+    // messages; one span DMA per chunk when src is pinned) while
+    // HC_COPY_THREADS threads frame dst: the two overlap instead of framing
+    // first and reading dst back.  The ragged last block (zero-padded) is
+    // hashed on the host after framing.
+    const int T = std::max(1, env_int("HC_COPY_THREADS", 8));
+    std::vector<uint32_t> crc(nfull);
+    int rc = HC_OK;
+    // (plain stores: streamed framing measured 10-35 % slower, profiles/r2/addcrcs/)
+    parallel_for(T + 1, [&](int t) {
+      if (t < T) {
+        frame(nb * t / T, nb * (t + 1) / T);
+        return;
+      }
+      if (!nfull) return;
+      if (is_pinned(src)) {  // span DMA wants explicit off/len
+        std::vector<uint64_t> o(nfull);
+        std::vector<uint32_t> l(nfull, (uint32_t)kPayloadPerBlock);
+        for (size_t k = 0; k < nfull; k++) o[k] = k * kPayloadPerBlock;
+        rc = host_batch(src, o.data(), l.data(), 0, 0, nfull, crc.data(), kFlagMessages);
+      } else {
+        rc = host_batch(src, nullptr, nullptr, kPayloadPerBlock, (uint32_t)kPayloadPerBlock, nfull, crc.data(),
+                        kFlagMessages);
+      }
+    });
     if (rc == HC_OK) {
+      parallel_for(T, [&](int t) {
+        for (size_t k = nfull * t / T, e = nfull * (t + 1) / T; k < e; k++)
+          std::memcpy(dst + k * HC_BLOCK_SIZE, &crc[k], 4);
+      });
+      for (size_t k = nfull; k < nb; k++) {  // the ragged last block
+        uint8_t *blk = dst + k * HC_BLOCK_SIZE;
+        const uint32_t c = hc::cpu_crc32_update(0, blk + HC_CRC_SIZE, kPayloadPerBlock);
+        std::memcpy(blk, &c, 4);
+      }
       on_gpu = true;
     } else if (rc != HC_E_NODEV || force_gpu()) {
       return (size_t)-1;
     }
+  } else {
+    frame(0, nb);
   }
   if (!on_gpu) {
     for (size_t b = 0; b < nb; b++) {

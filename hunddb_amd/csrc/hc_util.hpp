@@ -1,6 +1,10 @@
 // hc_util.hpp — small host-side helpers shared by the C ABI translation units.
 #pragma once
+#include <emmintrin.h>
+
+#include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -27,6 +31,33 @@ void parallel_for(int threads, F &&fn) {
   for (int t = 1; t < threads; t++) ts.emplace_back([&fn, t] { fn(t); });
   fn(0);
   for (auto &t : ts) t.join();
+}
+
+// Bytes written once and not read back by the CPU (framed output, staging
+// that the DMA engine reads): non-temporal 16-B stores skip the write-allocate
+// read of every destination line.  Weakly ordered: the writing thread issues
+// _mm_sfence() before another thread or the DMA engine reads the bytes.
+inline void copy_nt(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  if (n < 64) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  for (; n >= 64; n -= 64, dst += 64, src += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 48), d);
+  }
+  std::memcpy(dst, src, n);
 }
 
 }  // namespace hc

@@ -146,33 +146,10 @@ bool scan_block(Range &R, const uint8_t *b, uint32_t bs, uint64_t blk, uint64_t 
   return true;
 }
 
-// Record bytes are written once and not read back here: non-temporal 16-B
-// stores skip the write-allocate read of every destination line, which would
-// otherwise compete for host memory bandwidth with the verify batch's DMA of
-// the same image.
-void copy_nt(uint8_t *dst, const uint8_t *src, uint64_t n) {
-  if (n < 64) {
-    std::memcpy(dst, src, n);
-    return;
-  }
-  const uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
-  std::memcpy(dst, src, head);
-  dst += head;
-  src += head;
-  n -= head;
-  for (; n >= 64; n -= 64, dst += 64, src += 64) {
-    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src));
-    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16));
-    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 32));
-    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 48));
-    _mm_stream_si128(reinterpret_cast<__m128i *>(dst), a);
-    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 16), b);
-    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 32), c);
-    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 48), d);
-  }
-  std::memcpy(dst, src, n);
-}
-
+// Record bytes are written once and not read back here: hc::copy_nt's
+// non-temporal stores skip the write-allocate read of every destination line,
+// which would otherwise compete for host memory bandwidth with the verify
+// batch's DMA of the same image.
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }

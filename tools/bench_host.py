@@ -44,7 +44,7 @@ def host_array(nbytes, mem):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["host8k", "config5", "config5b", "replay"], default="host8k")
+    ap.add_argument("--mode", choices=["host8k", "config5", "config5b", "replay", "addcrcs"], default="host8k")
     ap.add_argument("--mem", choices=["pinned", "pageable"], default="pinned")
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--blocks", type=int, default=1_000_000)
@@ -92,6 +92,34 @@ def main():
         else:
             assert np.array_equal(got, want), "host-path CRCs differ from the device-resident path"
         bytes_ = n * B
+    elif args.mode == "addcrcs":
+        # AddCRCsToData (crc_util.go:41-64) over a host payload: --blocks output
+        # blocks, a ragged last one; rate = payload bytes / wall time
+        import ctypes
+        L = crc._lib()
+        n = args.blocks * 4092 - 1000
+        src, keep = host_array(n + 1, args.mem)
+        src = src[1:]  # odd address
+        src[:] = np.arange(n, dtype=np.uint64).astype(np.uint8) ^ 0x5A
+        cap = int(L.hc_add_crcs_size(n))
+        dst = np.empty(cap, dtype=np.uint8)
+        dst[::4096] = 1  # fault the output pages in once, outside the timed region
+        sp, dp = src.ctypes.data, dst.ctypes.data
+        L.hc_add_crcs(sp, 4092 * 300, dp, cap)  # warm
+        times = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            wrote = L.hc_add_crcs(sp, n, dp, cap)
+            times.append(time.perf_counter() - t)
+            assert wrote == cap, wrote
+        rng = np.random.default_rng(3)
+        for b in list(rng.choice(cap // 4096, 300, replace=False)) + [cap // 4096 - 1]:
+            blk = dst[b * 4096:(b + 1) * 4096]
+            assert crc.CheckBlockIntegrity(blk) is None, b
+            pay = src[b * 4092:min(n, (b + 1) * 4092)]
+            assert np.array_equal(blk[4:4 + len(pay)], pay), b
+        res.update(blocks=cap // 4096, payload=n)
+        bytes_ = n
     elif args.mode == "config5":
         import walgen
         t = time.perf_counter()
