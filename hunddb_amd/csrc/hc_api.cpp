@@ -898,6 +898,26 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
   for (uint64_t i = 0; i < nfull; i++)
     if (!known_good(i)) todo.push_back(i);
   int64_t bad = -1;
+  // append blockData[blockOffset : blockOffset+bytesToRead] of blocks [a, b)
+  // (:221-231); block i's output position is known in closed form: the first
+  // block gives B - boff bytes, every later one B - 4, capped at `size`
+  const uint64_t boff0 = boff, first_take = B - boff0;
+  auto produced_before = [&](uint64_t i) -> uint64_t {
+    return i == 0 ? 0 : std::min<uint64_t>(size, first_take + (i - 1) * (B - HC_CRC_SIZE));
+  };
+  auto copy_out = [&](uint64_t a, uint64_t b) {
+    for (uint64_t i = a; i < b; i++) {
+      const uint64_t produced = produced_before(i);
+      const uint64_t bo = i == 0 ? boff0 : HC_CRC_SIZE;
+      const uint64_t take = std::min<uint64_t>(size - produced, B - bo);
+      const uint64_t o = i * B + bo;
+      // bytes past `avail` are zeros
+      const uint64_t have = o >= avail ? 0 : std::min<uint64_t>(take, avail - o);
+      if (have) std::memcpy(out + produced, blocks + o, have);
+      if (have < take) std::memset(out + produced + have, 0, take - have);
+    }
+  };
+  bool copied = false;
   static const uint64_t gpu_min = (uint64_t)env_int("HC_READ_GPU_MIN_BLOCKS", 256);
   const uint64_t nt = todo.size();
   std::vector<uint8_t> ok(nt, 0);
@@ -906,15 +926,25 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
     std::vector<uint32_t> badj((nt + 31) / 32, 0);
     HostVerify hv;
     hv.bitmap = badj.data();
-    int rc;
-    if (nt == nfull) {  // nothing masked: one uniform batch
-      rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nt, nullptr, 0, nullptr, &hv);
-    } else {
-      std::vector<uint64_t> off(nt);
-      std::vector<uint32_t> len(nt, (uint32_t)B);
-      for (uint64_t j = 0; j < nt; j++) off[j] = todo[j] * B;
-      rc = host_batch(blocks, off.data(), len.data(), 0, 0, nt, nullptr, 0, nullptr, &hv);
-    }
+    // the copy-out runs on HC_COPY_THREADS threads while the batch verifies;
+    // on a CRC failure `out` is left unspecified (Go returns no data)
+    const int T = std::max(1, env_int("HC_COPY_THREADS", 8));
+    int rc = HC_OK;
+    parallel_for(T + 1, [&](int t) {
+      if (t < T) {
+        copy_out(k * t / T, k * (t + 1) / T);
+        return;
+      }
+      if (nt == nfull) {  // nothing masked: one uniform batch
+        rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nt, nullptr, 0, nullptr, &hv);
+      } else {
+        std::vector<uint64_t> off(nt);
+        std::vector<uint32_t> len(nt, (uint32_t)B);
+        for (uint64_t j = 0; j < nt; j++) off[j] = todo[j] * B;
+        rc = host_batch(blocks, off.data(), len.data(), 0, 0, nt, nullptr, 0, nullptr, &hv);
+      }
+    });
+    copied = true;
     if (rc != HC_OK) return rc;
     for (uint64_t j = 0; j < nt; j++) ok[j] = !((badj[j >> 5] >> (j & 31)) & 1u);
   } else {
@@ -953,19 +983,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
     if (bad_block) *bad_block = bad;
     return HC_ERR_CRC_MISMATCH;
   }
-  // append blockData[blockOffset : blockOffset+bytesToRead] per block (:221-231)
-  uint64_t produced = 0, rem = size;
-  for (uint64_t i = 0; i < k; i++) {
-    const uint64_t take = std::min<uint64_t>(rem, B - boff);
-    const uint64_t o = i * B + boff;
-    // bytes past `avail` are zeros
-    const uint64_t have = o >= avail ? 0 : std::min<uint64_t>(take, avail - o);
-    if (have) std::memcpy(out + produced, blocks + o, have);
-    if (have < take) std::memset(out + produced + have, 0, take - have);
-    produced += take;
-    rem -= take;
-    boff = HC_CRC_SIZE;
-  }
+  if (!copied) copy_out(0, k);
   if (final_offset) *final_offset = hc_size_after_crcs(hc_size_without_crcs(start_offset) + size);  // :237-239
   return HC_OK;
 }

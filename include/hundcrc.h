@@ -129,11 +129,13 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
  * (row f1): `blocks` holds the blocks from index start_offset/block_size on, as
  * the caller read them (`avail` bytes; past that a block reads as zeros, like
  * readBlockFromDisk's short read).  Every block the loop touches is verified in
- * ONE batch (GPU above HC_READ_GPU_MIN_BLOCKS = 256, host CPU below), then the
- * payload bytes [blockOffset:] of each are copied to out (size bytes), and
- * *final_offset = SizeAfterAddingCRCs(SizeWithoutCRCs(start_offset) + size).
+ * ONE batch (GPU above HC_READ_GPU_MIN_BLOCKS = 256, host CPU below), the
+ * payload bytes [blockOffset:] of each are copied to out (size bytes; with the
+ * GPU batch the copy runs on HC_COPY_THREADS threads while the batch verifies),
+ * and *final_offset = SizeAfterAddingCRCs(SizeWithoutCRCs(start_offset) + size).
  * Returns HC_OK or HC_ERR_CRC_MISMATCH with *bad_block = the index (relative to
- * `blocks`) of the first failing block -- the one the Go loop would stop at. */
+ * `blocks`) of the first failing block -- the one the Go loop would stop at;
+ * then `out` holds unspecified bytes (Go returns no data). */
 int hc_read_from_disk(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,
                       uint64_t size, uint8_t *out, uint64_t *final_offset, int64_t *bad_block);
 /* Number of blocks ReadFromDisk(start_offset, size) touches (the loop of

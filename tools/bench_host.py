@@ -44,7 +44,8 @@ def host_array(nbytes, mem):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["host8k", "config5", "config5b", "replay", "addcrcs"], default="host8k")
+    ap.add_argument("--mode", choices=["host8k", "config5", "config5b", "replay", "addcrcs", "readdisk"],
+                    default="host8k")
     ap.add_argument("--mem", choices=["pinned", "pageable"], default="pinned")
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--blocks", type=int, default=1_000_000)
@@ -120,6 +121,46 @@ def main():
             assert np.array_equal(blk[4:4 + len(pay)], pay), b
         res.update(blocks=cap // 4096, payload=n)
         bytes_ = n
+    elif args.mode == "readdisk":
+        # ReadFromDisk (block_manager.go:189-242 minus the file I/O) over --blocks
+        # stamped 4 KiB blocks from offset 4: verify every touched block, append
+        # each block's payload; rate = block bytes / wall time
+        import ctypes
+        L = crc._lib()
+        B, n = 4096, args.blocks
+        host, keep = host_array(n * B, args.mem)
+        dev = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+        crc.dev_fill_blocks(dev, 0x5EED, stride=B, ulen=B, nblocks=n)
+        words = torch.empty(n, dtype=torch.int32, device="cuda")
+        crc.dev_crc32_blocks(dev, words, stride=B, ulen=B, nblocks=n, flags=crc.HC_F_STAMP)
+        torch.cuda.synchronize()
+        host[:] = dev.cpu().numpy()
+        del dev
+        size = n * (B - 4) - 1000
+        out = np.empty(size, dtype=np.uint8)
+        out[::4096] = 0  # fault the output pages in once, outside the timed region
+        fo, bad, hashed = ctypes.c_uint64(0), ctypes.c_int64(-1), ctypes.c_uint64(0)
+        args_ = (host.ctypes.data, n * B, B, 4, size, None, out.ctypes.data,
+                 ctypes.byref(fo), ctypes.byref(bad), ctypes.byref(hashed))
+        L.hc_read_from_disk_v(host.ctypes.data, 300 * B, B, 4, 300 * (B - 4) - 10, None, out.ctypes.data,
+                              ctypes.byref(fo), ctypes.byref(bad), ctypes.byref(hashed))  # warm
+        times = []
+        for _ in range(args.steps):
+            t = time.perf_counter()
+            rc = L.hc_read_from_disk_v(*args_)
+            times.append(time.perf_counter() - t)
+            assert rc == 0 and bad.value == -1 and hashed.value == n, (rc, bad.value, hashed.value)
+        hv = host.reshape(n, B)
+        for b in list(np.random.default_rng(4).choice(n - 1, 300, replace=False)) + [n - 1]:
+            want = hv[b, 4:] if b < n - 1 else hv[b, 4:4 + size - (n - 1) * (B - 4)]
+            assert np.array_equal(out[b * (B - 4):b * (B - 4) + len(want)], want), b
+        victim = n // 3  # a corrupted block is found at its index
+        host[victim * B + 100] ^= 1
+        rc = L.hc_read_from_disk_v(*args_)
+        host[victim * B + 100] ^= 1
+        assert rc == 2 and bad.value == victim, (rc, bad.value)
+        res.update(blocks=n, payload=size)
+        bytes_ = n * B
     elif args.mode == "config5":
         import walgen
         t = time.perf_counter()
