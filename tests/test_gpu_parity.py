@@ -340,6 +340,53 @@ def test_add_crcs_to_data_gpu(cuda, hc, oracle):
         assert m == len(out) and bytes(out) == want.tobytes()
 
 
+@pytest.mark.parametrize("mem", ["pageable", "pinned"])
+def test_add_crcs_to_data_gpu_sources(cuda, hc, oracle, mem):
+    """hc_add_crcs frames dst on host threads while the GPU hashes the SOURCE
+    payload as 4092-byte messages (span DMA when src is pinned, CPU gather when
+    pageable); the ragged last block is hashed on the host.  Byte-exact vs the
+    oracle's crc_util.go:41-64 restatement: an exact multiple of 4092 (no ragged
+    block), odd source addresses, and 70 MB spanning several staging chunks."""
+    torch = cuda
+    rng = np.random.default_rng(21)
+    for n, shift in [(4092 * 300, 0), (4092 * 777, 3), (4092 * 300 + 4091, 1), (70_000_003, 5)]:
+        if mem == "pinned":
+            t = torch.empty(n + shift, dtype=torch.uint8, pin_memory=True)
+            buf = t.numpy()
+        else:
+            buf = np.empty(n + shift, dtype=np.uint8)
+        src = buf[shift:]
+        src[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        out = hc.AddCRCsToData(src)
+        want = np.zeros(hc.lib().hc_add_crcs_size(n), dtype=np.uint8)
+        m = oracle.lib().oc_add_crcs_to_data(src.tobytes(), n, want.ctypes.data)
+        assert m == len(out) and bytes(out) == want.tobytes(), (mem, n, shift)
+
+
+@pytest.mark.parametrize("B", [4096, 8192, 5000])
+def test_read_from_disk_gpu_copyout_shapes(cuda, hc, oracle, monkeypatch, B):
+    """ReadFromDisk's payload copy-out runs on HC_COPY_THREADS threads while the
+    GPU batch verifies; every block's output position comes from a closed form.
+    Odd start offsets, sizes ending mid-block, images shorter than the touched
+    range (zero-extended blocks), 1 and 3 copy threads, vs the oracle."""
+    rng = np.random.default_rng(B)
+    img = _stamped_blocks(oracle, rng, 1200, B)
+    for threads in ["1", "3"]:
+        monkeypatch.setenv("HC_COPY_THREADS", threads)
+        for start, size, cut in [(0, 1100 * (B - 4) + 333, 0), (7, 1000 * (B - 4), 0), (B + 123, 900 * (B - 4) + 1, 0),
+                                 (4, 1150 * (B - 4), B * 60 + 77)]:
+            view = img[(start // B) * B:].tobytes()
+            if cut:
+                view = view[:len(view) - cut]
+            got, fo, err = hc.ReadFromDisk(view, B, start, size)
+            want, wfo, wrc, wbad = oracle.read_from_disk(view, B, start, size)
+            assert (0 if err is None else err.code) == wrc, (threads, start, size, cut)
+            if wrc == 0:
+                assert got == want and fo == wfo, (threads, start, size, cut)
+            else:
+                assert hc.last_bad_block() == wbad
+
+
 def test_force_gpu_dropins(cuda, hc, golden, monkeypatch):
     monkeypatch.setenv("HC_FORCE_GPU", "1")
     assert hc.GetCRC(b"123456789") == 0xCBF43926
