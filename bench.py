@@ -46,6 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+COPY_CEILING_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy (SURVEY 8(d) asks for both)
 SEED = 0x48756E64
 WORKLOADS = {
     # name: (blocks per rank (weak) or in total (strong), block bytes or kind, scaling)
@@ -62,6 +63,9 @@ WORKLOADS = {
     "unframe": (1_000_000, "unframe", "weak"),
     # config2's blocks described by off/len arrays (the per-block metadata path)
     "offlen4k": (1_000_000, "offlen4k", "weak"),
+    # verify mode (CheckBlockIntegrity over the north-star batch, stamped): read B,
+    # compare, write the 4-B word + bitmap bits; SURVEY 8(d) counts B + 4 per block
+    "verify": (1_000_000, "verify", "weak"),
 }
 KERNEL_RE = {"frame": "k_frame", "unframe": "k_unframe"}  # else the streaming CRC kernel
 
@@ -159,6 +163,20 @@ def _rate(fn, nbytes, seconds):
             return k * nbytes / dt / 2**30
 
 
+def cpu_host():
+    """The host's CPU model and logical CPU count (SURVEY 8(d) asks for both)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
 def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None):
     """Go's crc32.ChecksumIEEE over block[4:len] of every sample block
     (crc_util.go:16,94), three ways: the oracle's restatement of Go's amd64
@@ -196,6 +214,7 @@ def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None):
                         f"same words as the oracle on the first 200 blocks: {zl_ok}"}
     if gpu_words is not None:
         res["matches_gpu"] = bool(np.array_equal(words, gpu_words))
+    res.update(cpu_host())
     return res
 
 
@@ -241,7 +260,7 @@ def cpu_baseline_framing(kind, dev_src, threads, budget_s):
             "sample": f"{what}, read+written bytes",
             "spread": [round(min(slices), 3), round(max(slices), 3)],
             "spread_note": f"min/max of 5 slices of {0.1 * budget_s:.1f} s on {threads} threads",
-            "single_thread": round(one, 3)}
+            "single_thread": round(one, 3), **cpu_host()}
 
 
 # --------------------------------------------------------------------------
@@ -338,6 +357,19 @@ def main(argv=None):
         kw = None
         step_bytes = npay + my * 4096  # one read of the payload + one write of the blocks
         block_desc = "AddCRCsToData: 4092-B payload slices -> 4096-B stamped blocks"
+    elif bsize == "verify":
+        B = 8192
+        buf = torch.empty(my * B, dtype=torch.uint8, device=dev)
+        crc.dev_fill_range(buf, SEED, lo, my, stride=B, ulen=B)
+        crc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=my, flags=crc.HC_F_STAMP)
+        bitmap = torch.empty((my + 31) // 32, dtype=torch.int32, device=dev)
+        first_bad = torch.empty(1, dtype=torch.int64, device=dev)
+        crc.dev_verify_prepare(bitmap, first_bad, my)  # all clean: nothing to reset per step
+        kw = dict(stride=B, ulen=B, nblocks=my, bad_bitmap=bitmap, first_bad=first_bad)
+        step_bytes = my * (B + 4)
+        block_desc = "8192 B, verify mode (stamped; B read + 4 B written per block)"
+        k = min(my, (512 << 20) // B)
+        sample = (slice(0, k * B), np.arange(k, dtype=np.uint64) * B, np.full(k, B, np.uint32))
     elif bsize == "unframe":
         buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
         crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
@@ -404,6 +436,11 @@ def main(argv=None):
     step = make_step(buf, out, kw)
     dt, mean_kern_s = timed(step, args.steps, args.warmup, world > 1)
     info = crc.last_launch()
+    verify_clean = None
+    if bsize == "verify":  # every stamped block must have verified clean
+        verify_clean = int(first_bad.item()) == 2**63 - 1 and int(bitmap.abs().sum().item()) == 0
+        if not verify_clean:
+            print("[bench] verify workload reported a bad block", file=sys.stderr)
 
     # max-over-ranks clock, summed bytes (all-reduce of 3 scalars, after the timed region)
     dt, mean_kern_s, all_bytes = shard.job_timing(dt, mean_kern_s, float(step_bytes), device=dev)
@@ -455,6 +492,8 @@ def main(argv=None):
                 "traffic": None if traffic is None else round(traffic["bytes"]),
                 "kernel": info["kernel"], "bytes_per_launch": step_bytes,
                 "mean_launch_ms": round(mean_kern_s * 1e3, 4),
+                "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
+                "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
                 "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
@@ -485,7 +524,8 @@ def main(argv=None):
                        "block_bytes": block_desc, "bytes_per_gpu_step": step_bytes,
                        "parallelism": f"shard-by-block-index x{world}",
                        "dist_backend": backend if world > 1 else None,
-                       "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4)},
+                       "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4),
+                       **({"verify_clean": verify_clean} if verify_clean is not None else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
