@@ -497,7 +497,7 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 //   * A block that is not 16-B aligned or whose length is not a positive
 //     multiple of 4096 costs one group of dummy rows (re-reads of the current
 //     group, never stored) and is left to k_crc_any (fast_mask 4095).
-template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false>
+template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false, bool kBatch = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ lens, uint64_t stride,
                                                          uint32_t ulen, uint32_t flags, uint64_t nblocks,
@@ -660,30 +660,46 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
     auto pin = [&] {
       if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
     };
-    meta_issue(i2);
-    q0 = load_row<1>(np, lane);
-    pin();
+    // kBatch (A/B only): the group's 4 refills issued together after its last
+    // row, as a plain read stream does, instead of each right after its row
+    if constexpr (!kBatch) {
+      meta_issue(i2);
+      q0 = load_row<1>(np, lane);
+      pin();
+    }
     c0 = row_step(c0, q1.x);
     c1 = row_step(c1, q1.y);
     c2 = row_step(c2, q1.z);
     c3 = row_step(c3, q1.w);
-    pin();
-    q1 = load_row<1>(np + 1024, lane);
-    pin();
+    if constexpr (!kBatch) {
+      pin();
+      q1 = load_row<1>(np + 1024, lane);
+      pin();
+    }
     c0 = row_step(c0, q2.x);
     c1 = row_step(c1, q2.y);
     c2 = row_step(c2, q2.z);
     c3 = row_step(c3, q2.w);
-    pin();
-    q2 = load_row<1>(np + 2048, lane);
-    pin();
+    if constexpr (!kBatch) {
+      pin();
+      q2 = load_row<1>(np + 2048, lane);
+      pin();
+    }
     c0 = row_step(c0, q3.x);
     c1 = row_step(c1, q3.y);
     c2 = row_step(c2, q3.z);
     c3 = row_step(c3, q3.w);
-    pin();
-    q3 = load_row<1>(np + 3072, lane);
-    pin();
+    if constexpr (!kBatch) {
+      pin();
+      q3 = load_row<1>(np + 3072, lane);
+      pin();
+    } else {
+      meta_issue(i2);
+      q0 = load_row<1>(np, lane);
+      q1 = load_row<1>(np + 1024, lane);
+      q2 = load_row<1>(np + 2048, lane);
+      q3 = load_row<1>(np + 3072, lane);
+    }
     if (last) {  // block cur is complete
       if (!cur.skip) {
         uint32_t crc;

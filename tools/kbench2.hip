@@ -157,14 +157,15 @@ int main(int argc, char **argv) {
       add("grp pinned C=512", true, GRP(false, true, false, 9, true));
       add("production launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
     } else {
-      add("grp pinned C=32", true, GRP(false, true, false, 5, true));
+      add("PROD launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
       add("grp pinned C=64", true, GRP(false, true, false, 6, true));
       add("grp pinned C=128", true, GRP(false, true, false, 7, true));
-      add("grp C=32 (not pinned)", true, GRP(false, true, false, 5));
-      add("uni (again)", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
-      add("grp pinned C=32 (again)", true, GRP(false, true, false, 5, true));
-      add("grp pinned C=128 (again)", true, GRP(false, true, false, 7, true));
-      add("NULL grp pinned C=32", false, GRP(false, true, true, 5, true));
+      add("grp BATCH refill C=64", true, GRP(false, true, false, 6, false, true));
+      add("grp BATCH refill C=128", true, GRP(false, true, false, 7, false, true));
+      add("NULL grp pinned C=128", false, GRP(false, true, true, 7, true));
+      add("NULL grp BATCH C=128", false, GRP(false, true, true, 7, false, true));
+      add("PROD launch_grp (again)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+      add("grp BATCH refill C=128 (again)", true, GRP(false, true, false, 7, false, true));
     }
   } else {
     add("r1 k_crc_fast + k_crc_any(1023)", true, [&](hipStream_t st) {
@@ -188,13 +189,21 @@ int main(int argc, char **argv) {
         launch_general(b, 4095, cus, st);
       });
     } else {
-      add("grp pinned C=32 + any(4095)", true, GRPANY(5));
+      add("PROD launch_grp + any", true, [&](hipStream_t st) {
+        launch_grp(b, cus, st);
+        launch_general(b, 4095, cus, st);
+      });
+      add("grp BATCH refill C=64 + any", true, [&](hipStream_t st) {
+        GRP(true, true, false, 6, false, true)(st);
+        launch_general(b, 4095, cus, st);
+      });
       add("grp pinned C=64 + any(4095)", true, GRPANY(6));
-      add("grp pinned C=128 + any(4095)", true, GRPANY(7));
-      add("grp pinned C=32 alone", true, GRP(true, true, false, 5, true));
-      add("grp pinned C=32 + any (again)", true, GRPANY(5));
-      add("any(4095) sweep alone (early exit)", false, [&](hipStream_t st) { launch_general(b, 4095, cus, st); });
-      add("NULL grp pinned C=32", false, GRP(true, true, true, 5, true));
+      add("NULL grp pinned C=64", false, GRP(true, true, true, 6, true));
+      add("NULL grp BATCH C=64", false, GRP(true, true, true, 6, false, true));
+      add("PROD launch_grp + any (again)", true, [&](hipStream_t st) {
+        launch_grp(b, cus, st);
+        launch_general(b, 4095, cus, st);
+      });
     }
   }
 
