@@ -145,6 +145,13 @@ int main(int argc, char **argv) {
     add("r1 static (again)", true, [&](hipStream_t st) { launch_general_static(b, 0, cus, st); });
     add("PROD launch_general (dyn, 1 window)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
     add("k_crc_any dyn C=4 (again)", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 2); });
+#define ANYV(VAR)                                                                                               \
+  [&](hipStream_t st) {                                                                                         \
+    hipLaunchKernelGGL((k_crc_any<4, VAR, true>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len,   \
+                       b.stride, b.ulen, b.flags, b.nblocks, 0u, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables); \
+  }
+    add("any kVar 1 (first batch only with body rows)", true, ANYV(1));
+    add("PROD launch_general (again)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
   } else if (!arrays) {
     add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
     if (sweep) {
