@@ -57,7 +57,10 @@ int main(int argc, char **argv) {
   // general-kernel modes (k_crc_any): msg = config 5b (log-uniform 64 B - 64 KiB
   // records packed back to back at an odd address, whole-message CRC), eq9815 =
   // equal 9815-B records, blk4092 = 4092-B blocks in block mode (off/len)
-  const bool general = mode == "msg" || mode == "eq9815" || mode == "blk4092";
+  // msgsmall / msgbig: the same log-uniform law restricted to records under /
+  // at or over 1 KiB (what config 5b's small records cost)
+  const bool logu = mode == "msg" || mode == "msgsmall" || mode == "msgbig";
+  const bool general = logu || mode == "eq9815" || mode == "blk4092";
   const bool arrays = mode == "mixed" || mode == "offlen4k" || general;
   const uint32_t B = arrays ? 4096 : (uint32_t)std::atoi(mode.c_str());
   if (!arrays && (B == 0 || B % 4096 != 0)) {  // never launch a kernel outside its layout contract
@@ -75,9 +78,12 @@ int main(int argc, char **argv) {
   for (uint64_t i = 0; i < N; i++) {
     uint32_t l = B;
     if (mode == "mixed") l = 4096u << (uint32_t)(splitmix_h(0x48756E64ull ^ 0x5A5A5A5A5A5A5A5Aull, i, (1u << 21) - 1) % 3);
-    if (mode == "msg") {  // log-uniform in [64, 65536]
-      const double u = (double)(splitmix_h(0x5B, i, 0) >> 11) / 9007199254740992.0;
+    if (logu) {  // log-uniform in [64, 65536] (msgsmall: [64, 1024), msgbig: [1024, 65536])
+      double u = (double)(splitmix_h(0x5B, i, 0) >> 11) / 9007199254740992.0;
+      if (mode == "msgsmall") u *= 0.4;
+      if (mode == "msgbig") u = 0.4 + 0.6 * u;
       l = (uint32_t)(64.0 * std::exp(u * std::log(1024.0)));
+      if (mode == "msgsmall" && l >= 1024) l = 1023;
     }
     if (mode == "eq9815") l = 9815;
     if (mode == "blk4092") l = 4092;
@@ -121,7 +127,7 @@ int main(int argc, char **argv) {
     b.off = doff;
     b.len = dlen;
   }
-  if (mode == "msg" || mode == "eq9815") b.flags = hc::kFlagMessages;
+  if (logu || mode == "eq9815") b.flags = hc::kFlagMessages;
   const uint32_t lg5 = 5;
   using namespace hc;
   std::vector<Variant> vs;
@@ -145,13 +151,16 @@ int main(int argc, char **argv) {
     add("r1 static (again)", true, [&](hipStream_t st) { launch_general_static(b, 0, cus, st); });
     add("PROD launch_general (dyn, 1 window)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
     add("k_crc_any dyn C=4 (again)", true, [&](hipStream_t st) { launch_general_dyn(b, 0, cus, st, 2); });
-#define ANYV(VAR)                                                                                               \
+#define ANYV(BATCH, VAR)                                                                                        \
   [&](hipStream_t st) {                                                                                         \
-    hipLaunchKernelGGL((k_crc_any<4, VAR, true>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len,   \
+    hipLaunchKernelGGL((k_crc_any<BATCH, VAR, true>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len, \
                        b.stride, b.ulen, b.flags, b.nblocks, 0u, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables); \
   }
-    add("any kVar 1 (first batch only with body rows)", true, ANYV(1));
+    add("any batch 8 rows", true, ANYV(8, 3));
+    add("any batch 6 rows", true, ANYV(6, 3));
+    add("any batch 2 rows", true, ANYV(2, 3));
     add("PROD launch_general (again)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
+    add("any batch 8 rows (again)", true, ANYV(8, 3));
   } else if (!arrays) {
     add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
     if (sweep) {
