@@ -857,7 +857,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
   const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
   const bool msg = (flags & kFlagMessages) != 0;
+  // kVar bit 3 (A/B, timing only): the LDS arithmetic replaced by an XOR fold
+  constexpr bool kNullMath = (kVar & 8) != 0;
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (kNullMath) return c ^ w;
     const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
     const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
     const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
@@ -865,6 +868,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     return xor3(xor3(t0, t1, t2), t3, w);
   };
   auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    if constexpr (kNullMath) return x ^ w;
     const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
     const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
     const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
@@ -1078,7 +1082,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     if constexpr ((kVar & 2) != 0) issue_first(ge);
 
     const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-    const uint32_t crcv = dshort ? 0u : wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    const uint32_t crcv = dshort ? 0u : wave_xor(kNullMath ? dd : matvec32(col, dd)) ^ 0xFFFFFFFFu;
     const bool bad = !msg && first_bad && (dshort || dsw != crcv);  // wave-uniform
     if (crc_out) lane0_store_u32(crc_out + done.blk, crcv);
     if (!msg && !dshort && (flags & kFlagStamp))  // PutUint32LE(block[0:4], crc)
