@@ -425,6 +425,63 @@ def test_concurrent_host_batches(cuda, hc, oracle):
     assert not errors
 
 
+def test_concurrent_mixed_host_entries(cuda, hc, oracle):
+    """Every host batch entry at once from 12 threads (3x the pipeline pool):
+    CRC words, GPU-side verify (clean and corrupt), stamping as chunks retire,
+    AddCRCsToData (framing overlapped with the source batch), ReadFromDisk
+    (copy-out overlapped with the verify) and whole-message CRCs; every result
+    against the oracle, the pool never above HC_MAX_PIPES."""
+    rng = np.random.default_rng(61)
+    B, nb = 4096, 3000
+    data = rng.integers(0, 256, nb * B, dtype=np.uint8)
+    words = oracle.crc32_blocks(data)
+    stamped = _stamped_blocks(oracle, rng, nb, B)
+    bad = stamped.copy()
+    bad[1777 * B + 99] ^= 1
+    payload = rng.integers(0, 256, 4092 * 600 + 123, dtype=np.uint8).tobytes()
+    frame_want = np.zeros(hc.lib().hc_add_crcs_size(len(payload)), dtype=np.uint8)
+    oracle.lib().oc_add_crcs_to_data(payload, len(payload), frame_want.ctypes.data)
+    rd_want = oracle.read_from_disk(stamped.tobytes(), B, 7, 2900 * 4092)
+    lens = rng.integers(0, 20000, 3000).astype(np.uint32)
+    off = np.zeros(3000, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    msgs = rng.integers(0, 256, int(off[-1]) + int(lens[-1]) + 16, dtype=np.uint8)
+    msg_want = oracle.crc32_messages(msgs, off, lens)
+    errors = []
+
+    def work(kind):
+        try:
+            for _ in range(3):
+                if kind == 0:
+                    assert (hc.crc32_blocks(data) == words).all()
+                elif kind == 1:
+                    err, _bm, fb = hc.verify_blocks(stamped)
+                    assert err is None and fb == -1
+                    err, bm, fb = hc.verify_blocks(bad)
+                    assert str(err) == "CRC mismatch in block" and fb == 1777
+                    assert np.nonzero(np.unpackbits(bm.view(np.uint8), bitorder="little"))[0].tolist() == [1777]
+                elif kind == 2:
+                    cp = stamped.copy()
+                    cp.reshape(nb, B)[:, :4] = 0
+                    hc.stamp_blocks(cp)
+                    assert np.array_equal(cp, stamped)
+                elif kind == 3:
+                    assert bytes(hc.AddCRCsToData(payload)) == frame_want.tobytes()
+                elif kind == 4:
+                    got, fo, err = hc.ReadFromDisk(stamped.tobytes(), B, 7, 2900 * 4092)
+                    assert err is None and got == rd_want[0] and fo == rd_want[1]
+                else:
+                    assert (hc.crc32_messages(msgs, off, lens) == msg_want).all()
+        except AssertionError as e:  # noqa: PERF203
+            errors.append((kind, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(i % 6,)) for i in range(12)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors, errors[:3]
+    assert hc.host_pipelines() <= 4
+
+
 def test_side_stream(cuda, hc, oracle):
     torch = cuda
     s = torch.cuda.Stream()
