@@ -910,6 +910,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
       const uint64_t produced = produced_before(i);
       const uint64_t bo = i == 0 ? boff0 : HC_CRC_SIZE;
       const uint64_t take = std::min<uint64_t>(size - produced, B - bo);
+      if (take == 0) continue;  // (out may be null when size == 0)
       const uint64_t o = i * B + bo;
       // bytes past `avail` are zeros
       const uint64_t have = o >= avail ? 0 : std::min<uint64_t>(take, avail - o);

@@ -367,3 +367,25 @@ def test_read_blocks_touched_matches_loop(hc):
                     blocks += 1
                     boff = 4
                 assert hc.read_blocks_touched(B, start, size) == blocks, (B, start, size)
+
+
+def test_read_from_disk_zero_size_null_out(hc, oracle):
+    """ReadFromDisk(start, 0) (block_manager.go:189-242 with size 0): the Go loop
+    (`for remainingBytes > 0`, :203) never runs, so no block is read or
+    verified and no output buffer is needed; finalPhysicalOffset is the
+    oracle's."""
+    import ctypes
+    rng = np.random.default_rng(91)
+    B = 4096
+    raw = rng.integers(0, 256, 3 * B, dtype=np.uint8)
+    crcs = oracle.crc32_blocks(raw, stride=B, ulen=B)
+    for i in range(3):
+        raw[i * B:i * B + 4] = np.frombuffer(np.uint32(crcs[i]).tobytes(), dtype=np.uint8)
+    for start in (0, 3, 4, 100, B - 1):
+        fo, bad, hashed = ctypes.c_uint64(0), ctypes.c_int64(0), ctypes.c_uint64(0)
+        rc = hc.lib().hc_read_from_disk_v(raw.ctypes.data, raw.size, B, start, 0, None, None, ctypes.byref(fo),
+                                         ctypes.byref(bad), ctypes.byref(hashed))
+        _, wfo, wrc, _ = oracle.read_from_disk(raw.tobytes(), B, start, 0)
+        assert rc == wrc == 0 and fo.value == wfo and bad.value == -1 and hashed.value == 0, start
+        assert hc.read_blocks_touched(B, start, 0) == 0
+
