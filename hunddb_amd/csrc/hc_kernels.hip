@@ -94,6 +94,19 @@ __device__ __forceinline__ void lane0_store_u32(uint32_t *p, uint32_t v) {
       : "v"(p), "v"(v)
       : "memory");
 }
+// per-lane store under an explicit exec mask (asm, so no VMEM instruction sits
+// behind a branch; safe for the waitcnt pass for the same reason as above)
+__device__ __forceinline__ void lanes_store_u32(uint32_t *p, uint32_t v, uint64_t mask) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, %3\n\t"
+      "global_store_dword %1, %2, off\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv)
+      : "v"(p), "v"(v), "s"(mask)
+      : "memory");
+}
 __device__ __forceinline__ void lane0_atomic_or(uint32_t *p, uint32_t v) {
   uint64_t sv;
   asm volatile(
@@ -876,6 +889,95 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     return xor3(xor3(t0, t1, t2), t3, w);
   };
 
+  // ---- small records, one per lane (kVar bit 4, whole-message mode) ---------
+  // A window's records of <= 1020 bytes (one row) are hashed lane-parallel:
+  // lane k takes record g+k (its metadata is already in this lane) and runs
+  // the Horner chain c <- shift4(c) ^ V_i over the 4-byte words of the
+  // virtual message zeros(z) || W0 || M (z = -L mod 4), then
+  // crc = shift4(c) ^ ~0 (the 4-byte placement of the row kernels' last lane).
+  // Loads are the aligned 16-B chunks of [Q, Q + T) (Q = P - z - 4), four in
+  // flight per lane; a chunk that does not overlap the record reads 16 bytes
+  // of the constant table image instead (only prefix bytes, masked, or bytes
+  // past the end, unused, come from such a chunk), so no byte outside the
+  // record's own aligned chunks is touched and no load sits behind a branch.
+  constexpr uint32_t kSmallMax = kRowBytes - 4;
+  auto small_lanes = [&](uint64_t m, uint64_t oj, uint32_t lj, uint64_t g0) {
+    const bool act = (m >> lane) & 1u;
+    const uint32_t L = act ? lj : 0u;
+    const uintptr_t P = (uintptr_t)base + (act ? oj : 0u);
+    const uint32_t z = (4u - (L & 3u)) & 3u;
+    const uint32_t T = z + 4u + L;  // virtual bytes, a multiple of 4
+    const uint32_t nw = T >> 2;
+    const uintptr_t Q = P - z - 4u;
+    const uintptr_t Qa = Q & ~(uintptr_t)15;
+    const uint32_t mq = (uint32_t)(Q & 15u), qw = mq >> 2, rb = mq & 3u;
+    const uint32_t nch = (mq + T + 15u) >> 4;
+    uint32_t mx = 0;  // wave max of nch (<= 66) by ballot
+    for (uint32_t bb = 64; bb; bb >>= 1)
+      if (__ballot(act && nch >= mx + bb)) mx += bb;
+    const uintptr_t safe = (uintptr_t)tables;
+    auto ld = [&](uint32_t c) -> uint4 {
+      const uintptr_t X = Qa + 16u * c;
+      const bool in = act && L > 0 && X + 16u > P && X < P + L;
+      // plain (cached) load: records packed back to back share lines that the
+      // next chunks of the neighbouring lanes read again
+      return *reinterpret_cast<const uint4 *>(in ? X : safe);
+    };
+    auto sel = [&](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return qw == 0 ? a : qw == 1 ? b : qw == 2 ? c2 : d; };
+    // 16 bytes at byte mq of the 32-byte pair (a, b), mq per lane
+    auto fun = [&](const uint4 &a, const uint4 &b) {
+      const uint32_t w0_ = sel(a.x, a.y, a.z, a.w), w1_ = sel(a.y, a.z, a.w, b.x), w2_ = sel(a.z, a.w, b.x, b.y),
+                     w3_ = sel(a.w, b.x, b.y, b.z), w4_ = sel(b.x, b.y, b.z, b.w);
+      return make_uint4(__builtin_amdgcn_alignbyte(w1_, w0_, rb), __builtin_amdgcn_alignbyte(w2_, w1_, rb),
+                        __builtin_amdgcn_alignbyte(w3_, w2_, rb), __builtin_amdgcn_alignbyte(w4_, w3_, rb));
+    };
+    const uint64_t Y = (uint64_t)w0 << 32;
+    uint32_t c = 0;
+    auto step = [&](uint32_t i, uint32_t w, bool head) {
+      if (head) {  // words 0 and 1 may hold the prefix: zeros, then W0 (as the edge rows do)
+        const int32_t d = -((int32_t)(4u * i) - (int32_t)z - 4);
+        const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : 0xFFFFFFFFu << (8 * d));
+        const uint32_t wv = (d >= 1 && d <= 8) ? (uint32_t)(Y >> (64 - 8 * d)) : 0u;
+        w = (w & dm) | wv;
+      }
+      const uint32_t nc = i == 0 ? w : shift4(c, w);
+      c = i < nw ? nc : c;
+    };
+    uint4 A0 = ld(0), A1 = ld(1), A2 = ld(2), A3 = ld(3);
+    for (uint32_t k = 0; k < mx; k += 4) {
+      // chunk pair (k+j, k+j+1) gives words 4(k+j) .. +3; chunk k+j is
+      // reloaded with chunk k+j+4 right after its last use
+      const bool head = k == 0;
+      uint4 f = fun(A0, A1);
+      A0 = ld(k + 4);
+      step(4 * k + 0, f.x, head);
+      step(4 * k + 1, f.y, head);
+      step(4 * k + 2, f.z, false);
+      step(4 * k + 3, f.w, false);
+      f = fun(A1, A2);
+      A1 = ld(k + 5);
+      step(4 * k + 4, f.x, false);
+      step(4 * k + 5, f.y, false);
+      step(4 * k + 6, f.z, false);
+      step(4 * k + 7, f.w, false);
+      f = fun(A2, A3);
+      A2 = ld(k + 6);
+      step(4 * k + 8, f.x, false);
+      step(4 * k + 9, f.y, false);
+      step(4 * k + 10, f.z, false);
+      step(4 * k + 11, f.w, false);
+      f = fun(A3, A0);
+      A3 = ld(k + 7);
+      step(4 * k + 12, f.x, false);
+      step(4 * k + 13, f.y, false);
+      step(4 * k + 14, f.z, false);
+      step(4 * k + 15, f.w, false);
+    }
+    asm volatile("" ::"v"(A0.x), "v"(A1.x), "v"(A2.x), "v"(A3.x));  // consume the last loads here
+    const uint32_t crc = shift4(c, 0u) ^ 0xFFFFFFFFu;
+    if (crc_out) lanes_store_u32(crc_out + g0 + lane, crc, m);
+  };
+
   // ---- message cursor ------------------------------------------------------
   // The metadata of 64 messages g .. g+63 sits one per lane (one coalesced
   // load); `todo` ballots the ones this kernel must do (only_nonfast: those
@@ -938,6 +1040,15 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       // blocks whose length is a positive multiple of fast_mask + 1
       const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & fast_mask) == 0 && lj != 0;
       todo = __ballot(j < b1 && !(fast_mask && fast));
+      if constexpr ((kVar & 16) != 0) {
+        if (msg) {
+          const uint64_t sm = __ballot(j < b1 && !(fast_mask && fast) && lj <= kSmallMax);
+          if (sm) {
+            small_lanes(sm, oj, lj, gv);
+            todo &= ~sm;
+          }
+        }
+      }
     }
   };
 
@@ -1595,8 +1706,15 @@ hipError_t launch_general_static(const Batch &b, uint32_t fast_mask, int grid, h
 
 hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s, int lg_chunk) {
   const uint32_t lg = lg_chunk >= 0 ? (uint32_t)lg_chunk : 0u;
-  hipLaunchKernelGGL((k_crc_any<4, 3, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                     b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+  // whole-message batches hash their records of <= 1020 bytes lane-parallel
+  // (kVar bit 4: 1.77x on small records, neutral on config 5b and on large
+  // ones, profiles/r2/any_small_lanes/); block mode keeps the leaner build
+  if (b.flags & kFlagMessages)
+    hipLaunchKernelGGL((k_crc_any<4, 19, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+  else
+    hipLaunchKernelGGL((k_crc_any<4, 3, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
   return hipGetLastError();
 }
 

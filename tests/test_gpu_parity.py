@@ -124,6 +124,44 @@ def test_general_lengths_and_alignment(cuda, hc, oracle):
     assert bad.size == 0, (bad[:10], lens[bad[:10]], off[bad[:10]] % 16)
 
 
+def test_small_messages_lane_parallel(cuda, hc, oracle):
+    """Whole-message CRCs of records <= 1020 B are hashed one per lane (k_crc_any
+    kVar bit 4): lengths 0..3, around the 1020/1021 threshold, any alignment,
+    unsorted and overlapping offsets, records at offset 0 and empty records at
+    the buffer's end, mixed with wave-path records -- vs the oracle."""
+    torch = cuda
+    rng = np.random.default_rng(1020)
+    total = 8_000_000
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    n = 40_000
+    kind = rng.integers(0, 10, n)
+    lens = np.where(kind < 4, rng.integers(0, 64, n),
+                    np.where(kind < 8, rng.integers(64, 1022, n), rng.integers(1021, 4000, n))).astype(np.uint32)
+    lens[:40] = np.r_[np.arange(8), np.arange(1014, 1030), np.arange(16)]
+    off = rng.integers(0, total - 4000, n).astype(np.uint64)  # unsorted, overlapping
+    off[:5] = 0
+    off[-5:] = total
+    lens[-5:] = 0
+    assert (off + lens <= total).all()  # every record inside the buffer before any launch
+    buf = torch.from_numpy(host).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.view(np.int32)).cuda()
+    got = dev_crc(torch, hc, buf, n, off=doff, lens=dlen, flags=hc.HC_F_MESSAGES)
+    want = oracle.crc32_messages(host, off, lens, threads=16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:10], lens[bad[:10]], off[bad[:10]] % 16)
+    # a batch of small records only, packed back to back at an odd address
+    sl = rng.integers(0, 1021, 6_000).astype(np.uint32)
+    so = np.zeros(sl.size, dtype=np.uint64)
+    so[1:] = np.cumsum(sl[:-1], dtype=np.uint64)
+    so += 1
+    assert (so + sl <= total).all()
+    dso = torch.from_numpy(so.view(np.int64)).cuda()
+    dsl = torch.from_numpy(sl.view(np.int32)).cuda()
+    got = dev_crc(torch, hc, buf, sl.size, off=dso, lens=dsl, flags=hc.HC_F_MESSAGES)
+    assert (got == oracle.crc32_messages(host, so, sl, threads=16)).all()
+
+
 @pytest.mark.parametrize("size,gap", [(1024, 0), (3072, 16), (5120, 0), (4096, 0), (4096, 16),
                                       (12288, 0), (20480, 48)])
 def test_uniform_kernel_routes(cuda, hc, oracle, size, gap):
