@@ -117,6 +117,7 @@ def _lib():
             "hc_read_blocks_touched": (U64, [U32, U64, U64]),
             "hc_dev_read_blocks": (I, [I, P, U64, U32, P, P, P, P, P]),
             "hc_wal_replay": (I, [P, U64, U32, U64, U64, U64, P, U64, P, P, U64, P, P, P, P]),
+            "hc_wal_replay_v": (I, [P, U64, U32, U64, U64, U64, P, U64, P, P, P, U64, P, P, P, P, P]),
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_device_count": (I, []),
@@ -279,13 +280,18 @@ def read_blocks_touched(block_size: int, start_offset: int, size: int) -> int:
 
 
 def wal_replay(blocks, block_size: int = BLOCK_SIZE, start_block: int = 0, start_offset: int = CRC_SIZE,
-               max_records: int = 0, buf_cap=None, slots=None, as_arrays=False, out=None):
+               max_records: int = 0, buf_cap=None, slots=None, as_arrays=False, out=None, end_blocks=False):
     """WAL recovery (lsm/wal/wal.go:362-455, row f3): verify every written block in
     one batch, then parse FULL records and reassemble fragments.
 
     Returns (records, err, bad_block, (pos_block, pos_offset)): `records` is a
     list of the serialized record bytes (what record.Deserialize receives),
-    `err` None or CRCError.  buf_cap/slots limit the output (resumable)."""
+    `err` None or CRCError.  buf_cap/slots limit the output (resumable).
+    end_blocks=True (hc_wal_replay_v) appends two items: the absolute block in
+    which each record completes (memtable.IsFull resumes at that + 1), and the
+    (block, offset) where fragments still pending at the end start (None if
+    nothing is pending or the call stopped early) -- a windowed replay's next
+    start."""
     p, n, _k = _ro_ptr(blocks)
     nb = n // block_size
     cap = nb * block_size if buf_cap is None else int(buf_cap)
@@ -296,9 +302,13 @@ def wal_replay(blocks, block_size: int = BLOCK_SIZE, start_block: int = 0, start
     off = np.empty(max(1, slots), dtype=np.uint64)
     ln = np.empty(max(1, slots), dtype=np.uint64)
     cnt, pb, po, bad = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int64(-1)
-    rc = _lib().hc_wal_replay(p if n else None, nb, block_size, start_block, start_offset, max_records,
-                              buf.ctypes.data, cap, off.ctypes.data, ln.ctypes.data, slots,
-                              ctypes.byref(cnt), ctypes.byref(pb), ctypes.byref(po), ctypes.byref(bad))
+    ends = np.empty(max(1, slots), dtype=np.uint64) if end_blocks else None
+    pend = np.zeros(2, dtype=np.uint64)
+    rc = _lib().hc_wal_replay_v(p if n else None, nb, block_size, start_block, start_offset, max_records,
+                                buf.ctypes.data, cap, off.ctypes.data, ln.ctypes.data,
+                                None if ends is None else ends.ctypes.data, slots,
+                                ctypes.byref(cnt), ctypes.byref(pb), ctypes.byref(po), ctypes.byref(bad),
+                                pend.ctypes.data)
     if rc < 0:
         raise HundCRCError(rc, "wal_replay")
     if as_arrays:  # (record bytes back to back, offsets, lengths) without per-record copies
@@ -306,7 +316,11 @@ def wal_replay(blocks, block_size: int = BLOCK_SIZE, start_block: int = 0, start
     else:
         mv = memoryview(buf)
         recs = [bytes(mv[int(off[i]):int(off[i]) + int(ln[i])]) for i in range(cnt.value)]
-    return recs, (None if rc == HC_OK else CRCError(rc)), bad.value, (pb.value, po.value)
+    res = (recs, (None if rc == HC_OK else CRCError(rc)), bad.value, (pb.value, po.value))
+    if not end_blocks:
+        return res
+    pending = None if int(pend[0]) == 2**64 - 1 else (int(pend[0]), int(pend[1]))
+    return res + (ends[:cnt.value].copy(), pending)
 
 
 # ---- batched, host-resident (GPU) ---------------------------------------------

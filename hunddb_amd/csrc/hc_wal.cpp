@@ -159,6 +159,16 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
                   uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t rec_buf_cap,
                   uint64_t *rec_off, uint64_t *rec_len, uint64_t rec_slots, uint64_t *nrec, uint64_t *pos_block,
                   uint64_t *pos_offset, int64_t *bad_block) {
+  return hc_wal_replay_v(blocks, nblocks, block_size, start_block, start_offset, max_records, rec_buf, rec_buf_cap,
+                         rec_off, rec_len, nullptr, rec_slots, nrec, pos_block, pos_offset, bad_block, nullptr);
+}
+
+int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, uint64_t start_block,
+                    uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t rec_buf_cap,
+                    uint64_t *rec_off, uint64_t *rec_len, uint64_t *rec_end_block, uint64_t rec_slots,
+                    uint64_t *nrec, uint64_t *pos_block, uint64_t *pos_offset, int64_t *bad_block,
+                    uint64_t *pend_pos) {
+  if (pend_pos) pend_pos[0] = UINT64_MAX, pend_pos[1] = 0;
   if (!nrec || !pos_block || !pos_offset) return HC_E_ARG;
   if (bad_block) *bad_block = -1;
   *nrec = 0;
@@ -183,6 +193,7 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   uint64_t stop_blk = 0;  // block of the error / of the record that filled the memtable / that did not fit
   int err_code = HC_OK;
   uint64_t pb = start_block + n, po = HC_CRC_SIZE, count = 0;
+  uint64_t pend_blk = UINT64_MAX, pend_hdr = 0;  // fragments still pending when the blocks run out
   std::vector<Range> R(T);
   int last_range = T - 1;  // ranges after a stop are not used
   double t0 = now_s(), tv = 0, ta = 0, tb = 0, tc = 0;
@@ -268,6 +279,10 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
         po = G.err_hdr;
       }
     }
+    if (stop == kAll && !pend.pieces.empty()) {
+      pend_blk = pend.blk;
+      pend_hdr = pend.hdr;
+    }
     tb = now_s() - t0;
     // C. offsets, lengths and record bytes, per range
     parallel_for(last_range + 1, [&](int t) {
@@ -277,6 +292,7 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
         const Rec &r = G.recs[i];
         rec_off[G.rec_base + i] = o;
         rec_len[G.rec_base + i] = r.len;
+        if (rec_end_block) rec_end_block[G.rec_base + i] = r.done_blk;
         if (r.head)
           for (const Piece &q : G.prefix) {
             copy_nt(rec_buf + o, q.p, q.len);
@@ -321,5 +337,6 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
   *nrec = count;
   *pos_block = pb;
   *pos_offset = po;
+  if (pend_pos && code == HC_OK && stop == kAll) pend_pos[0] = pend_blk, pend_pos[1] = pend_hdr;
   return code;
 }

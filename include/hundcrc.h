@@ -170,6 +170,23 @@ int hc_wal_replay(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, 
                   uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t rec_buf_cap,
                   uint64_t *rec_off, uint64_t *rec_len, uint64_t rec_slots, uint64_t *nrec, uint64_t *pos_block,
                   uint64_t *pos_offset, int64_t *bad_block);
+/* hc_wal_replay plus two optional outputs for callers that replay a long WAL
+ * in windows and decide memtable.IsFull themselves (it depends on distinct
+ * keys: lsm/memtable skip_list.go:418, btree.go:169, hashmap.go:332):
+ *  - rec_end_block (rec_slots entries): the absolute block in which record i
+ *    completes (its FULL or LAST fragment).  Replay with max_records = 0, Put
+ *    the records in order, and when the memtable fills on record i resume
+ *    where wal.go:392-397 does: block rec_end_block[i] + 1, offset CRC_SIZE.
+ *  - pend_pos (2 entries): when the call parsed every block without error
+ *    (HC_OK, no capacity or max_records stop), the (block, header offset) at
+ *    which the fragments still pending at the end start -- the next window
+ *    starts there so a record split across windows is rebuilt whole -- or
+ *    (UINT64_MAX, 0) when nothing is pending. */
+int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size, uint64_t start_block,
+                    uint64_t start_offset, uint64_t max_records, uint8_t *rec_buf, uint64_t rec_buf_cap,
+                    uint64_t *rec_off, uint64_t *rec_len, uint64_t *rec_end_block, uint64_t rec_slots,
+                    uint64_t *nrec, uint64_t *pos_block, uint64_t *pos_offset, int64_t *bad_block,
+                    uint64_t *pend_pos);
 
 /* Fused AddCRCsToData on device memory (utils/crc/crc_util.go:41-64): frame the
  * n-byte payload src (any alignment) into ceil(n/4092) zero-padded 4096-byte

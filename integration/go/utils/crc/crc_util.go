@@ -181,3 +181,50 @@ func ReadVerifiedCached(raw []byte, blockSize uint16, startOffset, size uint64, 
 	}
 	return out, uint64(final), nil
 }
+
+// WalWindow is what WalReplay returns for one window of WAL blocks.
+type WalWindow struct {
+	Records    [][]byte // serialized records (what record.Deserialize receives), in order
+	EndBlocks  []uint64 // block (index within the window) in which each record completes
+	PendBlock  int64    // where the fragments pending at the window's end start (-1: none)
+	PendOffset uint64
+	StopBlock  uint64 // after an error: the failing block (index within the window) ...
+	StopOffset uint64 // ... and the offset wal.go's position would hold there
+}
+
+// WalReplay is one window of WAL recovery (row f3; wal.go:362-455 minus the
+// file I/O and the memtable): blocks holds written WAL blocks of blockSize
+// bytes back to back, parsing starts at startOffset of the first block.  Every
+// block is verified in one batch (GPU from 256 blocks), then FULL payloads and
+// reassembled FIRST/MIDDLE/LAST fragments come back in order as slices of one
+// buffer.  A bad block ("CRC mismatch in block") or a framing error ("unknown
+// fragment type", or a header/payload past its block where Go panics) returns
+// the records before it with the error and StopBlock/StopOffset.
+func WalReplay(blocks []byte, blockSize int, startOffset uint64) (WalWindow, error) {
+	nb := len(blocks) / blockSize
+	slots := nb*((blockSize-CRC_SIZE)/17+1) + 1
+	buf := make([]byte, len(blocks)+1)
+	off := make([]uint64, slots)
+	ln := make([]uint64, slots)
+	ends := make([]uint64, slots)
+	pend := make([]uint64, 2)
+	var nrec, posBlock, posOffset C.uint64_t
+	var bad C.int64_t = -1
+	rc := C.hc_wal_replay_v(ptr(blocks), C.uint64_t(nb), C.uint32_t(blockSize), 0, C.uint64_t(startOffset), 0,
+		ptr(buf), C.uint64_t(len(buf)), (*C.uint64_t)(unsafe.Pointer(&off[0])), (*C.uint64_t)(unsafe.Pointer(&ln[0])),
+		(*C.uint64_t)(unsafe.Pointer(&ends[0])), C.uint64_t(slots), &nrec, &posBlock, &posOffset, &bad,
+		(*C.uint64_t)(unsafe.Pointer(&pend[0])))
+	w := WalWindow{PendBlock: -1, StopBlock: uint64(posBlock), StopOffset: uint64(posOffset)}
+	if rc < 0 {
+		return w, goErr(rc)
+	}
+	w.Records = make([][]byte, int(nrec))
+	for i := range w.Records {
+		w.Records[i] = buf[off[i] : off[i]+ln[i] : off[i]+ln[i]]
+	}
+	w.EndBlocks = ends[:int(nrec)]
+	if pend[0] != ^uint64(0) {
+		w.PendBlock, w.PendOffset = int64(pend[0]), pend[1]
+	}
+	return w, goErr(rc)
+}

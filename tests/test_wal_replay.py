@@ -71,6 +71,51 @@ def test_wal_replay_records_match_writer(hc, oracle):
     assert [len(r) for r in recs] == kept
 
 
+@pytest.mark.parametrize("seed", [4, 5])
+def test_wal_replay_end_blocks_give_the_memtable_full_position(hc, oracle, seed, ranges):
+    """hc_wal_replay_v's rec_end_block: the block each record completes in.  A
+    caller whose memtable.IsFull depends on the keys replays without a limit and
+    stops itself; stopping after record j must land where wal.go:392-397 (and
+    max_records = j, pinned by the oracle) lands: block end[j-1] + 1, offset 4."""
+    img, sizes, st = _image(oracle, seed, 140)
+    for sb in (0, 3):
+        full, err, _, end, ends, _pend = hc.wal_replay(bytes(img), 4096, sb, 4, end_blocks=True)
+        assert err is None and len(ends) == len(full)
+        assert (np.diff(ends.astype(np.int64)) >= 0).all() and ends[0] >= sb and ends[-1] < end[0]
+        for j in sorted({1, 2, len(full) // 3, len(full) // 2, len(full) - 1, len(full)}):
+            want, wrc, _, wpos = oracle.wal_replay(bytes(img), 4096, sb, 4, j)
+            assert wrc == 0 and want == full[:j]
+            assert wpos == (int(ends[j - 1]) + 1, 4), (sb, j)
+
+
+@pytest.mark.parametrize("win", [1, 2, 5, 17])
+def test_wal_replay_in_windows_equals_one_replay(hc, oracle, win, ranges):
+    """How integration/go/lsm/wal/wal_recover_gpu.go replays a long WAL: windows
+    of `win` blocks, each starting where the previous one's pending fragments
+    start (pend_pos) or at its end.  The records, their end blocks and the final
+    position are exactly those of one replay over the whole image."""
+    img, sizes, st = _image(oracle, 8, 160)
+    nb = len(img) // 4096
+    full, err, _, end, ends, pend = hc.wal_replay(bytes(img), 4096, end_blocks=True)
+    assert err is None and pend is None
+    got, got_ends = [], []
+    blk, off = 0, 4
+    w = win
+    while blk < nb:
+        hi = min(nb, blk + w)
+        part, err, _, pos, pe, pd = hc.wal_replay(bytes(img[:hi * 4096]), 4096, blk, off, end_blocks=True)
+        assert err is None and pos == (hi, 4)
+        got += part
+        got_ends += pe.tolist()
+        if pd is None or hi == nb:
+            blk, off, w = hi, 4, win
+        elif pd == (blk, off):  # one record longer than the window: widen it
+            w *= 2
+        else:
+            blk, off, w = pd[0], pd[1], win
+    assert got == full and got_ends == ends.tolist()
+
+
 def test_wal_replay_capacity_resume(hc, oracle, ranges):
     """Output capacity smaller than the image: resuming at the returned position
     yields exactly the unlimited replay's records."""
