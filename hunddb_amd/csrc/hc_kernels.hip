@@ -510,7 +510,8 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 //   * A block that is not 16-B aligned or whose length is not a positive
 //     multiple of 4096 costs one group of dummy rows (re-reads of the current
 //     group, never stored) and is left to k_crc_any (fast_mask 4095).
-template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false, bool kBatch = false>
+template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false, bool kBatch = false,
+          bool kXcd = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ lens, uint64_t stride,
                                                          uint32_t ulen, uint32_t flags, uint64_t nblocks,
@@ -561,7 +562,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   };
 
   const uint32_t wave = uni(tid >> 6);
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint64_t G = gridDim.x;
+  // kXcd (A/B only): workgroup g runs on XCD g % 8; renumber so that each
+  // XCD's workgroups own neighbouring chunk slots (G a multiple of 8)
+  const uint64_t wg = kXcd && (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   // k-th block of this workgroup's sequence, increasing in k: the first one
   // past the batch ends the wave (a per-workgroup rotation inside the chunks
@@ -1718,15 +1722,26 @@ hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipS
   return hipGetLastError();
 }
 
+// XCD-contiguous chunk slots: 8/16 KiB uniform batches up to 4M blocks (1M
+// blocks: +0.3-0.9 % on four boxes; 16M blocks: -0.3-0.7 %, workgroup order
+// at C = 128 kept there; profiles/r2/ab_xcd/)
+bool grp_xcd(uint32_t block_bytes, int grid, uint64_t nblocks) {
+  return block_bytes >= 8192 && (grid & 7) == 0 && nblocks <= (4ull << 20);
+}
+
 uint32_t grp_lg_chunk(uint64_t nblocks, int grid, uint32_t block_bytes) {
   // Chunk of C = 2^lg consecutive blocks per workgroup (tools/kbench2 sweeps,
-  // profiles/r2/sweep*: 1M blocks, C = 8 .. 512, four boxes): 8 and 16 KiB
-  // blocks run best at C = 128 (87-88 % of 8 TB/s), 4 KiB blocks at C = 64
-  // (84-85 %), mixed 4/8/16 KiB off/len batches (block_bytes 0) at C = 32-64.
-  // Small batches keep at least 4 chunks per workgroup.  HC_LG_CHUNK overrides
-  // (tuning sweeps only).
+  // profiles/r2/sweep*: 1M blocks, C = 8 .. 512, four boxes): 4 KiB blocks at
+  // C = 64 (84-85 % of 8 TB/s), mixed 4/8/16 KiB off/len batches (block_bytes
+  // 0) at C = 32-64.  8 and 16 KiB blocks with the XCD-contiguous slot order
+  // (grp_xcd; profiles/r2/ab_xcd/, three boxes) at C = 32 and 16: +0.3-0.9 %
+  // over C = 128 in workgroup order.  Small batches keep at least 4 chunks per
+  // workgroup.  HC_LG_CHUNK overrides (tuning sweeps only).
   static const int forced = env_int("HC_LG_CHUNK", -1);
-  uint32_t lg = forced >= 0 ? (uint32_t)forced : (block_bytes >= 8192 ? 7u : 6u);
+  uint32_t lg = forced >= 0                             ? (uint32_t)forced
+                : !grp_xcd(block_bytes, grid, nblocks)  ? (block_bytes >= 8192 ? 7u : 6u)
+                : block_bytes >= 16384                  ? 4u
+                                                        : 5u;
   if (forced < 0)
     while (lg > 0 && (nblocks >> lg) < (uint64_t)grid * 4) lg--;
   return lg;
@@ -1744,6 +1759,10 @@ hipError_t launch_grp(const Batch &b, int grid, hipStream_t s) {
     hipLaunchKernelGGL((k_crc_grp<true, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
                        b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,
                        b.tables);
+  else if (grp_xcd(b.ulen, grid, b.nblocks))  // each XCD's workgroups own neighbouring chunk slots
+    hipLaunchKernelGGL((k_crc_grp<false, true, false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s,
+                       b.base, b.off, b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap,
+                       b.first_bad, b.tables);
   else
     hipLaunchKernelGGL((k_crc_grp<false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
                        b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,

@@ -51,6 +51,7 @@ hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipS
 // k_crc_grp: 4 KiB-multiple blocks (uniform, or off/len with device-side
 // routing of the others to k_crc_any with fast_mask 4095), per-workgroup
 // dynamic hand-out of chunked blocks.
+bool grp_xcd(uint32_t block_bytes, int grid, uint64_t nblocks);
 uint32_t grp_lg_chunk(uint64_t nblocks, int grid, uint32_t block_bytes);
 hipError_t launch_grp(const Batch &b, int grid, hipStream_t s);
 // Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B blocks.

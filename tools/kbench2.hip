@@ -174,12 +174,10 @@ int main(int argc, char **argv) {
       add("PROD launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
       add("grp pinned C=64", true, GRP(false, true, false, 6, true));
       add("grp pinned C=128", true, GRP(false, true, false, 7, true));
-      add("grp BATCH refill C=64", true, GRP(false, true, false, 6, false, true));
-      add("grp BATCH refill C=128", true, GRP(false, true, false, 7, false, true));
-      add("NULL grp pinned C=128", false, GRP(false, true, true, 7, true));
-      add("NULL grp BATCH C=128", false, GRP(false, true, true, 7, false, true));
+      add("grp XCD-contiguous C=16", true, GRP(false, true, false, 4, true, false, true));
+      add("grp XCD-contiguous C=32", true, GRP(false, true, false, 5, true, false, true));
       add("PROD launch_grp (again)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
-      add("grp BATCH refill C=128 (again)", true, GRP(false, true, false, 7, false, true));
+      add("grp pinned C=128 (round-2 r1 production at 8/16 KiB)", true, GRP(false, true, false, 7, true));
     }
   } else {
     add("r1 k_crc_fast + k_crc_any(1023)", true, [&](hipStream_t st) {
