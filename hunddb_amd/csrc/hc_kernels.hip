@@ -1228,8 +1228,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 // from 5.0-5.5 TB/s with static deals to 5.9 TB/s this way).
 // kDepth: interior blocks in flight per wave (2: one prefetched while one is
 // framed; 3: two).  kNull: timing-only build, the CRC replaced by an XOR fold
-// (tools/kframe measures the memory pattern alone).
-template <int kDepth = 2, bool kNull = false>
+// (tools/kframe measures the memory pattern alone).  kXcd (A/B only): XCD-
+// contiguous chunk slots as in k_crc_grp.
+template <int kDepth = 2, bool kNull = false, bool kXcd = false>
 __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
                                                          uint8_t *__restrict__ dst, uint64_t nblk, uint32_t lg_chunk,
                                                          uint32_t *__restrict__ crc_out,
@@ -1347,7 +1348,8 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
   // masks -- and the next block's 4 rows are in flight while this one is hashed.
   // Interior index i (block i + 1) of the workgroup's k-th hand-out:
   const uint64_t ni = nblk > 2 ? nblk - 2 : 0;
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint64_t G = gridDim.x;
+  const uint64_t wg = kXcd && (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
   uint64_t c = blk_of(wave);
@@ -1451,7 +1453,7 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
 // block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
 // overlapping lane 1's store with identical bytes.
-template <uint32_t lg_groups, int kDepth = 2, bool kNull = false>
+template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                            uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
@@ -1505,7 +1507,8 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
   // blocks handed out as in k_crc_grp (chunks of 2^lg_chunk consecutive blocks
   // per workgroup, one block at a time per wave from an LDS counter); a wave
   // walks a block's 4 KiB groups in order
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint64_t G = gridDim.x;
+  const uint64_t wg = kXcd && (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
   const uint64_t bstart = blk_of(wave);

@@ -89,30 +89,31 @@ int main(int argc, char **argv) {
   const uint64_t nblk = N, ni = nblk - 2;
   using namespace hc;
   std::vector<Variant> vs;
-#define FRAME(D, NUL, LG)                                                                                          \
+#define FRAME(D, NUL, LG, ...)                                                                                     \
   [&, lg = (uint32_t)(LG)](hipStream_t st) {                                                                        \
-    hipLaunchKernelGGL((k_frame<D, NUL>), dim3(cus), dim3(kFastThreads), 0, st, src, npay, framed, nblk, lg, crc, dt); \
+    hipLaunchKernelGGL((k_frame<D, NUL __VA_OPT__(,) __VA_ARGS__>), dim3(cus), dim3(kFastThreads), 0, st, src, npay, \
+                       framed, nblk, lg, crc, dt);                                                                  \
   }
-#define UNFRAME(D, NUL, LG)                                                                                        \
+#define UNFRAME(D, NUL, LG, ...)                                                                                   \
   [&, lg = (uint32_t)(LG)](hipStream_t st) {                                                                        \
-    hipLaunchKernelGGL((k_unframe<0, D, NUL>), dim3(cus), dim3(kFastThreads), 0, st, blocks, nblk, lg, pay, crc,    \
-                       bitmap, fb, dt);                                                                             \
+    hipLaunchKernelGGL((k_unframe<0, D, NUL __VA_OPT__(,) __VA_ARGS__>), dim3(cus), dim3(kFastThreads), 0, st, blocks, \
+                       nblk, lg, pay, crc, bitmap, fb, dt);                                                         \
   }
   const uint32_t lgp = grp_lg_chunk(ni, cus, 4096);
   vs.push_back({"PROD k_frame depth 2", 0, true, FRAME(2, false, lgp), {}});
-  vs.push_back({"k_frame depth 3", 0, true, FRAME(3, false, lgp), {}});
-  vs.push_back({"k_frame depth 3 C=8", 0, true, FRAME(3, false, 3), {}});
-  vs.push_back({"k_frame depth 3 C=32", 0, true, FRAME(3, false, 5), {}});
-  vs.push_back({"NULL k_frame depth 2", 0, false, FRAME(2, true, lgp), {}});
-  vs.push_back({"NULL k_frame depth 3", 0, false, FRAME(3, true, lgp), {}});
+  vs.push_back({"k_frame XCD C=16", 0, true, FRAME(2, false, 4, true), {}});
+  vs.push_back({"k_frame XCD C=32", 0, true, FRAME(2, false, 5, true), {}});
+  vs.push_back({"k_frame XCD C=64", 0, true, FRAME(2, false, 6, true), {}});
+  vs.push_back({"k_frame C=128", 0, true, FRAME(2, false, 7), {}});
   vs.push_back({"PROD k_unframe depth 2", 1, true, UNFRAME(2, false, lgp), {}});
-  vs.push_back({"k_unframe depth 3", 1, true, UNFRAME(3, false, lgp), {}});
-  vs.push_back({"k_unframe depth 3 C=8", 1, true, UNFRAME(3, false, 3), {}});
-  vs.push_back({"k_unframe depth 3 C=32", 1, true, UNFRAME(3, false, 5), {}});
-  vs.push_back({"NULL k_unframe depth 2", 1, false, UNFRAME(2, true, lgp), {}});
-  vs.push_back({"NULL k_unframe depth 3", 1, false, UNFRAME(3, true, lgp), {}});
+  vs.push_back({"k_unframe XCD C=16", 1, true, UNFRAME(2, false, 4, true), {}});
+  vs.push_back({"k_unframe XCD C=32", 1, true, UNFRAME(2, false, 5, true), {}});
+  vs.push_back({"k_unframe XCD C=64", 1, true, UNFRAME(2, false, 6, true), {}});
+  vs.push_back({"k_unframe C=128", 1, true, UNFRAME(2, false, 7), {}});
   vs.push_back({"PROD k_frame depth 2 (again)", 0, true, FRAME(2, false, lgp), {}});
   vs.push_back({"PROD k_unframe depth 2 (again)", 1, true, UNFRAME(2, false, lgp), {}});
+  vs.push_back({"k_frame XCD C=32 (again)", 0, true, FRAME(2, false, 5, true), {}});
+  vs.push_back({"k_unframe XCD C=32 (again)", 1, true, UNFRAME(2, false, 5, true), {}});
 
   // reference outputs
   std::vector<uint32_t> cref_f(N), cref_u(N), got(N);
@@ -120,7 +121,7 @@ int main(int argc, char **argv) {
   CK(hipStreamSynchronize(s));
   CK(hipMemcpy(framed_ref, framed, N * 4096, hipMemcpyDeviceToDevice));
   CK(hipMemcpy(cref_f.data(), crc, N * 4, hipMemcpyDeviceToHost));
-  vs[6].run(s);
+  vs[5].run(s);  // PROD k_unframe
   CK(hipStreamSynchronize(s));
   CK(hipMemcpy(pay_ref, pay, N * 4092, hipMemcpyDeviceToDevice));
   CK(hipMemcpy(cref_u.data(), crc, N * 4, hipMemcpyDeviceToHost));
