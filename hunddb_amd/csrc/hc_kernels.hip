@@ -1184,6 +1184,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     // ~4 KiB do not help at 16 waves per CU (k_crc_fast: ring 4 beat ring 8)
     // (rolling refills in k_crc_grp's order -- row r+4 loaded right after row r
     // is hashed -- were 3-11 % slower: profiles/r2/any_rolling/)
+    // (a double-buffered body -- the next batch in flight while one is hashed,
+    // the batch past the end out of range, no branch -- was 7-10 % slower:
+    // profiles/r2/any_double/)
     for (uint32_t r0 = 2; r0 < ge.rows; r0 += kBatch) {
       if (r0 > 2) issue_body(rbody, r0, VA);
       hash_body(ge, r0, VA, c);

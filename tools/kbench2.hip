@@ -156,9 +156,8 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((k_crc_any<BATCH, VAR, true>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len, \
                        b.stride, b.ulen, b.flags, b.nblocks, 0u, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables); \
   }
-    add("any without small lanes (kVar 3, round-2 production)", true, ANYV(4, 3));
+    add("any without small lanes (kVar 3)", true, ANYV(4, 3));
     add("PROD launch_general (again)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
-    add("any without small lanes (again)", true, ANYV(4, 3));
   } else if (!arrays) {
     add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
     if (sweep) {
