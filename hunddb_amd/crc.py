@@ -120,6 +120,7 @@ def _lib():
             "hc_wal_replay_v": (I, [P, U64, U32, U64, U64, U64, P, U64, P, P, P, U64, P, P, P, P, P]),
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
+            "hc_debug_seg_taken": (I, []),
             "hc_device_count": (I, []),
             "hc_host_pipelines": (I, []),
             "hc_md5": (None, [P, S, P]),
@@ -501,6 +502,16 @@ def device_count() -> int:
 def host_pipelines() -> int:
     """Host-batch pipelines alive in this process (bounded by HC_MAX_PIPES)."""
     return int(_lib().hc_host_pipelines())
+
+
+def seg_taken() -> bool:
+    """Whether this thread's last device batch of packed whole messages was
+    hashed by the packed-record stream (k_seg_*) rather than k_crc_any
+    (synchronizes the device; tests and tools)."""
+    r = int(_lib().hc_debug_seg_taken())
+    if r < 0:
+        raise HundCRCError(r, "seg_taken")
+    return r == 1
 
 
 def debug_tables() -> np.ndarray:

@@ -41,10 +41,21 @@ struct DeviceState {
   int status = HC_E_NODEV;
   int cus = 0;
   DeviceTables *dtab = nullptr;  // device copy of the constant image
+  SegTables *dseg = nullptr;     // the packed-record path's tables (k_seg_*)
+  uint32_t *seg_last = nullptr;  // 1 when the last packed-record stream took its batch
 };
 
 constexpr int kMaxDevices = 64;
 DeviceState g_dev[kMaxDevices];
+
+const SegTables &host_seg_tables() {
+  static const SegTables *t = [] {
+    auto *p = new SegTables;
+    build_seg_tables(*p);
+    return p;
+  }();
+  return *t;
+}
 
 const DeviceTables &host_tables() {
   static const DeviceTables *t = [] {
@@ -91,6 +102,20 @@ int init_device(int dev) {
       return;
     }
     d.dtab = static_cast<DeviceTables *>(p);
+    if (hipMalloc(&p, sizeof(SegTables)) != hipSuccess) {
+      d.status = HC_E_NOMEM;
+      return;
+    }
+    if (hipMemcpy(p, &host_seg_tables(), sizeof(SegTables), hipMemcpyHostToDevice) != hipSuccess) {
+      d.status = HC_E_HIP;
+      return;
+    }
+    d.dseg = static_cast<SegTables *>(p);
+    if (hipMalloc(&p, 4) != hipSuccess || hipMemset(p, 0, 4) != hipSuccess) {
+      d.status = HC_E_NOMEM;
+      return;
+    }
+    d.seg_last = static_cast<uint32_t *>(p);
     d.cus = prop.multiProcessorCount;
     d.status = HC_OK;
   });
@@ -114,6 +139,7 @@ void set_last_launch(const hc_launch_info &info);
 namespace {
 
 thread_local hc_launch_info t_last{"", 0, 0, 0, 0, 0, 0};
+thread_local int t_seg_dev = -1;  // device of this thread's last packed-record stream (hc_debug_seg_taken)
 
 }  // namespace
 
@@ -123,9 +149,22 @@ namespace {
 
 // ---------------------------------------------------------------------------
 // Device batch dispatch (shared by _dev_ entries and the host pipeline)
+// Whole-message off/len batches of at least HC_SEG_MIN_MSGS messages (default
+// 131072) from a device entry first go to the packed-record stream (k_seg_*,
+// launch_seg): it takes the batch when its messages lie back to back
+// (off[i+1] = off[i] + len[i]) and mostly at least 64 B long, and raises a
+// device flag otherwise, on which k_crc_grp + k_crc_any run as before.  The
+// decision is made on the device (no host sync); the workspace comes from the
+// stream-ordered allocator.  The span is bounded by the allocation holding
+// `base` (a batch reaching past it is not packed for the stream).
+uint64_t seg_min_msgs() {
+  const char *v = std::getenv("HC_SEG_MIN_MSGS");
+  return v && *v ? std::strtoull(v, nullptr, 10) : (1ull << 17);
+}
+
 int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
              uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t *bitmap, int64_t *first_bad,
-             uint32_t flags, hipStream_t s, uint64_t bytes_hint) {
+             uint32_t flags, hipStream_t s, uint64_t bytes_hint, bool seg_ok = false) {
   DeviceState &d = g_dev[dev];
   Batch b{};
   b.base = base;
@@ -161,11 +200,26 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       info.general_blocks = n;
     }
   } else {
+    uint32_t *seg_ws = nullptr;
+    if (seg_ok && (flags & kFlagMessages) && off && len && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
+      hipDeviceptr_t pb = nullptr;
+      size_t ps = 0;
+      if (hipMemGetAddressRange(&pb, &ps, const_cast<uint8_t *>(base)) == hipSuccess && ps) {
+        const uint64_t lo = reinterpret_cast<uintptr_t>(base) & ~uint64_t(1023);
+        const uint64_t mu = seg_max_units(reinterpret_cast<uintptr_t>(pb) + ps - lo);
+        if (hipMallocAsync(reinterpret_cast<void **>(&seg_ws), seg_workspace_bytes(n, mu), s) != hipSuccess)
+          seg_ws = nullptr;
+        else if ((e = launch_seg(b, d.dseg, seg_ws, mu, fast_grid, s, d.seg_last)) == hipSuccess)
+          b.seg_flag = seg_ws;  // word 0: raised when the stream did not take the batch
+      }
+    }
     // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk
     // size, utils/config/config.go:137); the k_crc_any sweep does the rest
-    e = launch_grp(b, fast_grid, s);
+    if (e == hipSuccess) e = launch_grp(b, fast_grid, s);
     if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
-    info.kernel = "k_crc_grp+k_crc_any";
+    if (seg_ws && hipFreeAsync(seg_ws, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;
+    info.kernel = b.seg_flag ? "k_seg_stream|k_crc_grp+k_crc_any" : "k_crc_grp+k_crc_any";
+    t_seg_dev = b.seg_flag ? dev : -1;
     info.fast_blocks = n;  // routing is decided on the device per block
   }
   t_last = info;
@@ -862,7 +916,7 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
   DeviceGuard g(device);
   uint64_t bytes = (!off && !len) ? nblocks * (uint64_t)ulen : 0;
   return dispatch(device, static_cast<const uint8_t *>(base), off, len, stride, ulen, nblocks, crc_out,
-                  bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes);
+                  bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes, true);
 }
 
 uint64_t hc_read_blocks_touched(uint32_t block_size, uint64_t start_offset, uint64_t size) {
@@ -1072,6 +1126,17 @@ int hc_last_launch(hc_launch_info *info) {
   if (!info) return HC_E_ARG;
   *info = t_last;
   return HC_OK;
+}
+
+int hc_debug_seg_taken(void) {
+  const int dev = t_seg_dev;
+  if (dev < 0) return 0;
+  DeviceGuard g(dev);
+  uint32_t v = 0;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&v, g_dev[dev].seg_last, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return HC_E_HIP;
+  return v ? 1 : 0;
 }
 
 int hc_debug_tables(void *out, size_t cap) {

@@ -91,4 +91,86 @@ inline void build_device_tables(DeviceTables &d) {
   for (auto &p : d.pad) p = 0;
 }
 
+// 32x32 GF(2) matrix by columns: c[i] = M e_i (host side only).
+struct Mat32 {
+  uint32_t c[32];
+};
+inline uint32_t mat_apply(const Mat32 &m, uint32_t v) {
+  uint32_t r = 0;
+  for (int i = 0; i < 32; i++)
+    if ((v >> i) & 1u) r ^= m.c[i];
+  return r;
+}
+inline Mat32 mat_mul(const Mat32 &a, const Mat32 &b) {  // a o b
+  Mat32 r;
+  for (int i = 0; i < 32; i++) r.c[i] = mat_apply(a, b.c[i]);
+  return r;
+}
+inline Mat32 mat_inverse(const Mat32 &m) {  // Gauss-Jordan on [M | I]
+  uint32_t row[32], inv[32];
+  for (int r = 0; r < 32; r++) {
+    row[r] = 0;
+    for (int i = 0; i < 32; i++) row[r] |= ((m.c[i] >> r) & 1u) << i;
+    inv[r] = 1u << r;
+  }
+  for (int c = 0; c < 32; c++) {
+    int p = c;
+    while (p < 32 && !((row[p] >> c) & 1u)) p++;
+    if (p == 32) continue;  // singular: never, x is invertible mod P
+    uint32_t t = row[p]; row[p] = row[c]; row[c] = t;
+    t = inv[p]; inv[p] = inv[c]; inv[c] = t;
+    for (int r = 0; r < 32; r++)
+      if (r != c && ((row[r] >> c) & 1u)) {
+        row[r] ^= row[c];
+        inv[r] ^= inv[c];
+      }
+  }
+  Mat32 out;  // inv as rows -> columns
+  for (int i = 0; i < 32; i++) {
+    out.c[i] = 0;
+    for (int r = 0; r < 32; r++) out.c[i] |= ((inv[r] >> i) & 1u) << r;
+  }
+  return out;
+}
+inline Mat32 shift_mat(const Gf2 &g, uint64_t n) {
+  Mat32 m;
+  for (int i = 0; i < 32; i++) m.c[i] = g.shift_bytes(1u << i, n);
+  return m;
+}
+
+// Constant image of the packed-record path (k_seg_*; 164 KiB, global memory):
+//   pw[k][j][b]  = shift(b << 8j, 1024 * 2^k)     shift by whole rows
+//   inv[k][j][b] = shift^-1(b << 8j, 2^k)          inverse shift by bytes
+//   ones[d-1]    = shift(0xFFFFFFFF, d), d = 1..1024
+constexpr int kSegPw = 29;   // rows up to 2^29 (2^39 bytes)
+constexpr int kSegInv = 11;  // byte distances 1 .. 1024
+struct SegTables {
+  uint32_t pw[kSegPw][4][256];
+  uint32_t inv[kSegInv][4][256];
+  uint32_t ones[1024];
+};
+
+inline void build_seg_tables(SegTables &t) {
+  Gf2 g;
+  auto fill = [](uint32_t (&tab)[4][256], const Mat32 &m) {
+    for (int j = 0; j < 4; j++)
+      for (uint32_t b = 0; b < 256; b++) tab[j][b] = mat_apply(m, b << (8 * j));
+  };
+  Mat32 m = shift_mat(g, kRowBytes);
+  for (int k = 0; k < kSegPw; k++) {
+    fill(t.pw[k], m);
+    m = mat_mul(m, m);
+  }
+  Mat32 v = mat_inverse(shift_mat(g, 1));
+  for (int k = 0; k < kSegInv; k++) {
+    fill(t.inv[k], v);
+    v = mat_mul(v, v);
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (int d = 1; d <= 1024; d++) {
+    c = g.shift_bytes(c, 1);
+    t.ones[d - 1] = c;
+  }
+}
+
 }  // namespace hc

@@ -518,9 +518,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
                                                          uint32_t lg_chunk, uint32_t *__restrict__ crc_out,
                                                          uint32_t *__restrict__ bad_bitmap,
                                                          unsigned long long *__restrict__ first_bad,
-                                                         const DeviceTables *__restrict__ tables) {
+                                                         const DeviceTables *__restrict__ tables,
+                                                         const uint32_t *__restrict__ seg_flag = nullptr) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
+  if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   const uint32_t *tg = &tables->tg[0][0];
@@ -819,9 +821,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
-    unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
+    unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
+    const uint32_t *__restrict__ seg_flag = nullptr) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;
+  if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = uni(tid >> 6);
   const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
@@ -1683,6 +1687,451 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
   if (i == 0 && first_bad) *first_bad = (unsigned long long)LLONG_MAX;
 }
 
+// ---------------------------------------------------------------------------
+// Packed whole-message batches (records back to back: off[i+1] = off[i] +
+// len[i], GetCRC of each; config 5's per-record variant) by ONE stream over
+// their span instead of one wave per record.  With G(x) = raw(A0 .. x) over the
+// span from the 1 KiB-aligned origin A0, every record [a, b) is
+//     ChecksumIEEE = G(b) ^ shift(G(a) ^ ~0, b - a) ^ ~0,
+// so the stream only has to leave G at the record boundaries ("events").
+//   k_seg_plan     events -> first event of every 16 KiB unit; checks that the
+//                  batch is packed (else a flag sends it to k_crc_any)
+//   k_seg_stream   k_crc_grp's rows, groups and hand-out over the span's units;
+//                  per unit its raw CRC, and at every row holding events
+//                  H(x) = shift(raw(unit .. x), re - x) (re = the row's end):
+//                  the row start's value from the Horner streams, the row's
+//                  bytes before x placed at the row end (lane placement of the
+//                  whole lane chunks before x by an exclusive XOR scan, of the
+//                  event's own lane chunk masked at x)
+//   k_seg_scan_*   G at every unit start (prefix within blocks of 1024 units,
+//                  over the blocks, then per unit)
+//   k_seg_combine  per event: G(x) advanced to its row end = K(x) =
+//                  shift(G(unit), re - unit) ^ H(x); per record
+//                  shift(crc ^ ~0, re_b - b) = K(b) ^ shift(K(a) ^ shift(~0, re_a - a), re_b - re_a)
+//                  and one inverse shift by re_b - b (SegTables).
+constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups
+constexpr uint32_t kSegScanLg = 10;  // units per scan block
+
+struct SegGeo {
+  uint64_t a0, pend, units;
+};
+__device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *offs, const uint32_t *lens,
+                                          uint64_t n) {
+  SegGeo g;
+  g.a0 = ((uint64_t)base + offs[0]) & ~1023ull;
+  g.pend = (uint64_t)base + offs[n - 1] + lens[n - 1];
+  g.units = ((g.pend - g.a0) >> kSegUnitLg) + 1;
+  return g;
+}
+
+// shift by a byte-table multiply (4 lookups in a SegTables table)
+__device__ __forceinline__ uint32_t seg_tmul(const uint32_t (*t)[256], uint32_t v) {
+  return xor3(t[0][v & 255u], t[1][(v >> 8) & 255u], t[2][(v >> 16) & 255u]) ^ t[3][v >> 24];
+}
+// Events: position j = base + off[j] (j < n) and the span's end (j = n).
+// first_ev[u] = first event in unit u (u = 0 .. units; first_ev[units] = n + 1).
+// The flag is raised when the batch is not packed, exceeds max_units, or has
+// more than 64 events in one 4 KiB group (records under ~64 B: k_crc_any).
+__global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                  const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
+                                                  uint32_t *__restrict__ flag, uint32_t *__restrict__ first_ev) {
+  const SegGeo g = seg_geo(base, offs, lens, n);
+  bool bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= n && !bad; j += step) {
+    const uint64_t pj = j < n ? (uint64_t)base + offs[j] : g.pend;
+    uint64_t ulo = 0;
+    if (j > 0) {
+      const uint64_t pp = (uint64_t)base + offs[j - 1];
+      if ((j < n && offs[j] != offs[j - 1] + lens[j - 1]) || pj < pp) bad = true;
+      ulo = ((pp - g.a0) >> kSegUnitLg) + 1;
+    }
+    if (j >= 64 && ((pj - g.a0) >> 12) == (((uint64_t)base + offs[j - 64] - g.a0) >> 12)) bad = true;
+    const uint64_t uj = (pj - g.a0) >> kSegUnitLg;
+    if (uj >= g.units || pj < g.a0) bad = true;
+    if (bad) break;
+    for (uint64_t u = ulo; u <= uj; u++) first_ev[u] = (uint32_t)j;
+    if (j == n)
+      for (uint64_t u = uj + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(n + 1);
+  }
+  if (__ballot(bad)) lane0_atomic_or(flag, 1u);
+}
+
+template <bool kNull = false>
+__global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                            const uint32_t *__restrict__ lens, uint64_t n,
+                                                            uint32_t lg_chunk, const uint32_t *__restrict__ flag,
+                                                            const uint32_t *__restrict__ first_ev,
+                                                            uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
+                                                            const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
+  __shared__ uint32_t s_next;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) = make_uint4(v, v, v, v);
+  }
+  if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  __syncthreads();
+  if (*flag) return;  // not a packed batch: k_crc_any takes it
+
+  const uint32_t r4 = (lane & 31u) << 2;
+  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
+  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (kNull) return c ^ w;
+    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
+    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
+    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
+    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
+    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
+    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
+    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  // lane chunk (4 words) -> its raw CRC placed at the row end
+  auto place = [&](uint32_t a, uint32_t b_, uint32_t c, uint32_t d) -> uint32_t {
+    return matvec32(col, shift4(shift4(shift4(a, b_), c), d));
+  };
+
+  const uint32_t wave = uni(tid >> 6);
+  const uint32_t slot = kFastLdsBytes / 4 + wave * 64;  // lds[slot + l]: event -> lane routing
+  // (relaxed wavefront-scope atomics: ds_write/ds_read in program order, never
+  // forwarded by the compiler across the other lanes' writes)
+  auto slot_st = [&](uint32_t l, uint32_t v) {
+    __hip_atomic_store(&lds[slot + l], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  };
+  const SegGeo geo = seg_geo(base, offs, lens, n);
+  const uint64_t M = geo.units;
+  const uint64_t rhi = (geo.pend + 15) & ~15ull;  // loads past the span's last chunk return zeros
+  const uint64_t G = gridDim.x;
+  // chunks of 2^lg_chunk units (128 = 2 MiB best, profiles/r2/seg/), fewer
+  // for short spans: every workgroup gets at least 4 chunks
+  while (lg_chunk > 0 && (M >> lg_chunk) < G * 4) lg_chunk--;
+  const uint32_t cmask = (1u << lg_chunk) - 1u;
+  auto unit_of = [&](uint32_t k) -> uint64_t {
+    return (((uint64_t)(k >> lg_chunk) * G + blockIdx.x) << lg_chunk) | (k & cmask);
+  };
+  auto unit_rsrc = [&](uint64_t u) {
+    const uint64_t U = geo.a0 + (u << kSegUnitLg);
+    const uint64_t avail = u < M && rhi > U ? rhi - U : 0;
+    return buf_range(reinterpret_cast<const void *>(U), (uint32_t)(avail < (1u << kSegUnitLg) ? avail : (1u << kSegUnitLg)));
+  };
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  // window: the positions of events f .. f+63, one per lane (a group holds at most 64)
+  auto win_issue = [&](uint64_t f) -> u32x2 {
+    const uint64_t fc = f < n ? f : n;
+    const uint64_t cnt = n - fc;
+    const __amdgpu_buffer_rsrc_t r = buf_range(offs + fc, (uint32_t)(cnt < 64 ? cnt * 8 : 512));
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, 0, 0));
+  };
+  auto win_pos = [&](u32x2 v, uint64_t f) -> uint64_t {
+    const uint64_t j = f + lane;
+    return j < n ? (uint64_t)base + (((uint64_t)v.y << 32) | v.x) : j == n ? geo.pend : ~0ull;
+  };
+
+  uint64_t u = unit_of(wave);
+  if (u >= M) return;
+  uint64_t un = unit_of(kFastWaves + wave);
+  uint32_t kv = 0;  // VGPR: the LDS hand-out result, read one unit later
+  if (lane == 0) kv = atomicAdd(&s_next, 1u);
+  uint64_t wfirst = first_ev[u];
+  u32x2 wraw = win_issue(wfirst);
+  __amdgpu_buffer_rsrc_t rc = unit_rsrc(u);
+  uint4 q0 = buf_load16(rc, lane * 16u), q1 = buf_load16(rc, 1024u + lane * 16u),
+        q2 = buf_load16(rc, 2048u + lane * 16u), q3 = buf_load16(rc, 3072u + lane * 16u);
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, g = 0;
+
+  // H at the events of the row starting at rs (uniform mask evm of window
+  // lanes), from the streams c with the row already folded in: H(x) is the
+  // finalize of the row folded with its bytes from x on zeroed, i.e. of
+  // c ^ (w & ~m_x).  Rows with 1-2 events: one finalize per event.  More: the
+  // lane-parallel form H = F(re) ^ R ^ X_L ^ Epre_L with E_l every lane chunk
+  // placed at the row end, X its exclusive XOR scan, R = the row's raw CRC and
+  // Epre_L the event lane's chunk cut at x, placed (one pass per event that
+  // shares a lane chunk with an earlier one).
+  auto keep = [](int q, int k) -> uint32_t {  // bytes of word k below byte q of the chunk
+    const int nb = q - 4 * k;
+    return nb >= 4 ? 0xFFFFFFFFu : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+  };
+  auto events = [&](const uint4 w, uint64_t rs, uint64_t wpos, uint64_t evm) {
+    if (__popcll(evm) <= 2) {
+      for (uint64_t m = evm; m; m &= m - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(m);
+        const uint32_t rel = uni((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wpos - rs), k));
+        const int L = (int)(rel >> 4), q = lane == (uint32_t)L ? (int)(rel & 15u) : lane < (uint32_t)L ? 16 : 0;
+        const uint32_t h = wave_xor(place(c0 ^ (w.x & ~keep(q, 0)), c1 ^ (w.y & ~keep(q, 1)),
+                                          c2 ^ (w.z & ~keep(q, 2)), c3 ^ (w.w & ~keep(q, 3))));
+        lane0_store_u32(ev_h + wfirst + k, h);
+      }
+      return;
+    }
+    const uint32_t fre = wave_xor(place(c0, c1, c2, c3));  // raw(unit .. re)
+    const uint32_t e = place(w.x, w.y, w.z, w.w);
+    uint32_t x = e;  // inclusive XOR scan over the lanes
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(x, d);
+      if (lane >= d) x ^= t;
+    }
+    const uint32_t base_h = fre ^ uni((uint32_t)__builtin_amdgcn_readlane((int)x, 63));  // F(re) ^ R
+    x ^= e;                                                                              // exclusive
+    const uint32_t rel = (uint32_t)(wpos - rs);  // event lanes: < 1024
+    const uint32_t L = rel >> 4;
+    const uint32_t Lp = __shfl_up(L, 1);
+    const uint64_t same = __ballot(lane > 0 && Lp == L) & evm & (evm << 1);
+    uint64_t rem = evm;
+    while (rem) {  // one pass per event sharing a lane chunk with an earlier one
+      const uint64_t sel = rem & ~((rem << 1) & same);
+      slot_st(lane, 0xFFFFFFFFu);
+      if ((sel >> lane) & 1u) slot_st(L, lane | ((rel & 15u) << 8));
+      const uint32_t sv = __hip_atomic_load(&lds[slot + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const bool has = sv != 0xFFFFFFFFu;
+      const int q = has ? (int)(sv >> 8) : 0;
+      const uint32_t ep = place(w.x & keep(q, 0), w.y & keep(q, 1), w.z & keep(q, 2), w.w & keep(q, 3));
+      lanes_store_u32(ev_h + wfirst + (sv & 255u), base_h ^ x ^ ep, __ballot(has));
+      rem &= ~sel;
+    }
+  };
+  auto row = [&](const uint4 w, uint64_t rs, uint64_t wpos) {
+    c0 = row_step(c0, w.x);
+    c1 = row_step(c1, w.y);
+    c2 = row_step(c2, w.z);
+    c3 = row_step(c3, w.w);
+    const uint64_t evm = __ballot(wpos >= rs && wpos < rs + 1024u);
+    if (evm) events(w, rs, wpos, evm);
+    // the row is done here, before its refill (else its folds sink past the
+    // event branch's join and the refill needs a fresh register: see pin below)
+    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
+  };
+
+  for (;;) {
+    const uint64_t gs = geo.a0 + (u << kSegUnitLg) + ((uint64_t)g << 12);
+    const uint64_t wpos = win_pos(wraw, wfirst);
+    const bool lastg = g == 3;
+    // the next group: this unit's, or unit un's first; its events' window
+    const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M]
+                              : wfirst + (uint64_t)__popcll(__ballot(wpos < gs + 4096u));
+    const __amdgpu_buffer_rsrc_t rn = lastg ? unit_rsrc(un) : rc;
+    const uint32_t no = lastg ? lane * 16u : ((g + 1) << 12) + lane * 16u;
+    // each refill pinned right after its row (as k_crc_grp's kPin): hipcc
+    // otherwise hoists it into a fresh register and copies that at the loop
+    // latch, which waits for the load (vmcnt(0))
+    auto pin = [] { __builtin_amdgcn_sched_barrier(0); };
+    wraw = win_issue(nf);
+    row(q0, gs, wpos);
+    pin();
+    q0 = buf_load16(rn, no);
+    pin();
+    row(q1, gs + 1024u, wpos);
+    pin();
+    q1 = buf_load16(rn, no + 1024u);
+    pin();
+    row(q2, gs + 2048u, wpos);
+    pin();
+    q2 = buf_load16(rn, no + 2048u);
+    pin();
+    row(q3, gs + 3072u, wpos);
+    pin();
+    q3 = buf_load16(rn, no + 3072u);
+    pin();
+    wfirst = nf;
+    if (lastg) {
+      lane0_store_u32(unit_raw + u, wave_xor(place(c0, c1, c2, c3)));
+      if (un >= M) return;
+      u = un;
+      rc = rn;
+      g = 0;
+      c0 = c1 = c2 = c3 = 0;
+      un = unit_of(uni(kv));
+      if (lane == 0) kv = atomicAdd(&s_next, 1u);
+    } else {
+      g++;
+    }
+  }
+}
+
+// LDS copy of SegTables::pw[k0 .. k0+nk) at tl[0 ..) (1024 words per table)
+__device__ __forceinline__ void seg_lds_pw(uint32_t *tl, const SegTables *st, int k0, int nk) {
+  const uint32_t *src = &st->pw[k0][0][0];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)nk * 1024u; i += blockDim.x) tl[i] = src[i];
+}
+__device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) {
+  return xor3(t[v & 255u], t[256 + ((v >> 8) & 255u)], t[512 + ((v >> 16) & 255u)]) ^ t[768 + (v >> 24)];
+}
+
+// unit_incl[u] = raw of units [block start .. u] (blocks of 1024 units), and
+// blk_tot = each block's total: Hillis-Steele in LDS, persistent grid, the
+// shift tables (2^k units, k < 10) in LDS.
+__global__ __launch_bounds__(1024) void k_seg_scan_units(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ lens, uint64_t n,
+                                                         const uint32_t *__restrict__ flag,
+                                                         const uint32_t *__restrict__ unit_raw,
+                                                         uint32_t *__restrict__ unit_incl, uint32_t *__restrict__ blk_tot,
+                                                         const SegTables *__restrict__ st) {
+  constexpr int kPw0 = kSegUnitLg - 10;  // one unit = 2^4 rows
+  __shared__ uint32_t tl[kSegScanLg * 1024];
+  __shared__ uint32_t sv[1u << kSegScanLg];
+  seg_lds_pw(tl, st, kPw0, kSegScanLg);
+  __syncthreads();
+  if (*flag) return;
+  const SegGeo geo = seg_geo(base, offs, lens, n);
+  const uint32_t t = threadIdx.x;
+  for (uint64_t b = blockIdx.x; (b << kSegScanLg) < geo.units; b += gridDim.x) {
+    const uint64_t u = (b << kSegScanLg) + t;
+    uint32_t v = u < geo.units ? unit_raw[u] : 0u;
+    for (uint32_t k = 0; k < kSegScanLg; k++) {
+      sv[t] = v;
+      __syncthreads();
+      if (t >= (1u << k)) v ^= seg_lds_tmul(tl + k * 1024, sv[t - (1u << k)]);
+      __syncthreads();
+    }
+    if (u < geo.units) unit_incl[u] = v;
+    if (t == (1u << kSegScanLg) - 1) blk_tot[b] = v;
+  }
+}
+
+// blk_pre[b] = raw(A0 .. block b's first unit): one workgroup, runs of
+// consecutive blocks per thread, Hillis-Steele over the run totals (the
+// tables of 2^14 .. 2^28 rows in LDS).
+__global__ __launch_bounds__(1024) void k_seg_scan_blocks(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                          const uint32_t *__restrict__ lens, uint64_t n,
+                                                          const uint32_t *__restrict__ flag,
+                                                          const uint32_t *__restrict__ blk_tot,
+                                                          uint32_t *__restrict__ blk_pre,
+                                                          const SegTables *__restrict__ st) {
+  constexpr int kBlkPw = (int)(kSegUnitLg - 10 + kSegScanLg);  // one block = 2^14 rows
+  __shared__ uint32_t tl[(kSegPw - kBlkPw) * 1024];
+  __shared__ uint32_t sv[1024];
+  seg_lds_pw(tl, st, kBlkPw, kSegPw - kBlkPw);
+  __syncthreads();
+  if (*flag) return;
+  const SegGeo geo = seg_geo(base, offs, lens, n);
+  const uint64_t nb = (geo.units + (1u << kSegScanLg) - 1) >> kSegScanLg;
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint32_t t = threadIdx.x;
+  const uint64_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
+  auto shift_blocks = [&](uint32_t v, uint64_t blocks) {
+    for (int k = 0; blocks; k++, blocks >>= 1)
+      if (blocks & 1u) v = seg_lds_tmul(tl + k * 1024, v);
+    return v;
+  };
+  uint32_t v = 0;
+  for (uint64_t i = lo; i < hi; i++) v = seg_lds_tmul(tl, v) ^ blk_tot[i];
+  for (uint32_t k = 0; k < 10; k++) {
+    sv[t] = v;
+    __syncthreads();
+    if (t >= (1u << k)) v ^= shift_blocks(sv[t - (1u << k)], per << k);
+    __syncthreads();
+  }
+  sv[t] = v;
+  __syncthreads();
+  uint32_t p = t ? sv[t - 1] : 0u;
+  for (uint64_t i = lo; i < hi; i++) {
+    blk_pre[i] = p;
+    p = seg_lds_tmul(tl, p) ^ blk_tot[i];
+  }
+}
+
+// unit_g[u] = G(unit u's start) = shift(blk_pre[b], i units) ^ unit_incl[u - 1]
+// (u = 1024 b + i; written over unit_raw), persistent grid, tables in LDS.
+__global__ __launch_bounds__(1024) void k_seg_scan_final(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ lens, uint64_t n,
+                                                         const uint32_t *__restrict__ flag,
+                                                         const uint32_t *__restrict__ unit_incl,
+                                                         const uint32_t *__restrict__ blk_pre, uint32_t *__restrict__ unit_g,
+                                                         const SegTables *__restrict__ st) {
+  constexpr int kPw0 = kSegUnitLg - 10;
+  __shared__ uint32_t tl[kSegScanLg * 1024];
+  seg_lds_pw(tl, st, kPw0, kSegScanLg);
+  __syncthreads();
+  if (*flag) return;
+  const SegGeo geo = seg_geo(base, offs, lens, n);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < geo.units;
+       u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = (uint32_t)(u & ((1u << kSegScanLg) - 1));
+    uint32_t v = blk_pre[u >> kSegScanLg];
+#pragma unroll
+    for (int k = 0; k < (int)kSegScanLg; k++)
+      if ((i >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
+    if (i) v ^= unit_incl[u - 1];
+    unit_g[u] = v;
+  }
+}
+
+// Per event x (1024 per workgroup pass, persistent grid, two workgroups per
+// CU) K(x) = shift(G(x), re - x) = shift(G(U), re - U) ^ H(x) (re - U: 1 .. 16
+// rows), then per record [a, b) from K(a), K(b) (LDS exchange).  The tables of
+// row shifts up to 63 rows and every inverse byte shift in LDS (< 80 KiB).
+__global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                      const uint32_t *__restrict__ lens, uint64_t n,
+                                                      const uint32_t *__restrict__ flag,
+                                                      const uint32_t *__restrict__ unit_g,
+                                                      const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
+                                                      const SegTables *__restrict__ st, uint32_t *__restrict__ taken) {
+  constexpr int kPwL = 6, kInv0 = kPwL * 1024;
+  __shared__ uint32_t tl[(kPwL + kSegInv) * 1024];
+  __shared__ uint32_t sk[1025], sre[1025];  // K and the row end (in rows from A0) per event
+  seg_lds_pw(tl, st, 0, kPwL);
+  for (uint32_t i = threadIdx.x; i < kSegInv * 1024; i += blockDim.x) tl[kInv0 + i] = (&st->inv[0][0][0])[i];
+  if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
+  __syncthreads();
+  if (*flag) return;
+  const SegGeo geo = seg_geo(base, offs, lens, n);
+  auto rel = [&](uint64_t j) -> uint64_t { return (j < n ? (uint64_t)base + offs[j] : geo.pend) - geo.a0; };
+  auto K = [&](uint64_t j, uint32_t &re_rows) -> uint32_t {
+    const uint64_t x = rel(j), u = x >> kSegUnitLg;
+    re_rows = (uint32_t)(x >> 10) + 1u;
+    const uint32_t r = re_rows - (uint32_t)(u << (kSegUnitLg - 10));  // 1 .. 16 rows
+    uint32_t v = unit_g[u];
+#pragma unroll
+    for (int k = 0; k <= (int)(kSegUnitLg - 10); k++)
+      if ((r >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
+    return v ^ ev_h[j];
+  };
+  const uint32_t t = threadIdx.x;
+  for (uint64_t c = (uint64_t)blockIdx.x << 10; c < n; c += (uint64_t)gridDim.x << 10) {
+    const uint64_t j = c + t;
+    if (j <= n) sk[t] = K(j, sre[t]);
+    if (t == 0 && c + 1024 <= n) sk[1024] = K(c + 1024, sre[1024]);
+    __syncthreads();
+    if (j < n) {
+      const uint32_t ra = sre[t], rb = sre[t + 1];
+      const uint32_t da = (uint32_t)(((uint64_t)ra << 10) - rel(j)), db = (uint32_t)(((uint64_t)rb << 10) - rel(j + 1));
+      uint32_t v = sk[t] ^ st->ones[da - 1];  // K(a) ^ shift(~0, d_a), advanced to re_b
+      uint32_t rows = rb - ra;
+#pragma unroll
+      for (int k = 0; k < kPwL; k++)
+        if ((rows >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
+      rows >>= kPwL;
+      for (int k = kPwL; rows; k++, rows >>= 1)
+        if (rows & 1u) v = seg_tmul(st->pw[k], v);
+      uint32_t y = sk[t + 1] ^ v;
+#pragma unroll
+      for (int k = 0; k < kSegInv; k++)
+        if ((db >> k) & 1u) y = seg_lds_tmul(tl + kInv0 + k * 1024, y);
+      crc_out[j] = y ^ 0xFFFFFFFFu;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s) {
@@ -1710,7 +2159,7 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
 // static contiguous runs per wave (round 1; kept for A/B)
 hipError_t launch_general_static(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_any<4, 3>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                     b.ulen, b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+                     b.ulen, b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
   return hipGetLastError();
 }
 
@@ -1721,10 +2170,10 @@ hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipS
   // ones, profiles/r2/any_small_lanes/); block mode keeps the leaner build
   if (b.flags & kFlagMessages)
     hipLaunchKernelGGL((k_crc_any<4, 19, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
   else
     hipLaunchKernelGGL((k_crc_any<4, 3, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
   return hipGetLastError();
 }
 
@@ -1764,7 +2213,7 @@ hipError_t launch_grp(const Batch &b, int grid, hipStream_t s) {
   if (b.off || b.len)
     hipLaunchKernelGGL((k_crc_grp<true, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
                        b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,
-                       b.tables);
+                       b.tables, b.seg_flag);
   else if (grp_xcd(b.ulen, grid, b.nblocks))  // each XCD's workgroups own neighbouring chunk slots
     hipLaunchKernelGGL((k_crc_grp<false, true, false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s,
                        b.base, b.off, b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap,
@@ -1807,6 +2256,36 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                        uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s, uint64_t first) {
   hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, s, base, off, len, stride, ulen, n, seed, first);
+  return hipGetLastError();
+}
+
+uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
+
+uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
+  const uint64_t nb = (max_units >> kSegScanLg) + 1;
+  return 4 * (64 + (max_units + 1) + 2 * max_units + 2 * nb + n + 1);
+}
+
+hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
+                      uint32_t *taken) {
+  if (!b.base || !b.off || !b.len || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages)) return hipErrorInvalidValue;
+  const uint64_t n = b.nblocks, nb = (max_units >> kSegScanLg) + 1;
+  uint32_t *flag = ws, *first_ev = ws + 64, *unit_raw = first_ev + max_units + 1, *unit_incl = unit_raw + max_units,
+           *blk_tot = unit_incl + max_units, *blk_pre = blk_tot + nb, *ev_h = blk_pre + nb;
+  hipError_t e = hipMemsetAsync(flag, 0, 4, s);
+  if (e != hipSuccess) return e;
+  const uint64_t pg = (n + 256) / 256;
+  hipLaunchKernelGGL(k_seg_plan, dim3((unsigned)(pg < 16384 ? pg : 16384)), dim3(256), 0, s, b.base, b.off, b.len, n,
+                     max_units, flag, first_ev);
+  hipLaunchKernelGGL(k_seg_stream<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, 7u, flag,
+                     first_ev, unit_raw, ev_h, b.tables);
+  hipLaunchKernelGGL(k_seg_scan_units, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, unit_incl,
+                     blk_tot, st);
+  hipLaunchKernelGGL(k_seg_scan_blocks, dim3(1), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, blk_tot, blk_pre, st);
+  hipLaunchKernelGGL(k_seg_scan_final, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_incl, blk_pre,
+                     unit_raw, st);  // G per unit, over the raw words
+  hipLaunchKernelGGL(k_seg_combine, dim3(2 * grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
+                     b.crc_out, st, taken);
   return hipGetLastError();
 }
 

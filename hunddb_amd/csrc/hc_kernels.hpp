@@ -26,6 +26,9 @@ struct Batch {
   uint32_t *bad_bitmap;           // optional (verify)
   unsigned long long *first_bad;  // optional (verify), INT64_MAX when clean
   const DeviceTables *tables;
+  // optional: the flag of a packed-record stream launched before (launch_seg);
+  // k_crc_grp / k_crc_any do nothing when it is 0 (the stream took the batch)
+  const uint32_t *seg_flag;
 };
 
 // Streaming kernel geometry (one workgroup per CU; see DESIGN.md "Kernel").
@@ -74,6 +77,17 @@ uint64_t md5_workspace_bytes(uint64_t n);
 hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s);
 hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
+// Packed whole-message batches (off[i+1] = off[i] + len[i], HC_F_MESSAGES) as
+// one stream over their span (k_seg_*, hc_kernels.hip).  max_units bounds the
+// span's 16 KiB units (seg_max_units of a byte bound on the span); ws holds
+// seg_workspace_bytes(n, max_units) bytes.  A batch that is not packed, is
+// larger than the bound or holds records under ~64 B raises ws[0] on the
+// device and writes nothing (k_crc_any's launch then takes it).
+uint64_t seg_max_units(uint64_t span_bound);
+uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
+// taken (optional, device word): 1 when the stream took the batch, else 0.
+hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
+                      uint32_t *taken = nullptr);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
                                  hipStream_t s);
 

@@ -279,6 +279,12 @@ int hc_last_launch(hc_launch_info *info);
  * into out (returns HC_OK) or, if cap is too small, return its size. */
 int hc_debug_tables(void *out, size_t cap);
 
+/* 1 if this thread's last device batch of packed whole messages was hashed by
+ * the packed-record stream (k_seg_*), 0 if it fell back to
+ * k_crc_any on the device or was not offered to the stream; synchronizes that
+ * device (tests and tools only). */
+int hc_debug_seg_taken(void);
+
 /* Number of visible gfx950 devices (0 if none; never initialises a context
  * on a machine without GPUs). */
 int hc_device_count(void);

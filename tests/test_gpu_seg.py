@@ -1,0 +1,160 @@
+"""Packed-record stream (k_seg_*): GetCRC of every record of a
+batch whose records lie back to back (config 5's per-record variant,
+crc_util.go:15-17 per record), hashed as ONE stream over the span, against the
+oracle's restatement of Go's crc32.ChecksumIEEE; and the device-side fallback
+to k_crc_any for batches the stream does not take (gaps, overlaps, unsorted,
+runs of records under 64 B)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def packed(lens, start):
+    off = np.zeros(len(lens), dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return off + np.uint64(start)
+
+
+def run(torch, hc, buf, off, lens):
+    n = len(off)
+    out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
+    hc.dev_crc32_blocks(buf, out, nblocks=n, off=doff, lens=dlen, flags=hc.HC_F_MESSAGES)
+    torch.cuda.synchronize()
+    return u32(out), hc.seg_taken()
+
+
+@pytest.fixture
+def seg_all(monkeypatch):
+    monkeypatch.setenv("HC_SEG_MIN_MSGS", "1")  # offer every message batch to the stream
+
+
+def check(torch, hc, oracle, host, buf, off, lens, taken):
+    got, was = run(torch, hc, buf, off, lens)
+    want = oracle.crc32_messages(host, off, lens.astype(np.uint32), threads=16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:8], lens[bad[:8]], off[bad[:8]])
+    assert was == taken
+    return got
+
+
+@pytest.mark.parametrize("start", [0, 1, 1023, 1024, 4093, 16384 - 5])
+def test_seg_log_uniform_records(cuda, hc, oracle, seg_all, start):
+    """Config 5b's law (log-uniform 64 B - 64 KiB), packed at several start
+    alignments (row, group and unit boundaries): taken by the stream, bit-exact."""
+    torch = cuda
+    rng = np.random.default_rng(start + 5)
+    n = 20_000
+    lens = (64.0 * np.exp(rng.random(n) * np.log(1024.0))).astype(np.uint64)
+    off = packed(lens, start)
+    total = int(off[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    assert int(off[-1] + lens[-1]) <= total
+    check(torch, hc, oracle, host, buf, off, lens, True)
+    assert hc.last_launch()["kernel"].startswith("k_seg_stream")
+
+
+def test_seg_boundaries_and_shapes(cuda, hc, oracle, seg_all):
+    """Records ending exactly on row / group / unit boundaries, empty records,
+    records of 64 B .. 1 MiB (spanning many units), one record, two records."""
+    torch = cuda
+    rng = np.random.default_rng(7)
+    total = 48 << 20
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    cases = [
+        np.array([1024] * 3000, dtype=np.uint64),                  # row-aligned ends
+        np.array([4096, 16384, 64, 1023, 1025, 16383, 16385] * 500, dtype=np.uint64),
+        np.array([3000, 0, 0, 2000, 0, 64, 0] * 1000, dtype=np.uint64),  # empty records
+        np.array([1 << 20] * 20 + [77] * 100, dtype=np.uint64),    # 1 MiB records
+        np.array([5000], dtype=np.uint64),
+        np.array([64, 65], dtype=np.uint64),
+        np.array([12345678], dtype=np.uint64),                      # one record over many units
+    ]
+    for i, lens in enumerate(cases):
+        for start in (0, 3, 1024 - 1):
+            off = packed(lens, start)
+            assert int(off[-1] + lens[-1]) <= total
+            check(torch, hc, oracle, host, buf, off, lens, True)
+
+
+def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
+    """Batches the stream does not take are hashed by k_crc_grp + k_crc_any
+    (the device flag): a gap, an overlap, unsorted records, and 65 events in
+    one 4 KiB group (records under 64 B)."""
+    torch = cuda
+    rng = np.random.default_rng(11)
+    total = 8 << 20
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    lens = rng.integers(64, 4000, 3000).astype(np.uint64)
+    off = packed(lens, 5)
+    g = off.copy()
+    g[1500:] += 1  # one byte gap
+    check(torch, hc, oracle, host, buf, g, lens, False)
+    o = off.copy()
+    o[700:] -= 1  # one byte overlap
+    check(torch, hc, oracle, host, buf, o, lens, False)
+    p = rng.permutation(len(off))
+    check(torch, hc, oracle, host, buf, off[p], lens[p], False)
+    dense = np.array([100, 0, 0, 200, 0, 64, 0] * 1000, dtype=np.uint64)  # empty records, dense
+    check(torch, hc, oracle, host, buf, packed(dense, 3), dense, False)
+    small = np.full(5000, 63, dtype=np.uint64)  # 65 events in a 4 KiB group
+    check(torch, hc, oracle, host, buf, packed(small, 0), small, False)
+    small[:] = 64  # exactly 64 per group: still the stream
+    check(torch, hc, oracle, host, buf, packed(small, 0), small, True)
+
+
+def test_seg_threshold(cuda, hc, oracle, monkeypatch):
+    """Below HC_SEG_MIN_MSGS (default 131072 messages) the batch is not offered
+    to the stream."""
+    torch = cuda
+    rng = np.random.default_rng(3)
+    lens = rng.integers(64, 3000, 5000).astype(np.uint64)
+    off = packed(lens, 0)
+    total = int(off[-1] + lens[-1])
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    monkeypatch.delenv("HC_SEG_MIN_MSGS", raising=False)
+    check(torch, hc, oracle, host, buf, off, lens, False)
+    assert hc.last_launch()["kernel"] == "k_crc_grp+k_crc_any"
+
+
+def test_seg_config5b_size(cuda, hc, oracle):
+    """Config 5's per-record variant at 2M records (18.9 GB) with the default
+    threshold: taken by the stream; the oracle checks a sample of 20k records
+    (every record of the first MiB, then random ones) and the words are
+    identical to k_crc_any's (the stream's fallback, forced by a gap)."""
+    torch = cuda
+    n = 2_000_000
+    rng = np.random.default_rng(55)
+    lens = (64.0 * np.exp(rng.random(n) * np.log(1024.0))).astype(np.uint64)
+    off = packed(lens, 1)
+    total = int(off[-1] + lens[-1]) + 64
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    hc.dev_fill_range(buf, 0x5B, 0, 1, stride=total, ulen=total)
+    got, was = run(torch, hc, buf, off, lens)
+    assert was
+    # oracle on 20k records of the first 512 MB (all of the first 200)
+    head = int(np.searchsorted(off, 512 << 20))
+    pick = np.unique(np.r_[np.arange(200), rng.choice(head, 20_000, replace=False)])
+    hi = int((off[pick] + lens[pick]).max())
+    sample = buf[:hi].cpu().numpy()
+    want = oracle.crc32_messages(sample, off[pick], lens[pick].astype(np.uint32), threads=16)
+    assert (got[pick] == want).all()
+    # every word against k_crc_any: the same records with the last one moved one
+    # byte up (a gap: not packed, so the device flag sends it to k_crc_any)
+    g = off.copy()
+    g[-1] += 1
+    l3 = lens.copy()
+    l3[-1] -= 1
+    got3, was3 = run(torch, hc, buf, g, l3)
+    assert not was3
+    assert (got3[:-1] == got[:-1]).all()

@@ -128,6 +128,16 @@ int main(int argc, char **argv) {
     b.len = dlen;
   }
   if (logu || mode == "eq9815") b.flags = hc::kFlagMessages;
+  hc::SegTables *seg_t;
+  CK(hipMalloc(&seg_t, sizeof(hc::SegTables)));
+  {
+    std::vector<hc::SegTables> h(1);
+    hc::build_seg_tables(h[0]);
+    CK(hipMemcpy(seg_t, h.data(), sizeof(hc::SegTables), hipMemcpyHostToDevice));
+  }
+  const uint64_t seg_mu = hc::seg_max_units(total + 1024);
+  uint32_t *seg_ws;
+  CK(hipMalloc(&seg_ws, hc::seg_workspace_bytes(N, seg_mu)));
   const uint32_t lg5 = 5;
   using namespace hc;
   std::vector<Variant> vs;
@@ -156,7 +166,22 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((k_crc_any<BATCH, VAR, true>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len, \
                        b.stride, b.ulen, b.flags, b.nblocks, 0u, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables); \
   }
-    add("any without small lanes (kVar 3)", true, ANYV(4, 3));
+    if (b.flags & kFlagMessages) {  // packed records: one stream over the span (k_seg_*)
+      add("SEG packed stream (6 launches)", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st); });
+#define SEGSTREAM(NUL, LG)                                                                                     \
+  [&](hipStream_t st) {                                                                                       \
+    hipLaunchKernelGGL(k_seg_stream<NUL>, dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len, b.nblocks, \
+                       (uint32_t)(LG), seg_ws, seg_ws + 64, seg_ws + 64 + seg_mu + 1,                             \
+                       seg_ws + 64 + 3 * seg_mu + 1 + 2 * ((seg_mu >> 10) + 1), b.tables);                         \
+  }
+      add("SEG k_seg_stream alone C=32", false, SEGSTREAM(false, 5));
+      add("SEG k_seg_stream NULL math C=32", false, SEGSTREAM(true, 5));
+      add("SEG k_seg_stream C=8", false, SEGSTREAM(false, 3));
+      add("SEG k_seg_stream C=16", false, SEGSTREAM(false, 4));
+      add("SEG k_seg_stream C=64", false, SEGSTREAM(false, 6));
+      add("SEG k_seg_stream C=128", false, SEGSTREAM(false, 7));
+      add("SEG k_seg_stream C=32 (again)", false, SEGSTREAM(false, 5));
+    }
     add("PROD launch_general (again)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
   } else if (!arrays) {
     add("PROD k_crc_uni", true, [&](hipStream_t st) { launch_uni(b, cus, st); });
@@ -243,6 +268,11 @@ int main(int argc, char **argv) {
     }
   }
   CK(hipStreamSynchronize(s));
+  if (b.flags & kFlagMessages) {
+    uint32_t fl = 0;
+    CK(hipMemcpy(&fl, seg_ws, 4, hipMemcpyDeviceToHost));
+    std::printf("seg flag (1 = not taken) = %u\n", fl);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
