@@ -66,8 +66,13 @@ WORKLOADS = {
     # verify mode (CheckBlockIntegrity over the north-star batch, stamped): read B,
     # compare, write the 4-B word + bitmap bits; SURVEY 8(d) counts B + 4 per block
     "verify": (1_000_000, "verify", "weak"),
+    # configs[4]'s per-record variant on the device (SURVEY 8(d) config 5 notes):
+    # GetCRC of 2M records, log-uniform 64 B - 64 KiB, back to back at an odd
+    # address (18.9 GB) -> the packed-record stream (k_seg_*); bytes = record
+    # bytes read + 4-B words written
+    "records": (2_000_000, "records", "weak"),
 }
-KERNEL_RE = {"frame": "k_frame", "unframe": "k_unframe"}  # else the streaming CRC kernel
+KERNEL_RE = {"frame": "k_frame", "unframe": "k_unframe", "records": "k_seg_stream"}  # else the streaming CRC kernel
 
 
 def parse(argv=None):
@@ -177,9 +182,24 @@ def cpu_host():
     return {"cpu_model": model, "nproc": os.cpu_count()}
 
 
-def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None):
+def record_sizes(n):
+    """configs[4]'s record law: log-uniform in [64, 65536] B (u = splitmix64(0x5B,
+    i, 0) >> 11 / 2^53, tools/kbench2.hip's draw)."""
+    import numpy as np
+    i = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(0x5B) + (i << np.uint64(21)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(11)).astype(np.float64) / 9007199254740992.0
+    return (64.0 * np.exp(u * np.log(1024.0))).astype(np.uint32)
+
+
+def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None, messages=False):
     """Go's crc32.ChecksumIEEE over block[4:len] of every sample block
-    (crc_util.go:16,94), three ways: the oracle's restatement of Go's amd64
+    (crc_util.go:16,94; with messages: over each whole record, GetCRC
+    crc_util.go:15-17), three ways: the oracle's restatement of Go's amd64
     algorithm (oracle/hc_oracle.c oc_crc32_go_amd64: PCLMULQDQ fold + slicing-by-8)
     on `threads` threads (5 slices: median and spread) and on 1 thread, and
     system zlib's crc32 (Python zlib, an independent implementation) on 1 thread.
@@ -190,20 +210,24 @@ def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None):
 
     from oracle import oracle as O
     nbytes = int(lens.sum(dtype=np.uint64))
-    port = lambda t: O.crc32_blocks(sample, off=off, lens=lens, threads=t)  # noqa: E731
+    if messages:
+        port = lambda t: O.crc32_messages(sample, off, lens, threads=t)  # noqa: E731
+    else:
+        port = lambda t: O.crc32_blocks(sample, off=off, lens=lens, threads=t)  # noqa: E731
     words = port(threads)
     mv = memoryview(sample)
+    skip = 0 if messages else 4
     pairs = list(zip(off.tolist(), lens.tolist()))
 
     def zl():
         for o, n_ in pairs:
-            zlib.crc32(mv[o + 4:o + n_])
-    zl_ok = all(zlib.crc32(mv[o + 4:o + n_]) == int(words[k]) for k, (o, n_) in enumerate(pairs[:200]))
+            zlib.crc32(mv[o + skip:o + n_])
+    zl_ok = all(zlib.crc32(mv[o + skip:o + n_]) == int(words[k]) for k, (o, n_) in enumerate(pairs[:200]))
     slices = [_rate(lambda: port(threads), nbytes, 0.1 * budget_s) for _ in range(5)]
     one = _rate(lambda: port(1), nbytes, 0.25 * budget_s)
     zrate = _rate(zl, nbytes, 0.25 * budget_s)
     res = {"value": round(float(np.median(slices)), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-           "sample": f"{what}: {len(pairs)} blocks, {nbytes / 2**20:.0f} MiB copied from the GPU batch; "
+           "sample": f"{what}: {len(pairs)} {'records' if messages else 'blocks'}, {nbytes / 2**20:.0f} MiB copied from the GPU batch; "
                      f"oracle/hc_oracle.c oc_crc32_go_amd64 restates Go 1.23 hash/crc32 amd64 "
                      f"(PCLMULQDQ fold + slicing-by-8), pclmul={O.lib().oc_have_pclmul()}",
            "spread": [round(min(slices), 3), round(max(slices), 3)],
@@ -370,6 +394,21 @@ def main(argv=None):
         block_desc = "8192 B, verify mode (stamped; B read + 4 B written per block)"
         k = min(my, (512 << 20) // B)
         sample = (slice(0, k * B), np.arange(k, dtype=np.uint64) * B, np.full(k, B, np.uint32))
+    elif bsize == "records":
+        lens_h = record_sizes(my) if not args.blocks else record_sizes(nblk)[:my]
+        off_h = np.zeros(my, dtype=np.uint64)
+        off_h[1:] = np.cumsum(lens_h[:-1], dtype=np.uint64)
+        off_h += np.uint64(1)  # back to back from an odd address
+        total = (int(off_h[-1]) + int(lens_h[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        crc.dev_fill_range(buf, SEED, lo << 20, total >> 20, stride=1 << 20, ulen=1 << 20)
+        doff = torch.from_numpy(off_h.view(np.int64)).to(dev)
+        dlen = torch.from_numpy(lens_h.view(np.int32)).to(dev)
+        kw = dict(off=doff, lens=dlen, nblocks=my, flags=crc.HC_F_MESSAGES)
+        step_bytes = int(lens_h.sum(dtype=np.uint64)) + 4 * my
+        block_desc = "GetCRC per record: log-uniform 64 B - 64 KiB records back to back (off/len arrays)"
+        k = int(np.searchsorted(off_h, 512 << 20))
+        sample = (slice(0, int(off_h[k - 1]) + int(lens_h[k - 1])), off_h[:k].copy(), lens_h[:k].copy())
     elif bsize == "unframe":
         buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
         crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
@@ -436,6 +475,7 @@ def main(argv=None):
     step = make_step(buf, out, kw)
     dt, mean_kern_s = timed(step, args.steps, args.warmup, world > 1)
     info = crc.last_launch()
+    seg_taken = crc.seg_taken() if bsize == "records" else None
     verify_clean = None
     if bsize == "verify":  # every stamped block must have verified clean
         verify_clean = int(first_bad.item()) == 2**63 - 1 and int(bitmap.abs().sum().item()) == 0
@@ -494,6 +534,9 @@ def main(argv=None):
                 "mean_launch_ms": round(mean_kern_s * 1e3, 4),
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
+                **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + 3 scan/combine kernels "
+                                   "(+ a 4-B memset, stream-ordered workspace); traffic: k_seg_stream"}
+                   if bsize == "records" else {}),
                 "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
@@ -506,7 +549,8 @@ def main(argv=None):
                 host = buf[sl].cpu().numpy()
                 cpu = cpu_baseline(host, soff, slen, args.cpu_threads, args.cpu_seconds,
                                    f"{args.workload} ({block_desc})",
-                                   gpu_words=out[: len(soff)].cpu().numpy().view(np.uint32))
+                                   gpu_words=out[: len(soff)].cpu().numpy().view(np.uint32),
+                                   messages=bsize == "records")
         res = {
             "metric": "GiB/s CRC32 over device-resident batched 4/8/16 KB blocks; % HBM peak",
             "value": round(gib_s, 2),
@@ -525,7 +569,8 @@ def main(argv=None):
                        "parallelism": f"shard-by-block-index x{world}",
                        "dist_backend": backend if world > 1 else None,
                        "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4),
-                       **({"verify_clean": verify_clean} if verify_clean is not None else {})},
+                       **({"verify_clean": verify_clean} if verify_clean is not None else {}),
+                       **({"packed_stream_taken": seg_taken} if seg_taken is not None else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
