@@ -1757,7 +1757,9 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
   if (__ballot(bad)) lane0_atomic_or(flag, 1u);
 }
 
-template <bool kNull = false>
+// kNull (A/B only): rows XOR-folded instead of CRC'd; kNoEv (A/B only): no event
+// processing at all (the memory pattern alone)
+template <bool kNull = false, bool kNoEv = false>
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
                                                             uint32_t lg_chunk, const uint32_t *__restrict__ flag,
@@ -1909,16 +1911,23 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
       rem &= ~sel;
     }
   };
-  auto row = [&](const uint4 w, uint64_t rs, uint64_t wpos) {
+  // a row: fold it, issue its register's refill, then its events (from a copy
+  // of the row, so the wave keeps 4 loads in flight through the event work)
+  auto row = [&](uint4 &q, uint64_t rs, uint64_t wpos, __amdgpu_buffer_rsrc_t rn, uint32_t no) {
+    const uint4 w = q;
     c0 = row_step(c0, w.x);
     c1 = row_step(c1, w.y);
     c2 = row_step(c2, w.z);
     c3 = row_step(c3, w.w);
-    const uint64_t evm = __ballot(wpos >= rs && wpos < rs + 1024u);
-    if (evm) events(w, rs, wpos, evm);
-    // the row is done here, before its refill (else its folds sink past the
-    // event branch's join and the refill needs a fresh register: see pin below)
-    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
+    const uint64_t evm = kNoEv ? 0 : __ballot(wpos >= rs && wpos < rs + 1024u);
+    uint4 we = w;
+    // the folds complete before the refill (else they sink past the event
+    // branch's join and the refill needs a fresh register: see pin below)
+    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(we.x), "+v"(we.y), "+v"(we.z), "+v"(we.w));
+    __builtin_amdgcn_sched_barrier(0);
+    q = buf_load16(rn, no);
+    __builtin_amdgcn_sched_barrier(0);
+    if (evm) events(we, rs, wpos, evm);
   };
 
   for (;;) {
@@ -1930,27 +1939,14 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
                               : wfirst + (uint64_t)__popcll(__ballot(wpos < gs + 4096u));
     const __amdgpu_buffer_rsrc_t rn = lastg ? unit_rsrc(un) : rc;
     const uint32_t no = lastg ? lane * 16u : ((g + 1) << 12) + lane * 16u;
-    // each refill pinned right after its row (as k_crc_grp's kPin): hipcc
-    // otherwise hoists it into a fresh register and copies that at the loop
-    // latch, which waits for the load (vmcnt(0))
-    auto pin = [] { __builtin_amdgcn_sched_barrier(0); };
+    // each refill pinned right after its row's fold (as k_crc_grp's kPin):
+    // hipcc otherwise hoists it into a fresh register and copies that at the
+    // loop latch, which waits for the load (vmcnt(0))
     wraw = win_issue(nf);
-    row(q0, gs, wpos);
-    pin();
-    q0 = buf_load16(rn, no);
-    pin();
-    row(q1, gs + 1024u, wpos);
-    pin();
-    q1 = buf_load16(rn, no + 1024u);
-    pin();
-    row(q2, gs + 2048u, wpos);
-    pin();
-    q2 = buf_load16(rn, no + 2048u);
-    pin();
-    row(q3, gs + 3072u, wpos);
-    pin();
-    q3 = buf_load16(rn, no + 3072u);
-    pin();
+    row(q0, gs, wpos, rn, no);
+    row(q1, gs + 1024u, wpos, rn, no + 1024u);
+    row(q2, gs + 2048u, wpos, rn, no + 2048u);
+    row(q3, gs + 3072u, wpos, rn, no + 3072u);
     wfirst = nf;
     if (lastg) {
       lane0_store_u32(unit_raw + u, wave_xor(place(c0, c1, c2, c3)));
@@ -2277,7 +2273,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint64_t pg = (n + 256) / 256;
   hipLaunchKernelGGL(k_seg_plan, dim3((unsigned)(pg < 16384 ? pg : 16384)), dim3(256), 0, s, b.base, b.off, b.len, n,
                      max_units, flag, first_ev);
-  hipLaunchKernelGGL(k_seg_stream<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, 7u, flag,
+  hipLaunchKernelGGL((k_seg_stream<false, false>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, 7u, flag,
                      first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_scan_units, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, unit_incl,
                      blk_tot, st);

@@ -168,19 +168,17 @@ int main(int argc, char **argv) {
   }
     if (b.flags & kFlagMessages) {  // packed records: one stream over the span (k_seg_*)
       add("SEG packed stream (6 launches)", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st); });
-#define SEGSTREAM(NUL, LG)                                                                                     \
+#define SEGSTREAM(NUL, NOEV, LG)                                                                               \
   [&](hipStream_t st) {                                                                                       \
-    hipLaunchKernelGGL(k_seg_stream<NUL>, dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len, b.nblocks, \
-                       (uint32_t)(LG), seg_ws, seg_ws + 64, seg_ws + 64 + seg_mu + 1,                             \
+    hipLaunchKernelGGL((k_seg_stream<NUL, NOEV>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.off, b.len,  \
+                       b.nblocks, (uint32_t)(LG), seg_ws, seg_ws + 64, seg_ws + 64 + seg_mu + 1,                  \
                        seg_ws + 64 + 3 * seg_mu + 1 + 2 * ((seg_mu >> 10) + 1), b.tables);                         \
   }
-      add("SEG k_seg_stream alone C=32", false, SEGSTREAM(false, 5));
-      add("SEG k_seg_stream NULL math C=32", false, SEGSTREAM(true, 5));
-      add("SEG k_seg_stream C=8", false, SEGSTREAM(false, 3));
-      add("SEG k_seg_stream C=16", false, SEGSTREAM(false, 4));
-      add("SEG k_seg_stream C=64", false, SEGSTREAM(false, 6));
-      add("SEG k_seg_stream C=128", false, SEGSTREAM(false, 7));
-      add("SEG k_seg_stream C=32 (again)", false, SEGSTREAM(false, 5));
+      add("SEG k_seg_stream alone (C=128)", false, SEGSTREAM(false, false, 7));
+      add("SEG k_seg_stream NULL math", false, SEGSTREAM(true, false, 7));
+      add("SEG k_seg_stream no events", false, SEGSTREAM(false, true, 7));
+      add("SEG k_seg_stream NULL + no events", false, SEGSTREAM(true, true, 7));
+      add("SEG packed stream (again)", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st); });
     }
     add("PROD launch_general (again)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });
   } else if (!arrays) {
