@@ -1460,7 +1460,11 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
 // block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
 // overlapping lane 1's store with identical bytes.
-template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false>
+// kSt (A/B only, tools/kframe): 0 = each row stored before it is hashed
+// (production); 1 = each row stored after it is hashed; 2 = the group's four
+// rows hashed, then its four stores; 3 = production order with write-back
+// (not nt) stores.
+template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 0>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                            uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
@@ -1533,6 +1537,14 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
     const uint64_t b = p >> lg_groups;
     const uint32_t g = (uint32_t)p & gmask;
     uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
+    auto st16 = [&](u32x4 v, uint8_t *a) {
+      if constexpr (kSt == 3)
+        *reinterpret_cast<u32x4_u *>(a) = v;
+      else
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(a));
+    };
+    u32x4 sv[4];
+    uint8_t *sa[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       u32x4 v = cur[r];
@@ -1540,16 +1552,23 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
         const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v.x, 0x101, 0xF, 0xF, false);  // lane+1's x
         stored = __builtin_amdgcn_readfirstlane(v.x);                   // LE32(block[0:4])
         const u32x4 first = {v.y, v.z, v.w, nx};
-        const u32x4 sv = lane == 0 ? first : v;
-        __builtin_nontemporal_store(sv, reinterpret_cast<u32x4_u *>(ob + (lane == 0 ? 4 : 0)));
+        sv[r] = lane == 0 ? first : v;
+        sa[r] = ob + (lane == 0 ? 4 : 0);
         v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
       } else {
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(ob + r * kRowBytes));
+        sv[r] = v;
+        sa[r] = ob + r * kRowBytes;
       }
+      if constexpr (kSt == 0 || kSt == 3) st16(sv[r], sa[r]);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; k++)
         c[k] = (r == 0 && g == 0) ? w[k] : (kNull ? c[k] ^ w[k] : row_step(c[k], w[k]));
+      if constexpr (kSt == 1) st16(sv[r], sa[r]);
+    }
+    if constexpr (kSt == 2) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) st16(sv[r], sa[r]);
     }
     if (g == gmask) {
       uint32_t crcv;
@@ -2263,7 +2282,7 @@ uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken) {
+                      uint32_t *taken, uint32_t lg_chunk) {
   if (!b.base || !b.off || !b.len || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages)) return hipErrorInvalidValue;
   const uint64_t n = b.nblocks, nb = (max_units >> kSegScanLg) + 1;
   uint32_t *flag = ws, *first_ev = ws + 64, *unit_raw = first_ev + max_units + 1, *unit_incl = unit_raw + max_units,
@@ -2273,8 +2292,8 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint64_t pg = (n + 256) / 256;
   hipLaunchKernelGGL(k_seg_plan, dim3((unsigned)(pg < 16384 ? pg : 16384)), dim3(256), 0, s, b.base, b.off, b.len, n,
                      max_units, flag, first_ev);
-  hipLaunchKernelGGL((k_seg_stream<false, false>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, 7u, flag,
-                     first_ev, unit_raw, ev_h, b.tables);
+  hipLaunchKernelGGL((k_seg_stream<false, false>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
+                     flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_scan_units, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, unit_incl,
                      blk_tot, st);
   hipLaunchKernelGGL(k_seg_scan_blocks, dim3(1), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, blk_tot, blk_pre, st);

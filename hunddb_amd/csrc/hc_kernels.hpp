@@ -87,7 +87,7 @@ uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
 // taken (optional, device word): 1 when the stream took the batch, else 0.
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken = nullptr);
+                      uint32_t *taken = nullptr, uint32_t lg_chunk = 7);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
                                  hipStream_t s);
 

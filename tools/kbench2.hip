@@ -178,6 +178,15 @@ int main(int argc, char **argv) {
       add("SEG k_seg_stream NULL math", false, SEGSTREAM(true, false, 7));
       add("SEG k_seg_stream no events", false, SEGSTREAM(false, true, 7));
       add("SEG k_seg_stream NULL + no events", false, SEGSTREAM(true, true, 7));
+      if (sweep) {
+        add("SEG packed stream C=8", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st, nullptr, 3); });
+        add("SEG packed stream C=16", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st, nullptr, 4); });
+        add("SEG packed stream C=32", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st, nullptr, 5); });
+        add("SEG packed stream C=64", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st, nullptr, 6); });
+        add("SEG k_seg_stream NULL+noev C=8", false, SEGSTREAM(true, true, 3));
+        add("SEG k_seg_stream NULL+noev C=16", false, SEGSTREAM(true, true, 4));
+        add("SEG k_seg_stream NULL+noev C=32", false, SEGSTREAM(true, true, 5));
+      }
       add("SEG packed stream (again)", true, [&](hipStream_t st) { launch_seg(b, seg_t, seg_ws, seg_mu, cus, st); });
     }
     add("PROD launch_general (again)", true, [&](hipStream_t st) { launch_general(b, 0, cus, st); });

@@ -164,6 +164,18 @@ int main(int argc, char **argv) {
                 }, {}})
   DYN(8, 7);
   DYN(4, 6);
+  if (std::getenv("KREAD_DYN")) {  // hand-out piece size x chunk sweep
+    DYN(4, 4);
+    DYN(4, 5);
+    DYN(8, 4);
+    DYN(8, 5);
+    DYN(8, 6);
+    DYN(16, 3);
+    DYN(16, 4);
+    DYN(16, 5);
+    DYN(16, 6);
+    DYN(16, 7);
+  }
   GS(4, 1, 8);
   GS(8, 1, 8);
   GS(4, 1, 16);
