@@ -1237,7 +1237,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 // framed; 3: two).  kNull: timing-only build, the CRC replaced by an XOR fold
 // (tools/kframe measures the memory pattern alone).  kXcd (A/B only): XCD-
 // contiguous chunk slots as in k_crc_grp.
-template <int kDepth = 2, bool kNull = false, bool kXcd = false>
+// kSt (A/B only, tools/kframe): 0 = each row stored before it is hashed
+// (production); 2 = the block's four rows hashed, then its four stores;
+// 4 = the four stores, then the hashing.
+template <int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 0>
 __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
                                                          uint8_t *__restrict__ dst, uint64_t nblk, uint32_t lg_chunk,
                                                          uint32_t *__restrict__ crc_out,
@@ -1374,17 +1377,31 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
     const uint64_t b = i + 1;
     uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
     uint32_t cc[4];
+    u32x4 sv[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       u32x4 v = cur[r];
       // every lane stores (no divergent branch between the loads and their
       // use); lane 0 writes zeros to bytes 0..3 and the CRC over them below
       if (r == 0) v.x = lane == 0 ? 0u : v.x;
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+      sv[r] = v;
+      if constexpr (kSt == 0) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+    }
+    if constexpr (kSt == 4) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 v = cur[r];
       if (r == 0) v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : (kNull ? cc[k] ^ w[k] : row_step(cc[k], w[k]));
+    }
+    if constexpr (kSt == 2) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
     }
     uint32_t crcv;
     if constexpr (kNull) {
@@ -1456,15 +1473,17 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // back (block b's block[4:B] at out + b*(B-4)) -- the inverse of k_frame, one
 // read of the blocks and one write of the payload.  B = 4096 << lg_groups.
 // A wave walks its blocks in 4 KiB groups (4 rows of 1 KiB), the next group's
-// rows in flight while the current one is hashed and stored.  Payload stores
-// are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
+// rows in flight while the current one is hashed and stored (the four stores
+// after the group's hashing, kSt).  Payload stores are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
 // block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
 // overlapping lane 1's store with identical bytes.
-// kSt (A/B only, tools/kframe): 0 = each row stored before it is hashed
-// (production); 1 = each row stored after it is hashed; 2 = the group's four
-// rows hashed, then its four stores; 3 = production order with write-back
-// (not nt) stores.
-template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 0>
+// kSt: store order.  Production 2: the group's four rows are hashed, then its
+// four payload stores are issued together -- +3.9 % over storing each row
+// before hashing it (round-2 production), on two boxes, at the speed of the
+// timing-only build (profiles/r2/framing_store/).  A/B only: 0 = each row
+// stored before it is hashed; 1 = each row stored after it is hashed; 3 = 0
+// with write-back (not nt) stores; 4 = rows 0-2 hashed, the four stores, row 3.
+template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 2>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                            uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
@@ -1560,6 +1579,10 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
         sa[r] = ob + r * kRowBytes;
       }
       if constexpr (kSt == 0 || kSt == 3) st16(sv[r], sa[r]);
+      if constexpr (kSt == 4)
+        if (r == 3)
+#pragma unroll
+          for (int q = 0; q < 4; q++) st16(sv[q], sa[q]);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; k++)

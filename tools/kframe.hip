@@ -53,12 +53,21 @@ int main(int argc, char **argv) {
   uint32_t *crc, *crc_ref, *bitmap;
   unsigned long long *fb;
   hc::DeviceTables *dt;
+  // KFRAME_ORDER=bench: the unframe buffers first, in bench.py's order (blocks,
+  // payload); the HBM placement of the two streams moves k_unframe by ~2 %
+  if (std::getenv("KFRAME_ORDER")) {
+    CK(hipMalloc(&blocks, N * 4096));
+    CK(hipMalloc(&pay, N * 4092));
+  }
   CK(hipMalloc(&raw, npay + 16));
   CK(hipMalloc(&framed, N * 4096));
   CK(hipMalloc(&framed_ref, N * 4096));
-  CK(hipMalloc(&blocks, N * 4096));
-  CK(hipMalloc(&pay, N * 4092));
+  if (!std::getenv("KFRAME_ORDER")) {
+    CK(hipMalloc(&blocks, N * 4096));
+    CK(hipMalloc(&pay, N * 4092));
+  }
   CK(hipMalloc(&pay_ref, N * 4092));
+  std::printf("blocks %p payload %p\n", (void *)blocks, (void *)pay);
   CK(hipMalloc(&crc, N * 4));
   CK(hipMalloc(&crc_ref, N * 4));
   CK(hipMalloc(&bitmap, (N + 31) / 32 * 4));
@@ -105,12 +114,21 @@ int main(int argc, char **argv) {
     vs.push_back({"k_frame XCD C=16", 0, true, FRAME(2, false, 4, true), {}});
     vs.push_back({"k_frame XCD C=32", 0, true, FRAME(2, false, 5, true), {}});
   }
+  vs.push_back({"k_frame hash then 4 stores", 0, true, FRAME(2, false, lgp, false, 2), {}});
+  vs.push_back({"k_frame 4 stores then hash", 0, true, FRAME(2, false, lgp, false, 4), {}});
+  vs.push_back({"NULL k_frame", 0, false, FRAME(2, true, lgp), {}});
+  vs.push_back({"NULL k_frame hash then 4 stores", 0, false, FRAME(2, true, lgp, false, 2), {}});
   vs.push_back({"PROD k_unframe depth 2", 1, true, UNFRAME(2, false, lgp), {}});
-  vs.push_back({"NULL k_unframe", 1, false, UNFRAME(2, true, lgp), {}});
+  vs.push_back({"k_unframe round-2 store order (each row, then hash)", 1, true, UNFRAME(2, false, lgp, false, 0), {}});
+  vs.push_back({"k_unframe stores after rows 0-2", 1, true, UNFRAME(2, false, lgp, false, 4), {}});
+  vs.push_back({"NULL k_unframe 4 stores after group", 1, false, UNFRAME(2, true, lgp, false, 2), {}});
+  vs.push_back({"k_unframe 4 stores after group, depth 3", 1, true, UNFRAME(3, false, lgp, false, 2), {}});
+  vs.push_back({"NULL k_unframe round-2 order", 1, false, UNFRAME(2, true, lgp, false, 0), {}});
   vs.push_back({"k_unframe store after hash", 1, true, UNFRAME(2, false, lgp, false, 1), {}});
   vs.push_back({"k_unframe 4 stores after group", 1, true, UNFRAME(2, false, lgp, false, 2), {}});
   vs.push_back({"k_unframe write-back stores", 1, true, UNFRAME(2, false, lgp, false, 3), {}});
   vs.push_back({"NULL k_unframe write-back stores", 1, false, UNFRAME(2, true, lgp, false, 3), {}});
+  vs.push_back({"NULL k_unframe (production order)", 1, false, UNFRAME(2, true, lgp), {}});
   vs.push_back({"PROD k_frame depth 2 (again)", 0, true, FRAME(2, false, lgp), {}});
   vs.push_back({"PROD k_unframe depth 2 (again)", 1, true, UNFRAME(2, false, lgp), {}});
 
