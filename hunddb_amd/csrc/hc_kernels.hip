@@ -1237,6 +1237,58 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 // framed; 3: two).  kNull: timing-only build, the CRC replaced by an XOR fold
 // (tools/kframe measures the memory pattern alone).  kXcd (A/B only): XCD-
 // contiguous chunk slots as in k_crc_grp.
+// Edge blocks of AddCRCsToData framing (the first, whose row 0 would start 4
+// bytes before src, and the last, whose payload may end mid-row): aligned
+// loads predicated on the payload range + funnel shift + byte masks -- never
+// touches a byte outside src.  Stores block b's rows (lane 0's first 16 bytes
+// are returned in `keep` for the caller to store with the CRC in front) and
+// leaves the four Horner streams in c (lane 0's row-0 word 0 = W0).
+template <class RowStep>
+__device__ __forceinline__ void frame_edge_rows(uint64_t b, const uint8_t *__restrict__ src, uint64_t n,
+                                                uint8_t *__restrict__ dst, uint32_t lane, uint32_t w0,
+                                                RowStep row_step, uint32_t (&c)[4], uint4 &keep) {
+  constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const uintptr_t P = (uintptr_t)src + b * kPay;                      // payload start
+  const uint64_t len = (n - b * kPay) < kPay ? (n - b * kPay) : kPay;  // payload bytes
+  const uintptr_t S0 = P - 4;                                          // source of output byte 0
+  const uint32_t m = (uint32_t)(S0 & 15u), q = m >> 2, rb = m & 3u;
+  const uintptr_t Ab = S0 - m;
+  uint4 ch0[4], ch1[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uintptr_t X0 = Ab + (uintptr_t)r * kRowBytes + 16u * lane, X1 = X0 + 16;
+    ch0[r] = ch1[r] = make_uint4(0, 0, 0, 0);
+    if (X0 + 16 > P && X0 < P + len) ch0[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X0), 0);
+    if (X1 + 16 > P && X1 < P + len) ch1[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X1), 0);
+  }
+  keep = make_uint4(0, 0, 0, 0);
+  uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint4 fw = funnel16(ch0[r], ch1[r], q, rb);
+    uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
+    // keep output bytes t (= 1024r + 16l + 4k + j) with 4 <= t < 4 + len
+    const int32_t hi = 4 + (int32_t)len - (r * (int32_t)kRowBytes + 16 * (int32_t)lane);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t nb = hi - 4 * k;  // bytes of this word still inside the payload
+      uint32_t dm = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
+      if (r == 0 && k == 0) dm &= lane == 0 ? 0u : 0xFFFFFFFFu;  // bytes 0..3: the CRC field
+      w[k] &= dm;
+    }
+    const u32x4 outv = {w[0], w[1], w[2], w[3]};
+    if (r == 0 && lane == 0) {
+      keep = make_uint4(w[0], w[1], w[2], w[3]);
+      w[0] = w0;  // Go's init in place of the CRC field
+    } else {
+      __builtin_nontemporal_store(outv, reinterpret_cast<u32x4 *>(ob + r * kRowBytes + 16 * lane));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : row_step(c[k], w[k]);
+  }
+}
+
 // kSt (A/B only, tools/kframe): 0 = each row stored before it is hashed
 // (production); 2 = the block's four rows hashed, then its four stores;
 // 4 = the four stores, then the hashing.
@@ -1303,49 +1355,10 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
     }
   };
 
-  // Edge blocks (the first, whose row 0 would start 4 bytes before src, and the
-  // last, whose payload may end mid-row): aligned loads predicated on the
-  // payload range + funnel shift + byte masks -- never touches a byte outside src.
   auto edge_block = [&](uint64_t b) {
-    const uintptr_t P = (uintptr_t)src + b * kPay;                      // payload start
-    const uint64_t len = (n - b * kPay) < kPay ? (n - b * kPay) : kPay;  // payload bytes
-    const uintptr_t S0 = P - 4;                                          // source of output byte 0
-    const uint32_t m = (uint32_t)(S0 & 15u), q = m >> 2, rb = m & 3u;
-    const uintptr_t Ab = S0 - m;
-    uint4 ch0[4], ch1[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uintptr_t X0 = Ab + (uintptr_t)r * kRowBytes + 16u * lane, X1 = X0 + 16;
-      ch0[r] = ch1[r] = make_uint4(0, 0, 0, 0);
-      if (X0 + 16 > P && X0 < P + len) ch0[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X0), 0);
-      if (X1 + 16 > P && X1 < P + len) ch1[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X1), 0);
-    }
-    uint32_t c[4] = {0, 0, 0, 0};
-    uint4 keep = make_uint4(0, 0, 0, 0);
-    uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uint4 fw = funnel16(ch0[r], ch1[r], q, rb);
-      uint32_t w[4] = {fw.x, fw.y, fw.z, fw.w};
-      // keep output bytes t (= 1024r + 16l + 4k + j) with 4 <= t < 4 + len
-      const int32_t hi = 4 + (int32_t)len - (r * (int32_t)kRowBytes + 16 * (int32_t)lane);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int32_t nb = hi - 4 * k;  // bytes of this word still inside the payload
-        uint32_t dm = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
-        if (r == 0 && k == 0) dm &= lane == 0 ? 0u : 0xFFFFFFFFu;  // bytes 0..3: the CRC field
-        w[k] &= dm;
-      }
-      const u32x4 outv = {w[0], w[1], w[2], w[3]};
-      if (r == 0 && lane == 0) {
-        keep = make_uint4(w[0], w[1], w[2], w[3]);
-        w[0] = w0;  // Go's init in place of the CRC field
-      } else {
-        __builtin_nontemporal_store(outv, reinterpret_cast<u32x4 *>(ob + r * kRowBytes + 16 * lane));
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : row_step(c[k], w[k]);
-    }
+    uint32_t c[4];
+    uint4 keep;
+    frame_edge_rows(b, src, n, dst, lane, w0, row_step, c, keep);
     finish(b, c, keep);
   };
 
@@ -1462,6 +1475,112 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
       frame(n3, A);
       n1 = n4;
       n2 = n5;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_frame_np (A/B, tools/kframe): AddCRCsToData framing by short-lived 4-wave
+// workgroups, as the non-persistent copies that reach 5.6-6.0 TB/s do
+// (DESIGN 4.4a), instead of one persistent 16-wave workgroup per CU.  That
+// needs tables small enough for several workgroups per CU: the row-shift
+// tables with kR replicas (lane l reads replica l % kR; bank (v*kR + l % kR) %
+// 32, so 32/kR lanes of a half-wave spread over 32/kR banks), the 4-byte shift
+// tables unreplicated and the lane-placement columns, 16 + 4 + 8 KiB at kR = 4.
+// Wave w of workgroup g frames interior blocks (g*4 + w)*kPer + k + 1: its rows
+// are loaded first, in flight while the workgroup fills its tables.
+template <int kR = 4, int kPer = 1>
+__global__ __launch_bounds__(256) void k_frame_np(const uint8_t *__restrict__ src, uint64_t n,
+                                                  uint8_t *__restrict__ dst, uint64_t nblk,
+                                                  uint32_t *__restrict__ crc_out,
+                                                  const DeviceTables *__restrict__ tables) {
+  static_assert(kR == 1 || kR == 2 || kR == 4 || kR == 8, "replicas");
+  __shared__ __attribute__((aligned(16))) uint32_t tm[4 * 256 * kR];  // [t][v][replica]
+  __shared__ __attribute__((aligned(16))) uint32_t ts4[4 * 256];      // [t][v]
+  __shared__ uint32_t tl[32 * 64];                                     // [i][lane]
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  constexpr uint64_t kPay = 4092;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = uni(tid >> 6);
+  const uint64_t ni = nblk > 2 ? nblk - 2 : 0;
+  const uint64_t i0 = ((uint64_t)blockIdx.x * 4 + wave) * kPer;
+  // 1) this wave's rows (past the end: re-read interior block 0, never stored)
+  u32x4 v[kPer][4];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = i0 + k < ni ? i0 + k : 0;
+    const uint8_t *S = src + (i + 1) * kPay - 4 + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (ni) v[k][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * kRowBytes));
+  }
+  // 2) tables into LDS while the rows are in flight
+  {
+    const uint32_t *tg = &tables->tg[0][0];
+    for (uint32_t e = tid; e < 1024; e += 256) {
+      const uint32_t x = tg[e];
+#pragma unroll
+      for (int q = 0; q < kR; q++) tm[e * kR + q] = x;
+    }
+    const uint32_t *s4 = &tables->s4[0][0];
+    for (uint32_t e = tid; e < 1024; e += 256) ts4[e] = s4[e];
+    const uint32_t *lt = &tables->lane[0][0];
+    for (uint32_t e = tid; e < 2048; e += 256) tl[(e & 31u) * 64 + (e >> 5)] = lt[e];
+  }
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tl[i * 64 + lane];
+  const uint32_t rep4 = (lane % kR) * 4u;
+  // shift(c, 1024) = tg[0][c0] ^ tg[1][c1] ^ tg[2][c2] ^ tg[3][c3]: byte address
+  // t*1024*kR + v*4*kR + 4*(l % kR)
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    constexpr uint32_t E = 4u * kR, T = 1024u * kR;
+    const uint32_t t0 = lds_u32(tm, ((c & 255u) * E) | rep4);
+    const uint32_t t1 = lds_u32(tm, T + ((((c >> 8) & 255u) * E) | rep4));
+    const uint32_t t2 = lds_u32(tm, 2 * T + ((((c >> 16) & 255u) * E) | rep4));
+    const uint32_t t3 = lds_u32(tm, 3 * T + (((c >> 24) * E) | rep4));
+    return xor3(xor3(t0, t1, t2), t3, w);
+  };
+  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    return xor3(xor3(ts4[x & 255u], ts4[256 + ((x >> 8) & 255u)], ts4[512 + ((x >> 16) & 255u)]),
+                ts4[768 + (x >> 24)], w);
+  };
+  // 3) store, hash, finalize
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    if (i0 + k >= ni) break;  // wave-uniform
+    const uint64_t b = i0 + k + 1;
+    uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+    uint32_t cc[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 x = v[k][r];
+      if (r == 0) x.x = lane == 0 ? 0u : x.x;  // bytes 0..3: zeros now, the CRC below
+      __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+      if (r == 0) x.x = lane == 0 ? w0 : x.x;  // Go's init in place of the CRC field
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) cc[q] = r == 0 ? w[q] : row_step(cc[q], w[q]);
+    }
+    const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
+    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);
+    if (crc_out) lane0_store_u32(crc_out + b, crcv);
+  }
+  // 4) the edge blocks: workgroup 0's waves 0 and 1
+  if (blockIdx.x == 0 && wave < 2 && (wave == 0 || nblk > 1)) {
+    const uint64_t b = wave == 0 ? 0 : nblk - 1;
+    uint32_t c[4];
+    uint4 keep;
+    frame_edge_rows(b, src, n, dst, lane, w0, row_step, c, keep);
+    const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    if (lane == 0) {
+      keep.x = crcv;
+      *reinterpret_cast<uint4 *>(dst + b * (uint64_t)HC_FRAME_BLOCK) = keep;
+      if (crc_out) crc_out[b] = crcv;
     }
   }
 }

@@ -103,6 +103,12 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((k_frame<D, NUL __VA_OPT__(,) __VA_ARGS__>), dim3(cus), dim3(kFastThreads), 0, st, src, npay, \
                        framed, nblk, lg, crc, dt);                                                                  \
   }
+#define FRAME_NP(R, PER)                                                                                         \
+  [&](hipStream_t st) {                                                                                          \
+    const uint64_t g_ = (ni + 4 * (PER)-1) / (4 * (PER));                                                         \
+    hipLaunchKernelGGL((k_frame_np<R, PER>), dim3((unsigned)(g_ ? g_ : 1)), dim3(256), 0, st, src, npay, framed, nblk, \
+                       crc, dt);                                                                                 \
+  }
 #define UNFRAME(D, NUL, LG, ...)                                                                                   \
   [&, lg = (uint32_t)(LG)](hipStream_t st) {                                                                        \
     hipLaunchKernelGGL((k_unframe<0, D, NUL __VA_OPT__(,) __VA_ARGS__>), dim3(cus), dim3(kFastThreads), 0, st, blocks, \
@@ -114,6 +120,11 @@ int main(int argc, char **argv) {
     vs.push_back({"k_frame XCD C=16", 0, true, FRAME(2, false, 4, true), {}});
     vs.push_back({"k_frame XCD C=32", 0, true, FRAME(2, false, 5, true), {}});
   }
+  vs.push_back({"np frame R=4 1 blk/wave", 0, true, FRAME_NP(4, 1), {}});
+  vs.push_back({"np frame R=4 2 blk/wave", 0, true, FRAME_NP(4, 2), {}});
+  vs.push_back({"np frame R=8 1 blk/wave", 0, true, FRAME_NP(8, 1), {}});
+  vs.push_back({"np frame R=2 1 blk/wave", 0, true, FRAME_NP(2, 1), {}});
+  vs.push_back({"np frame R=4 4 blk/wave", 0, true, FRAME_NP(4, 4), {}});
   vs.push_back({"k_frame hash then 4 stores", 0, true, FRAME(2, false, lgp, false, 2), {}});
   vs.push_back({"k_frame 4 stores then hash", 0, true, FRAME(2, false, lgp, false, 4), {}});
   vs.push_back({"NULL k_frame", 0, false, FRAME(2, true, lgp), {}});
