@@ -2232,60 +2232,74 @@ __global__ __launch_bounds__(1024) void k_seg_scan_final(const uint8_t *base, co
   }
 }
 
-// Per event x (1024 per workgroup pass, persistent grid, two workgroups per
-// CU) K(x) = shift(G(x), re - x) = shift(G(U), re - U) ^ H(x) (re - U: 1 .. 16
-// rows), then per record [a, b) from K(a), K(b) (LDS exchange).  The tables of
-// row shifts up to 63 rows and every inverse byte shift in LDS (< 80 KiB).
+// Per event x: K(x) = shift(G(x), re - x) = shift(G(U), re - U) ^ H(x) (re - U:
+// 1 .. 16 rows); per record [a, b) from K(a), K(b).  Waves work independently
+// (persistent grid, two workgroups per CU, no barrier after the table fill):
+// an iteration of a wave covers kSub sub-passes of 64 events (K per lane) and
+// 63 records (K(b) from the next lane by a shuffle), with every sub-pass's loads
+// issued before the first is used.  The tables of row shifts up to 63 rows and
+// every inverse byte shift in LDS (68 KiB).
 __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ lens, uint64_t n,
                                                       const uint32_t *__restrict__ flag,
                                                       const uint32_t *__restrict__ unit_g,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken) {
-  constexpr int kPwL = 6, kInv0 = kPwL * 1024;
+  constexpr int kPwL = 6, kInv0 = kPwL * 1024, kSub = 4;
   __shared__ uint32_t tl[(kPwL + kSegInv) * 1024];
-  __shared__ uint32_t sk[1025], sre[1025];  // K and the row end (in rows from A0) per event
   seg_lds_pw(tl, st, 0, kPwL);
   for (uint32_t i = threadIdx.x; i < kSegInv * 1024; i += blockDim.x) tl[kInv0 + i] = (&st->inv[0][0][0])[i];
   if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
   __syncthreads();
   if (*flag) return;
   const SegGeo geo = seg_geo(base, offs, lens, n);
-  auto rel = [&](uint64_t j) -> uint64_t { return (j < n ? (uint64_t)base + offs[j] : geo.pend) - geo.a0; };
-  auto K = [&](uint64_t j, uint32_t &re_rows) -> uint32_t {
-    const uint64_t x = rel(j), u = x >> kSegUnitLg;
-    re_rows = (uint32_t)(x >> 10) + 1u;
-    const uint32_t r = re_rows - (uint32_t)(u << (kSegUnitLg - 10));  // 1 .. 16 rows
-    uint32_t v = unit_g[u];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t c = wv * 63u * kSub; c < n; c += nw * 63u * kSub) {
+    uint64_t x[kSub];
+    uint32_t eh[kSub], ug[kSub], kv[kSub], re[kSub];
 #pragma unroll
-    for (int k = 0; k <= (int)(kSegUnitLg - 10); k++)
-      if ((r >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
-    return v ^ ev_h[j];
-  };
-  const uint32_t t = threadIdx.x;
-  for (uint64_t c = (uint64_t)blockIdx.x << 10; c < n; c += (uint64_t)gridDim.x << 10) {
-    const uint64_t j = c + t;
-    if (j <= n) sk[t] = K(j, sre[t]);
-    if (t == 0 && c + 1024 <= n) sk[1024] = K(c + 1024, sre[1024]);
-    __syncthreads();
-    if (j < n) {
-      const uint32_t ra = sre[t], rb = sre[t + 1];
-      const uint32_t da = (uint32_t)(((uint64_t)ra << 10) - rel(j)), db = (uint32_t)(((uint64_t)rb << 10) - rel(j + 1));
-      uint32_t v = sk[t] ^ st->ones[da - 1];  // K(a) ^ shift(~0, d_a), advanced to re_b
-      uint32_t rows = rb - ra;
-#pragma unroll
-      for (int k = 0; k < kPwL; k++)
-        if ((rows >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
-      rows >>= kPwL;
-      for (int k = kPwL; rows; k++, rows >>= 1)
-        if (rows & 1u) v = seg_tmul(st->pw[k], v);
-      uint32_t y = sk[t + 1] ^ v;
-#pragma unroll
-      for (int k = 0; k < kSegInv; k++)
-        if ((db >> k) & 1u) y = seg_lds_tmul(tl + kInv0 + k * 1024, y);
-      crc_out[j] = y ^ 0xFFFFFFFFu;
+    for (int p = 0; p < kSub; p++) {  // event c + 63p + lane (past n: the span's end again)
+      const uint64_t j = c + 63u * p + lane, jj = j < n ? j : n;
+      x[p] = (jj < n ? (uint64_t)base + offs[jj] : geo.pend) - geo.a0;
+      eh[p] = ev_h[jj];
     }
-    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < kSub; p++) ug[p] = unit_g[x[p] >> kSegUnitLg];
+#pragma unroll
+    for (int p = 0; p < kSub; p++) {
+      re[p] = (uint32_t)(x[p] >> 10) + 1u;  // the row end, in rows from A0
+      const uint32_t r = re[p] - (uint32_t)((x[p] >> kSegUnitLg) << (kSegUnitLg - 10));  // 1 .. 16 rows
+      uint32_t v = ug[p];
+#pragma unroll
+      for (int k = 0; k <= (int)(kSegUnitLg - 10); k++)
+        if ((r >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
+      kv[p] = v ^ eh[p];
+    }
+#pragma unroll
+    for (int p = 0; p < kSub; p++) {
+      const uint64_t j = c + 63u * p + lane;
+      const uint32_t kb = __shfl_down(kv[p], 1), rb = __shfl_down(re[p], 1);
+      const uint64_t xb = __shfl_down((unsigned long long)x[p], 1);
+      if (lane < 63 && j < n) {
+        const uint32_t ra = re[p];
+        const uint32_t da = (uint32_t)(((uint64_t)ra << 10) - x[p]), db = (uint32_t)(((uint64_t)rb << 10) - xb);
+        uint32_t v = kv[p] ^ st->ones[da - 1];  // K(a) ^ shift(~0, d_a), advanced to re_b
+        uint32_t rows = rb - ra;
+#pragma unroll
+        for (int k = 0; k < kPwL; k++)
+          if ((rows >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
+        rows >>= kPwL;
+        for (int k = kPwL; rows; k++, rows >>= 1)
+          if (rows & 1u) v = seg_tmul(st->pw[k], v);
+        uint32_t y = kb ^ v;
+#pragma unroll
+        for (int k = 0; k < kSegInv; k++)
+          if ((db >> k) & 1u) y = seg_lds_tmul(tl + kInv0 + k * 1024, y);
+        crc_out[j] = y ^ 0xFFFFFFFFu;
+      }
+    }
   }
 }
 
