@@ -13,7 +13,7 @@ if [ "${PART:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$OUT/prof -o run -- python3 $R/bench.py --pmc off --cpu-seconds 0 --json-out $R/gpurun_out/$OUT/bench_under_rocprof.json > $R/gpurun_out/$OUT/rocprof.log 2>&1 || exit $?
 else
-  for w in northstar config2 config3 offlen4k 16k verify config4 frame unframe; do
+  for w in northstar config2 config3 offlen4k 16k verify config4 frame unframe records; do
     timeout -k 10 400 python bench.py --workload $w --json-out gpurun_out/$OUT/bench_$w.json > gpurun_out/$OUT/bench_$w.log 2>&1 || exit $?
   done
 fi
