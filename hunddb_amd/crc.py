@@ -80,6 +80,13 @@ class LaunchInfo(ctypes.Structure):
                 ("lds_bytes", ctypes.c_uint32)]
 
 
+class DevShard(ctypes.Structure):  # hc_dev_shard (include/hundcrc.h)
+    _fields_ = [("device", ctypes.c_int), ("base", ctypes.c_void_p), ("off", ctypes.c_void_p),
+                ("len", ctypes.c_void_p), ("stride", ctypes.c_uint64), ("ulen", ctypes.c_uint32),
+                ("nblocks", ctypes.c_uint64), ("crc_out", ctypes.c_void_p), ("bad_bitmap", ctypes.c_void_p),
+                ("first_bad", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
 _LIB = None
 _u8p = ctypes.c_void_p
 
@@ -107,6 +114,11 @@ def _lib():
             "hc_verify_blocks": (I, [P, P, P, U64, U32, U64, P, P]),
             "hc_stamp_blocks": (I, [P, P, P, U64, U32, U64]),
             "hc_crc32_messages": (I, [P, P, P, U64, P]),
+            "hc_shard_plan": (I, [U64, P, I, P]),
+            "hc_multi_crc32_blocks": (I, [P, P, P, U64, U32, U64, P, I, P, P]),
+            "hc_multi_verify_blocks": (I, [P, P, P, U64, U32, U64, P, P, I, P, P]),
+            "hc_multi_stamp_blocks": (I, [P, P, P, U64, U32, U64, I, P, P]),
+            "hc_dev_multi_crc32_blocks": (I, [ctypes.POINTER(DevShard), I, U32]),
             "hc_dev_crc32_blocks": (I, [I, P, P, P, U64, U32, U64, P, P, P, U32, P]),
             "hc_dev_verify_prepare": (I, [I, P, P, U64, P]),
             "hc_dev_fill_blocks": (I, [I, P, P, P, U64, U32, U64, U64, P]),
@@ -379,6 +391,100 @@ def stamp_blocks(buf, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, n
     if rc != HC_OK:
         raise HundCRCError(rc, "stamp_blocks")
     return buf
+
+
+# ---- several GPUs in one process (include/hundcrc.h hc_shard_plan, hc_multi_*) ----
+def shard_plan(nblocks: int, ndev: int, lens=None) -> np.ndarray:
+    """Block-index bounds (ndev+1) of a batch split over ndev GPUs: by count, or
+    balanced by bytes when `lens` is given (the plan of shard.py)."""
+    l = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint32)
+    b = np.zeros(ndev + 1, dtype=np.uint64)
+    rc = _lib().hc_shard_plan(int(nblocks), None if l is None else l.ctypes.data, int(ndev), b.ctypes.data)
+    if rc != HC_OK:
+        raise HundCRCError(rc, "shard_plan")
+    return b
+
+
+def _devs(devices, bounds):
+    d = np.ascontiguousarray(devices, dtype=np.int32)
+    b = None if bounds is None else np.ascontiguousarray(bounds, dtype=np.uint64)
+    if b is not None and len(b) != len(d) + 1:
+        raise ValueError("bounds needs len(devices) + 1 entries")
+    return d, b
+
+
+def multi_crc32_blocks(buf, devices, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None,
+                       bounds=None) -> np.ndarray:
+    """crc32_blocks with shard d of the plan on devices[d] (one host pipeline and thread per shard)."""
+    p, n, _k = _ro_ptr(buf)
+    o, l = _meta(off, lens)
+    nb = _nblocks(n, o, l, stride, ulen, nblocks)
+    d, b = _devs(devices, bounds)
+    out = np.zeros(nb, dtype=np.uint32)
+    rc = _lib().hc_multi_crc32_blocks(p, None if o is None else o.ctypes.data, None if l is None else l.ctypes.data,
+                                      stride, ulen, nb, out.ctypes.data, len(d), d.ctypes.data,
+                                      None if b is None else b.ctypes.data)
+    if rc != HC_OK:
+        raise HundCRCError(rc, "multi_crc32_blocks")
+    return out
+
+
+def multi_verify_blocks(buf, devices, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None,
+                        bounds=None):
+    """verify_blocks over several GPUs: (err | None, bad_bitmap uint32[], first_bad int)."""
+    p, n, _k = _ro_ptr(buf)
+    o, l = _meta(off, lens)
+    nb = _nblocks(n, o, l, stride, ulen, nblocks)
+    d, b = _devs(devices, bounds)
+    bm = np.zeros((nb + 31) // 32, dtype=np.uint32)
+    fb = ctypes.c_int64(-1)
+    rc = _lib().hc_multi_verify_blocks(p, None if o is None else o.ctypes.data, None if l is None else l.ctypes.data,
+                                       stride, ulen, nb, bm.ctypes.data if nb else None, ctypes.addressof(fb),
+                                       len(d), d.ctypes.data, None if b is None else b.ctypes.data)
+    if rc < 0:
+        raise HundCRCError(rc, "multi_verify_blocks")
+    return _err(rc), bm, fb.value
+
+
+def multi_stamp_blocks(buf, devices, off=None, lens=None, stride=BLOCK_SIZE, ulen=BLOCK_SIZE, nblocks=None,
+                       bounds=None):
+    """stamp_blocks over several GPUs (in place)."""
+    p, n, _k = _rw_ptr(buf)
+    o, l = _meta(off, lens)
+    nb = _nblocks(n, o, l, stride, ulen, nblocks)
+    d, b = _devs(devices, bounds)
+    rc = _lib().hc_multi_stamp_blocks(p, None if o is None else o.ctypes.data, None if l is None else l.ctypes.data,
+                                      stride, ulen, nb, len(d), d.ctypes.data, None if b is None else b.ctypes.data)
+    if rc != HC_OK:
+        raise HundCRCError(rc, "multi_stamp_blocks")
+    return buf
+
+
+def dev_multi_crc32_blocks(shards, flags=0):
+    """hc_dev_multi_crc32_blocks: `shards` = dicts with device, buf (torch tensor on
+    that device), out (int32 tensor or None), stride/ulen/nblocks, off/lens
+    (device tensors or None), stream (or None); enqueued, not synchronised."""
+    arr = (DevShard * len(shards))()
+    for k, sh in enumerate(shards):
+        buf = sh["buf"]
+        arr[k].device = int(sh.get("device", buf.device.index or 0))
+        arr[k].base = buf.data_ptr()
+        arr[k].off = _tptr(sh.get("off"))
+        arr[k].len = _tptr(sh.get("lens"))
+        arr[k].stride = int(sh.get("stride", 0))
+        arr[k].ulen = int(sh.get("ulen", 0))
+        arr[k].nblocks = int(sh["nblocks"])
+        arr[k].crc_out = _tptr(sh.get("out"))
+        arr[k].bad_bitmap = _tptr(sh.get("bad_bitmap"))
+        arr[k].first_bad = _tptr(sh.get("first_bad"))
+        st = sh.get("stream")
+        if st is None:
+            import torch
+            st = torch.cuda.current_stream(buf.device)
+        arr[k].stream = st.cuda_stream
+    rc = _lib().hc_dev_multi_crc32_blocks(arr, len(shards), int(flags))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "dev_multi_crc32_blocks")
 
 
 def crc32_messages(buf, off, lens) -> np.ndarray:

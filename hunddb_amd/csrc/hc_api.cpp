@@ -259,6 +259,7 @@ struct Slot {
 
 struct HostPipe {
   int dev = -1;
+  int home = -1;  // the device the pool created it for
   size_t chunk = 0;   // staging bytes per slot
   size_t maxblk = 0;  // metadata capacity per slot
   size_t span = 0;    // span-DMA bytes per slot (device memory only: no pinned staging)
@@ -337,25 +338,31 @@ class PipePool {
     static PipePool *p = new PipePool;
     return *p;
   }
+  // At most cap_ pipelines per device (several GPUs in one process each get
+  // their own: hc_multi_*); a pipeline never moves between devices.
   HostPipe *acquire(int dev) {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      for (size_t k = 0; k < idle_.size(); k++)  // an idle pipeline already on this device
-        if (idle_[k]->ok && idle_[k]->dev == dev) return take(k);
-      if (live_ < cap_) {
+      for (size_t k = 0; k < idle_.size(); k++)  // an idle pipeline on this device
+        if (idle_[k]->dev == dev) return take(k);
+      if (live_dev_[dev] < cap_) {
+        live_dev_[dev]++;
         live_++;
-        return new HostPipe;
+        auto *p = new HostPipe;
+        p->dev = -1;  // initialised on `dev` by the caller
+        p->home = dev;
+        return p;
       }
-      if (!idle_.empty()) return take(0);  // re-initialised on `dev` by the caller
       cv_.wait(lk);
     }
   }
   void release(HostPipe *p) {
     {
       std::lock_guard<std::mutex> lk(mu_);
+      if (p->dev < 0) p->dev = p->home;  // (its init failed: it stays this device's)
       idle_.push_back(p);
     }
-    cv_.notify_one();
+    cv_.notify_all();
   }
   int live() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -373,6 +380,7 @@ class PipePool {
   std::condition_variable cv_;
   std::vector<HostPipe *> idle_;
   int live_ = 0;
+  int live_dev_[kMaxDevices] = {};
   const int cap_;
 };
 
@@ -419,8 +427,8 @@ constexpr uint64_t kMd5MaxPerChunk = 262144;  // bounds the per-message MD5 work
 // retires (blocks of >= 4 bytes), overlapped with the later chunks' copies.
 int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t flags, uint8_t *md5_out = nullptr,
-               HostVerify *hv = nullptr, uint8_t *stamp = nullptr) {
-  const int dev = default_device();
+               HostVerify *hv = nullptr, uint8_t *stamp = nullptr, int device = -1) {
+  const int dev = device >= 0 ? device : default_device();
   int st = init_device(dev);
   if (st != HC_OK) return st;
   PipeLease lease(dev);
@@ -903,6 +911,125 @@ int hc_stamp_blocks(uint8_t *base, const uint64_t *off, const uint32_t *len, uin
   return host_batch(base, off, len, stride, ulen, nblocks, nullptr, 0, nullptr, nullptr, base);
 }
 
+// ---- several GPUs in one process ---------------------------------------------
+int hc_shard_plan(uint64_t nblocks, const uint32_t *len, int ndev, uint64_t *bounds) {
+  if (ndev < 1 || ndev > kMaxDevices || !bounds) return HC_E_ARG;
+  bounds[0] = 0;
+  bounds[ndev] = nblocks;
+  if (!len) {  // shard.index_range: n*d/ndev
+    for (int d = 1; d < ndev; d++) bounds[d] = (uint64_t)((unsigned __int128)nblocks * (unsigned)d / (unsigned)ndev);
+    return HC_OK;
+  }
+  // shard.byte_balanced_bounds: the first block whose prefix sum (bytes of the
+  // blocks before it) reaches total*d/ndev
+  unsigned __int128 total = 0;
+  for (uint64_t i = 0; i < nblocks; i++) total += len[i];
+  uint64_t i = 0;
+  unsigned __int128 csum = 0;  // bytes of blocks [0, i)
+  for (int d = 1; d < ndev; d++) {
+    const unsigned __int128 target = total * (unsigned)d / (unsigned)ndev;
+    while (i < nblocks && csum < target) csum += len[i++];
+    bounds[d] = i;
+  }
+  return HC_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// Runs fn(d, lo, hi, device) for every shard d on its own thread (the caller's
+// for shard 0) after checking the plan; returns the first failing shard's code.
+template <class F>
+int multi_run(uint64_t nblocks, const uint32_t *len, int ndev, const int *devices, const uint64_t *bounds_in,
+              F &&fn) {
+  if (ndev < 1 || ndev > kMaxDevices || !devices) return HC_E_ARG;
+  std::vector<uint64_t> bounds(ndev + 1);
+  if (bounds_in) {
+    std::copy(bounds_in, bounds_in + ndev + 1, bounds.begin());
+    if (bounds[0] != 0 || bounds[ndev] != nblocks) return HC_E_ARG;
+    for (int d = 0; d < ndev; d++)
+      if (bounds[d] > bounds[d + 1]) return HC_E_ARG;
+  } else if (hc_shard_plan(nblocks, len, ndev, bounds.data()) != HC_OK) {
+    return HC_E_ARG;
+  }
+  for (int d = 0; d < ndev; d++) {
+    const int st = init_device(devices[d]);
+    if (st != HC_OK) return st;
+  }
+  std::vector<int> rc(ndev, HC_OK);
+  parallel_for(ndev, [&](int d) {
+    if (bounds[d + 1] > bounds[d]) rc[d] = fn(d, bounds[d], bounds[d + 1], devices[d]);
+  });
+  for (int d = 0; d < ndev; d++)
+    if (rc[d] != HC_OK) return rc[d];
+  return HC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int hc_multi_crc32_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                          uint32_t ulen, uint64_t nblocks, uint32_t *crc_out, int ndev, const int *devices,
+                          const uint64_t *bounds) {
+  if (nblocks == 0) return HC_OK;
+  if (!base || !crc_out) return HC_E_ARG;
+  return multi_run(nblocks, len, ndev, devices, bounds, [&](int, uint64_t lo, uint64_t hi, int dev) {
+    return host_batch(off ? base : base + lo * stride, off ? off + lo : nullptr, len ? len + lo : nullptr, stride,
+                      ulen, hi - lo, crc_out + lo, 0, nullptr, nullptr, nullptr, dev);
+  });
+}
+
+int hc_multi_verify_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                           uint32_t ulen, uint64_t nblocks, uint32_t *bad_bitmap, int64_t *first_bad, int ndev,
+                           const int *devices, const uint64_t *bounds) {
+  if (first_bad) *first_bad = -1;
+  if (bad_bitmap) std::memset(bad_bitmap, 0, ((nblocks + 31) / 32) * 4);
+  if (nblocks == 0) return HC_OK;
+  if (!base || ndev < 1 || ndev > kMaxDevices) return HC_E_ARG;
+  // each shard verifies into a bitmap of its own (its blocks from bit 0)
+  std::vector<std::vector<uint32_t>> bm(ndev);
+  std::vector<int64_t> fb(ndev, -1);
+  std::vector<uint64_t> los(ndev, 0);
+  const int rc = multi_run(nblocks, len, ndev, devices, bounds, [&](int d, uint64_t lo, uint64_t hi, int dev) {
+    HostVerify hv;
+    if (bad_bitmap) {
+      bm[d].assign((hi - lo + 31) / 32, 0);
+      hv.bitmap = bm[d].data();
+    }
+    los[d] = lo;
+    const int r = host_batch(off ? base : base + lo * stride, off ? off + lo : nullptr, len ? len + lo : nullptr,
+                             stride, ulen, hi - lo, nullptr, 0, nullptr, &hv, nullptr, dev);
+    fb[d] = hv.first_bad;
+    return r;
+  });
+  if (rc != HC_OK) return rc;
+  int64_t first = -1;
+  for (int d = 0; d < ndev; d++) {
+    if (fb[d] < 0) continue;
+    const int64_t g = (int64_t)los[d] + fb[d];
+    if (first < 0 || g < first) first = g;
+    for (uint64_t w = 0; w < bm[d].size(); w++)
+      for (uint32_t m = bm[d][w]; m; m &= m - 1) {
+        const uint64_t k = los[d] + 32 * w + (uint32_t)__builtin_ctz(m);
+        bad_bitmap[k >> 5] |= 1u << (k & 31);
+      }
+  }
+  if (first < 0) return HC_OK;
+  if (first_bad) *first_bad = first;
+  return blk_len(len, ulen, (uint64_t)first) < HC_CRC_SIZE ? HC_ERR_INVALID_BLOCK : HC_ERR_CRC_MISMATCH;
+}
+
+int hc_multi_stamp_blocks(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
+                          uint64_t nblocks, int ndev, const int *devices, const uint64_t *bounds) {
+  if (nblocks == 0) return HC_OK;
+  if (!base) return HC_E_ARG;
+  return multi_run(nblocks, len, ndev, devices, bounds, [&](int, uint64_t lo, uint64_t hi, int dev) {
+    uint8_t *b = off ? base : base + lo * stride;
+    return host_batch(b, off ? off + lo : nullptr, len ? len + lo : nullptr, stride, ulen, hi - lo, nullptr, 0,
+                      nullptr, nullptr, b, dev);
+  });
+}
+
 // ---- device-resident batches ---------------------------------------------------
 int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const uint32_t *len,
                         uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out,
@@ -917,6 +1044,17 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
   uint64_t bytes = (!off && !len) ? nblocks * (uint64_t)ulen : 0;
   return dispatch(device, static_cast<const uint8_t *>(base), off, len, stride, ulen, nblocks, crc_out,
                   bad_bitmap, first_bad, flags, static_cast<hipStream_t>(stream), bytes, true);
+}
+
+int hc_dev_multi_crc32_blocks(const hc_dev_shard *shards, int nshards, uint32_t flags) {
+  if (nshards < 0 || (nshards > 0 && !shards)) return HC_E_ARG;
+  for (int k = 0; k < nshards; k++) {
+    const hc_dev_shard &h = shards[k];
+    const int rc = hc_dev_crc32_blocks(h.device, h.base, h.off, h.len, h.stride, h.ulen, h.nblocks, h.crc_out,
+                                       h.bad_bitmap, h.first_bad, flags, h.stream);
+    if (rc != HC_OK) return rc;
+  }
+  return HC_OK;
 }
 
 uint64_t hc_read_blocks_touched(uint32_t block_size, uint64_t start_offset, uint64_t size) {

@@ -113,6 +113,28 @@ int hc_stamp_blocks(uint8_t *base, const uint64_t *off, const uint32_t *len, uin
 int hc_crc32_messages(const uint8_t *base, const uint64_t *off, const uint32_t *len,
                       uint64_t nmsgs, uint32_t *crc_out);
 
+/* ---------------- several GPUs in one process ---------------- */
+/* Shard plan: contiguous block-index ranges [bounds[d], bounds[d+1]) for ndev
+ * GPUs (bounds has ndev+1 entries, bounds[0] = 0, bounds[ndev] = nblocks).
+ * len == NULL: by count, bounds[d] = nblocks*d/ndev; else balanced by bytes,
+ * bounds[d] = the first block whose byte prefix sum reaches total*d/ndev.  The
+ * same plan as hunddb_amd/shard.py (index_range / byte_balanced_bounds). */
+int hc_shard_plan(uint64_t nblocks, const uint32_t *len, int ndev, uint64_t *bounds);
+/* hc_crc32_blocks / hc_verify_blocks / hc_stamp_blocks over several GPUs: shard d
+ * (blocks [bounds[d], bounds[d+1]) of the plan, bounds == NULL: hc_shard_plan)
+ * runs on devices[d] through its own host pipeline on its own thread, so each
+ * GPU's PCIe link carries its shard.  Outputs as in the one-GPU entries
+ * (bad_bitmap / first_bad over the whole batch).  A device may appear more than
+ * once.  Returns the first failing shard's error, else as the one-GPU entry. */
+int hc_multi_crc32_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                          uint32_t ulen, uint64_t nblocks, uint32_t *crc_out, int ndev, const int *devices,
+                          const uint64_t *bounds);
+int hc_multi_verify_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                           uint32_t ulen, uint64_t nblocks, uint32_t *bad_bitmap, int64_t *first_bad, int ndev,
+                           const int *devices, const uint64_t *bounds);
+int hc_multi_stamp_blocks(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
+                          uint64_t nblocks, int ndev, const int *devices, const uint64_t *bounds);
+
 /* ---------------- batched, device-resident (GPU) ---------------- */
 /* As above with device pointers (base, off, len, outputs) on `device`,
  * asynchronous on `stream` (hipStream_t).  crc_out, bad_bitmap and first_bad
@@ -125,6 +147,26 @@ int hc_dev_crc32_blocks(int device, const void *base, const uint64_t *off, const
                         uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out,
                         uint32_t *bad_bitmap, int64_t *first_bad, uint32_t flags,
                         void *stream);
+/* One shard of a device-resident batch: its blocks, outputs and stream live on
+ * `device` (off/len/outputs indexed from the shard's first block). */
+typedef struct hc_dev_shard {
+  int device;
+  const void *base;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint64_t stride;
+  uint32_t ulen;
+  uint64_t nblocks;
+  uint32_t *crc_out;
+  uint32_t *bad_bitmap;
+  int64_t *first_bad;
+  void *stream;
+} hc_dev_shard;
+/* hc_dev_crc32_blocks on every shard (each GPU its own shard of a batch,
+ * no exchange between them); enqueued on each shard's stream,
+ * no synchronisation.  Returns HC_OK once all are enqueued, else the first
+ * failing shard's error (shards before it are enqueued). */
+int hc_dev_multi_crc32_blocks(const hc_dev_shard *shards, int nshards, uint32_t flags);
 /* lsm/block_manager/block_manager.go:189-242 ReadFromDisk, minus the file I/O
  * (row f1): `blocks` holds the blocks from index start_offset/block_size on, as
  * the caller read them (`avail` bytes; past that a block reads as zeros, like

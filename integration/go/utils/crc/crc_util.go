@@ -127,6 +127,39 @@ func AddCRCToBlocks(data []byte, blockSize int) error {
 	return goErr(C.hc_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize), C.uint64_t(n)))
 }
 
+// CheckBlocksIntegrityOn is CheckBlocksIntegrity over several GPUs of this
+// process: the blocks are split into contiguous ranges (hc_shard_plan), range d
+// is verified on devices[d] through its own host pipeline, so every GPU's PCIe
+// link carries its share.  Same result as CheckBlocksIntegrity.
+func CheckBlocksIntegrityOn(data []byte, blockSize int, devices []int) (int, error) {
+	n := len(data) / blockSize
+	devs := make([]C.int, len(devices))
+	for i, d := range devices {
+		devs[i] = C.int(d)
+	}
+	if len(devs) == 0 {
+		return CheckBlocksIntegrity(data, blockSize)
+	}
+	var first C.int64_t = -1
+	rc := C.hc_multi_verify_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize),
+		C.uint64_t(n), nil, &first, C.int(len(devs)), &devs[0], nil)
+	return int(first), goErr(rc)
+}
+
+// AddCRCToBlocksOn is AddCRCToBlocks over several GPUs (see CheckBlocksIntegrityOn).
+func AddCRCToBlocksOn(data []byte, blockSize int, devices []int) error {
+	n := len(data) / blockSize
+	devs := make([]C.int, len(devices))
+	for i, d := range devices {
+		devs[i] = C.int(d)
+	}
+	if len(devs) == 0 {
+		return AddCRCToBlocks(data, blockSize)
+	}
+	return goErr(C.hc_multi_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize),
+		C.uint64_t(n), C.int(len(devs)), &devs[0], nil))
+}
+
 // ReadVerified is BlockManager.ReadFromDisk (block_manager.go:189-242) minus
 // the file I/O: raw holds the blocks from startOffset/blockSize on, as read
 // (cache or disk).  Every touched block is verified in one batch, then the
