@@ -90,6 +90,12 @@ def parse(argv=None):
     ap.add_argument("--ref1", choices=["auto", "on", "off"], default="auto",
                     help="strong scaling: rank 0 re-runs the whole batch alone (speedup + word check)")
     ap.add_argument("--settle", type=float, default=0.5, help="untimed clock-settle seconds before warmup")
+    # bracket: one event pair on the launch stream around the K launches (the mean
+    # launch time then includes the ~1.5 us gaps between launches: conservative);
+    # step: a pair around every launch, whose recording costs the wall clock
+    # ~0.5 % (profiles/r2/bench_events/)
+    ap.add_argument("--kernel-events", choices=["step", "bracket"], default="bracket",
+                    help="HIP events around the K launches (bracket) or around every launch (step)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
@@ -456,21 +462,29 @@ def main(argv=None):
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        per_step = args.kernel_events == "step"
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps if per_step else 1)]
         if barrier:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(steps):
-            ev[i][0].record(stream)
-            step()
-            ev[i][1].record(stream)
+        if per_step:
+            for i in range(steps):
+                ev[i][0].record(stream)
+                step()
+                ev[i][1].record(stream)
+        else:  # one pair around the K launches: the mean includes the gaps between them
+            ev[0][0].record(stream)
+            for i in range(steps):
+                step()
+            ev[0][1].record(stream)
         torch.cuda.synchronize()
         if barrier:
             dist.barrier()
         dt = time.perf_counter() - t0
         kern_ms = [a.elapsed_time(b) for a, b in ev]
-        return dt, sum(kern_ms) / len(kern_ms) / 1e3
+        return dt, sum(kern_ms) / (steps if not per_step else len(kern_ms)) / 1e3
 
     step = make_step(buf, out, kw)
     dt, mean_kern_s = timed(step, args.steps, args.warmup, world > 1)
@@ -532,6 +546,9 @@ def main(argv=None):
                 "traffic": None if traffic is None else round(traffic["bytes"]),
                 "kernel": info["kernel"], "bytes_per_launch": step_bytes,
                 "mean_launch_ms": round(mean_kern_s * 1e3, 4),
+                "launch_timing": ("HIP events on the launch stream around the K timed launches; mean = span / K "
+                                  "(includes the gaps between launches)" if args.kernel_events == "bracket"
+                                  else "HIP events on the launch stream around every timed launch"),
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
                 **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + 3 scan/combine kernels "
