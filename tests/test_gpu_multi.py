@@ -91,3 +91,26 @@ def test_dev_multi_shards_equal_one_launch(cuda, hc):
     hc.dev_multi_crc32_blocks(shards)
     torch.cuda.synchronize()
     assert torch.equal(torch.cat(outs), whole)
+
+
+def test_multi_more_devices_than_blocks(cuda, hc, oracle):
+    """8 ranges over 5 blocks: the empty ranges do nothing, the others run."""
+    n, B = 5, 4096
+    buf = blocks(oracle, n, B, seed=0x3)
+    want = oracle.crc32_blocks(buf, stride=B, ulen=B)
+    assert np.array_equal(hc.multi_crc32_blocks(buf, [0] * 8, stride=B, ulen=B), want)
+    err, bm, fb = hc.multi_verify_blocks(buf, [0] * 8, stride=B, ulen=B)
+    assert fb == 0 and err is not None  # unstamped blocks fail
+
+
+def test_multi_pinned_span_dma(cuda, hc, oracle):
+    """Pinned records through the span-DMA path of every range's pipeline."""
+    torch = cuda
+    rng = np.random.default_rng(11)
+    lens = rng.integers(64, 65536, 4000).astype(np.uint32)
+    host, off, lens = oracle.fill_blocks(0x44, len(lens), sizes=lens)
+    pinned = torch.empty(len(host), dtype=torch.uint8, pin_memory=True)
+    pinned.numpy()[:] = host
+    want = oracle.crc32_blocks(host, off=off, lens=lens)
+    got = hc.multi_crc32_blocks(pinned.numpy(), [0, 0, 0], off=off, lens=lens)
+    assert np.array_equal(got, want)

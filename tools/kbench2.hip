@@ -201,6 +201,25 @@ int main(int argc, char **argv) {
       add("grp pinned C=256", true, GRP(false, true, false, 8, true));
       add("grp pinned C=512", true, GRP(false, true, false, 9, true));
       add("production launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+    } else if (std::getenv("KB2_PIECE") && (B == 8192 || B == 16384)) {  // 4 KiB pieces of 8/16 KiB blocks
+#define PIECE(GG, LG, X)                                                                                      \
+  [&](hipStream_t st) {                                                                                      \
+    hipLaunchKernelGGL((k_crc_piece<GG, X>), dim3(cus), dim3(kFastThreads), 0, st, b.base, b.stride, b.flags,  \
+                       b.nblocks, (uint32_t)(LG), b.crc_out, b.bad_bitmap, b.first_bad, b.tables, seg_t);       \
+  }
+      add("PROD launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+      if (B == 8192) {
+        add("PIECE G=2 C=64 pieces", true, PIECE(2, 6, false));
+        add("PIECE G=2 C=32 pieces", true, PIECE(2, 5, false));
+        add("PIECE G=2 C=128 pieces", true, PIECE(2, 7, false));
+        add("PIECE G=2 XCD C=64 pieces", true, PIECE(2, 6, true));
+        add("PIECE G=2 XCD C=32 pieces", true, PIECE(2, 5, true));
+      } else {
+        add("PIECE G=4 C=64 pieces", true, PIECE(4, 6, false));
+        add("PIECE G=4 C=128 pieces", true, PIECE(4, 7, false));
+        add("PIECE G=4 XCD C=64 pieces", true, PIECE(4, 6, true));
+      }
+      add("PROD launch_grp (again)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
     } else {
       add("PROD launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
       add("grp pinned C=64", true, GRP(false, true, false, 6, true));
