@@ -1,0 +1,140 @@
+"""Seeded random layouts through the batch entries, against the oracle.
+
+Each case draws a layout the reference's callers can produce or the C ABI
+accepts: uniform blocks (4/8/16 KiB and any other length, any stride, any
+start alignment), off/len blocks (4 KiB multiples mixed with arbitrary
+lengths, gaps, unaligned starts, lengths 0-3, shuffled and overlapping
+entries) and whole messages (packed back to back, or scattered).  Every case
+runs the device entry (hc_dev_crc32_blocks, so k_crc_grp / k_crc_fast /
+k_crc_any routing and, for packed message batches with HC_SEG_MIN_MSGS=1, the
+k_seg_* stream) and the host entry (the pipelined staging path), and compares
+the words with the oracle.  Non-overlapping block cases are then stamped on
+the device, compared byte for byte, corrupted at random blocks and verified:
+bitmap and first_bad must name exactly the corrupted blocks plus every block
+shorter than 4 bytes (crc_util.go:89-91)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = 192
+MAX_BYTES = 24 << 20
+
+
+def _len(rng):
+    r = rng.random()
+    if r < 0.45:
+        return int(rng.choice([4096, 8192, 16384]))
+    if r < 0.55:
+        return int(rng.integers(0, 4))
+    if r < 0.7:
+        return 1024 * int(rng.integers(1, 20))
+    return int(rng.integers(4, 20000))
+
+
+def gen_case(seed):
+    rng = np.random.default_rng(seed)
+    kind = ["uniform", "offlen", "messages"][seed % 3]
+    lead = int(rng.choice([0, 0, 0, int(rng.integers(1, 16))]))  # start alignment of the data
+    if kind == "uniform":
+        ulen = _len(rng)
+        stride = ulen + int(rng.choice([0, 0, 16 * int(rng.integers(1, 8)), int(rng.integers(1, 64))]))
+        stride = max(stride, 1)
+        n = int(rng.integers(1, max(2, min(3000, MAX_BYTES // stride))))
+        size = lead + stride * (n - 1) + ulen + 64
+        off, lens = None, None  # blocks start at byte `lead` of the buffer
+    else:
+        n = int(rng.integers(1, 3000))
+        lens = np.array([_len(rng) for _ in range(n)], dtype=np.uint32)
+        while lens.sum() > MAX_BYTES:
+            lens = lens[: len(lens) // 2]
+        n = len(lens)
+        packed = kind == "messages" and rng.random() < 0.5
+        gaps = np.zeros(n, dtype=np.uint64) if packed else rng.integers(0, 40, n).astype(np.uint64)
+        off = np.zeros(n, dtype=np.uint64)
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+        off += np.uint64(lead)
+        size = int(off[-1]) + int(lens[-1]) + 64
+        if kind == "offlen" and rng.random() < 0.3:  # shuffled order, some entries repeated
+            perm = rng.permutation(n)
+            off, lens = off[perm], lens[perm]
+            k = max(1, n // 10)
+            off[:k], lens[:k] = off[-k:], lens[-k:]
+        stride = ulen = 0
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    return kind, buf, off, lens, stride, ulen, n, (lead if off is None else 0)
+
+
+def _words(oracle, kind, buf, off, lens, stride, ulen, n):
+    if kind == "messages":
+        return oracle.crc32_messages(buf, off, lens)
+    return oracle.crc32_blocks(buf, off=off, lens=lens, stride=stride or 1, ulen=ulen, nblocks=n)
+
+
+def _dev(torch, a):
+    return None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(
+        np.int64 if a.dtype == np.uint64 else np.int32)).cuda()
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_layout(cuda, hc, oracle, seed, monkeypatch):
+    torch = cuda
+    kind, buf, off, lens, stride, ulen, n, lead = gen_case(1000 + seed)
+    packed = kind == "messages" and n > 1 and bool(
+        np.all(off[1:] == off[:-1] + lens[:-1].astype(np.uint64)))
+    if packed and seed % 2:
+        monkeypatch.setenv("HC_SEG_MIN_MSGS", "1")  # the packed-record stream on a small batch
+    want = _words(oracle, kind, buf[lead:], off, lens, stride, ulen, n)
+    flags = hc.HC_F_MESSAGES if kind == "messages" else 0
+    # device entry
+    dall = torch.from_numpy(buf).cuda()
+    dbuf = dall[lead:]
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    hc.dev_crc32_blocks(dbuf, out, off=_dev(torch, off), lens=_dev(torch, lens), stride=stride, ulen=ulen,
+                        nblocks=n, flags=flags)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want), (kind, int(np.flatnonzero(got != want)[0]), hc.last_launch())
+    # host entry
+    if kind == "messages":
+        got_h = hc.crc32_messages(buf, off, lens)
+    else:
+        got_h = hc.crc32_blocks(buf[lead:], off=off, lens=lens, stride=stride, ulen=ulen, nblocks=n)
+    assert np.array_equal(got_h, want), kind
+    if kind == "messages":
+        return
+    # stamp + verify on the device (blocks must not overlap for a stamp)
+    if off is not None:
+        o = off.astype(np.int64)
+        order = np.argsort(o, kind="stable")
+        ends = o[order] + lens[order].astype(np.int64)
+        if np.any(o[order][1:] < ends[:-1]) or len(np.unique(o)) != len(o):
+            return
+    rng = np.random.default_rng(seed)
+    hc.dev_crc32_blocks(dbuf, None, off=_dev(torch, off), lens=_dev(torch, lens), stride=stride, ulen=ulen,
+                        nblocks=n, flags=hc.HC_F_STAMP)
+    torch.cuda.synchronize()
+    ref = buf.copy()
+    offs = off.astype(np.int64) if off is not None else lead + np.arange(n, dtype=np.int64) * stride
+    L = lens if lens is not None else np.full(n, ulen, dtype=np.uint32)
+    for i in range(n):
+        if L[i] >= 4:
+            ref[offs[i]:offs[i] + 4] = np.array([want[i]], dtype=np.uint32).view(np.uint8)
+    assert np.array_equal(dall.cpu().numpy(), ref), kind
+    bad = set(int(i) for i in np.flatnonzero(L < 4))
+    cand = np.flatnonzero(L >= 5)
+    for i in rng.choice(cand, size=min(len(cand), int(rng.integers(0, 4))), replace=False) if len(cand) else []:
+        pos = int(offs[i]) + int(rng.integers(4, int(L[i])))
+        dall[pos] ^= 0x40
+        bad.add(int(i))
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(dbuf, None, off=_dev(torch, off), lens=_dev(torch, lens), stride=stride, ulen=ulen,
+                        nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    bits = np.flatnonzero(np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little"))
+    assert sorted(bits.tolist()) == sorted(bad), kind
+    assert int(fb.item()) == (min(bad) if bad else 2**63 - 1)
