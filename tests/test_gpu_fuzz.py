@@ -138,3 +138,63 @@ def test_random_layout(cuda, hc, oracle, seed, monkeypatch):
     bits = np.flatnonzero(np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little"))
     assert sorted(bits.tolist()) == sorted(bad), kind
     assert int(fb.item()) == (min(bad) if bad else 2**63 - 1)
+
+
+N_FRAMING = 48
+
+
+@pytest.mark.parametrize("seed", range(N_FRAMING))
+def test_random_framing_round_trip(cuda, hc, oracle, seed):
+    """AddCRCsToData (host entry: GPU batch from 256 blocks, host below; device
+    entry k_frame) on random payload sizes at random alignments, byte-exact vs
+    the oracle; then ReadFromDisk over the framed image (host entry and the
+    device k_unframe) at random start offsets and sizes, vs the oracle's
+    block_manager.go:189-242 restatement, with one corrupted block in half the
+    cases."""
+    torch = cuda
+    rng = np.random.default_rng(5000 + seed)
+    n = int(rng.choice([0, 1, 4091, 4092, 4093, int(rng.integers(1, 200 * 4092)),
+                        int(rng.integers(256 * 4092, 1200 * 4092))]))
+    lead = int(rng.integers(0, 16))
+    raw = rng.integers(0, 256, n + lead + 16, dtype=np.uint8)
+    pay = raw[lead:lead + n]
+    want = np.zeros(hc.hc_add_crcs_size_py(n), dtype=np.uint8)
+    if n:
+        oracle.lib().oc_add_crcs_to_data(pay.ctypes.data, n, want.ctypes.data)
+    got = np.frombuffer(bytes(hc.AddCRCsToData(pay)), dtype=np.uint8)
+    assert np.array_equal(got, want)
+    if n:
+        dsrc = torch.from_numpy(raw).cuda()[lead:lead + n]
+        framed = hc.dev_add_crcs(dsrc)
+        torch.cuda.synchronize()
+        assert np.array_equal(framed.cpu().numpy(), want)
+    if len(want) == 0:
+        return
+    nb = len(want) // 4096
+    img = want.copy()
+    bad_blk = None
+    if seed % 2 and nb > 1:
+        bad_blk = int(rng.integers(0, nb))
+        img[bad_blk * 4096 + int(rng.integers(4, 4096))] ^= 0x08
+    # device k_unframe over the whole image
+    dimg = torch.from_numpy(img).cuda()
+    bm = torch.empty((nb + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, nb)
+    payload = hc.dev_read_blocks(dimg, 4096, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    assert int(fb.item()) == (bad_blk if bad_blk is not None else 2**63 - 1)
+    if bad_blk is None:
+        assert np.array_equal(payload.cpu().numpy()[:n], pay)
+    # host ReadFromDisk at random offsets and sizes
+    for _ in range(3):
+        start = int(rng.integers(0, len(img)))
+        size = int(rng.integers(0, max(1, len(img) - start)))
+        b0 = start // 4096
+        blocks = img[b0 * 4096:].tobytes()
+        w_pay, w_fo, w_rc, w_bad = oracle.read_from_disk(blocks, 4096, start, size)
+        g_pay, g_fo, g_err = hc.ReadFromDisk(blocks, 4096, start, size)
+        if w_rc == 0:
+            assert g_err is None and g_pay == w_pay and g_fo == w_fo
+        else:
+            assert g_err is not None and int(g_err.code) == w_rc and hc.last_bad_block() == w_bad
