@@ -97,6 +97,10 @@ def parse(argv=None):
     ap.add_argument("--kernel-events", choices=["step", "bracket"], default="bracket",
                     help="HIP events around the K launches (bracket) or around every launch (step)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--input", choices=["resident", "scatter"], default="resident",
+                    help="N>1 strong scaling: each rank fills its shard in HBM (resident), or rank 0 holds the "
+                         "whole batch and sends the shards over RCCL first (scatter; timed and reported "
+                         "separately, SURVEY.md 8e)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -342,6 +346,10 @@ def main(argv=None):
     nblk, bsize, scaling = WORKLOADS[args.workload]
     if args.blocks:
         nblk = args.blocks
+    scatter_in = args.input == "scatter" and world > 1 and scaling == "strong" and isinstance(bsize, int)
+    if args.input == "scatter" and not scatter_in:
+        raise SystemExit("--input scatter needs --gpus N > 1 and a uniform strong-scaling workload (config4)")
+    full, scatter_s = None, None
     if scaling == "strong":  # one global batch, partitioned by block index
         lo, hi = shard.index_range(nblk, world, rank)
         total_blocks = nblk
@@ -427,8 +435,22 @@ def main(argv=None):
         step_bytes = my * 4096 + my * 4092  # one read of the blocks + one write of the payload
         block_desc = "ReadFromDisk: verify 4096-B blocks + strip CRCs"
     else:
-        buf = torch.empty(my * bsize, dtype=torch.uint8, device=dev)
-        crc.dev_fill_range(buf, SEED, lo, my, stride=bsize, ulen=bsize)
+        if scatter_in:
+            # the batch starts on rank 0's GPU: its shards go out by RCCL send/recv
+            if rank == 0:
+                full = torch.empty(total_blocks * bsize, dtype=torch.uint8, device=dev)
+                crc.dev_fill_range(full, SEED, 0, total_blocks, stride=bsize, ulen=bsize)
+            bnd = [shard.index_range(nblk, world, r)[0] * bsize for r in range(world)] + [nblk * bsize]
+            torch.cuda.synchronize()
+            dist.barrier()
+            ts = time.perf_counter()
+            buf = shard.scatter_from_root(full, bnd, device=dev)
+            torch.cuda.synchronize()
+            dist.barrier()
+            scatter_s = time.perf_counter() - ts
+        else:
+            buf = torch.empty(my * bsize, dtype=torch.uint8, device=dev)
+            crc.dev_fill_range(buf, SEED, lo, my, stride=bsize, ulen=bsize)
         kw = dict(stride=bsize, ulen=bsize, nblocks=my)
         step_bytes = my * bsize
         block_desc = f"{bsize} B"
@@ -515,12 +537,20 @@ def main(argv=None):
         gather_s = time.perf_counter() - tg
         ref1 = args.ref1 == "on" or (args.ref1 == "auto" and scaling == "strong")
         if rank == 0:
-            multi = {"gathered_words": int(gathered.numel()), "gather_ms": round(gather_s * 1e3, 3)}
+            multi = {"gathered_words": int(gathered.numel()), "gather_ms": round(gather_s * 1e3, 3),
+                     "input": args.input}
+            if scatter_s is not None:
+                moved = total_blocks * bsize - counts[0] * bsize
+                multi.update({"scatter_ms": round(scatter_s * 1e3, 3), "scatter_bytes": moved,
+                              "scatter_gb_s": round(moved / scatter_s / 1e9, 2),
+                              "scatter_note": "rank 0 -> every other rank, RCCL send/recv grouped; outside the "
+                                              "timed CRC region (SURVEY.md 8e)"})
             if ref1 and isinstance(kw, dict) and "stride" in kw and scaling == "strong":
                 del step, buf, out  # the shard (the step closure holds it too)
                 torch.cuda.empty_cache()
-                full = torch.empty(total_blocks * bsize, dtype=torch.uint8, device=dev)
-                crc.dev_fill_range(full, SEED, 0, total_blocks, stride=bsize, ulen=bsize)
+                if full is None:  # (scatter input: rank 0 still holds the whole batch)
+                    full = torch.empty(total_blocks * bsize, dtype=torch.uint8, device=dev)
+                    crc.dev_fill_range(full, SEED, 0, total_blocks, stride=bsize, ulen=bsize)
                 outf = torch.empty(total_blocks, dtype=torch.int32, device=dev)
                 t1, k1 = timed(make_step(full, outf, dict(stride=bsize, ulen=bsize, nblocks=total_blocks)),
                                args.steps, args.warmup, False)

@@ -59,6 +59,37 @@ def gather_crcs(local, counts, dst: int = 0, group=None):
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
+def scatter_from_root(full, bounds_bytes, device=None, root: int = 0, group=None):
+    """The batch starts on one GPU (reported separately from the
+    device-resident numbers): `root` holds the whole uint8 tensor `full` and
+    sends every other rank its byte range [bounds_bytes[r], bounds_bytes[r+1])
+    by point-to-point transfers (RCCL send/recv over xGMI, batched into one
+    group; gloo on CPU tests).  Returns the rank's shard: on the root a view of
+    `full`, elsewhere a new tensor on `device`."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    nccl = dist.get_backend(group) == "nccl"
+    lo, hi = int(bounds_bytes[rank]), int(bounds_bytes[rank + 1])
+    if rank == root:
+        # (gloo moves host copies: a one-GPU rehearsal of the RCCL path)
+        ops = [dist.P2POp(dist.isend, full[int(bounds_bytes[r]):int(bounds_bytes[r + 1])].contiguous()
+                          if nccl else full[int(bounds_bytes[r]):int(bounds_bytes[r + 1])].cpu(), r, group)
+               for r in range(world) if r != root and bounds_bytes[r + 1] > bounds_bytes[r]]
+        mine = full[lo:hi]
+    else:
+        mine = torch.empty(hi - lo, dtype=torch.uint8, device=device if nccl else "cpu")
+        ops = [dist.P2POp(dist.irecv, mine, root, group)] if hi > lo else []
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if rank != root and not nccl and device is not None:
+        mine = mine.to(device)
+    return mine
+
+
 def free_port() -> int:
     import socket
     s = socket.socket()

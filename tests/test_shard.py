@@ -97,3 +97,48 @@ def test_index_range_covers():
         for w in (1, 2, 3, 8):
             r = [shard.index_range(n, w, k) for k in range(w)]
             assert r[0][0] == 0 and r[-1][1] == n and all(r[k][1] == r[k + 1][0] for k in range(w - 1))
+
+
+def _scatter_worker(rank, world, port, nbytes, q):
+    import torch
+    import torch.distributed as dist
+
+    from hunddb_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bounds = [shard.index_range(nbytes, world, r)[0] for r in range(world)] + [nbytes]
+        full = None
+        if rank == 0:
+            full = torch.from_numpy(np.random.default_rng(9).integers(0, 256, nbytes, dtype=np.uint8))
+        mine = shard.scatter_from_root(full, bounds)
+        got = shard.gather_crcs(torch.from_numpy(np.frombuffer(mine.numpy().tobytes() + b"\0" * (-mine.numel() % 4),
+                                                                dtype=np.int32).copy()),
+                                [(bounds[r + 1] - bounds[r] + 3) // 4 for r in range(world)])
+        if rank == 0:
+            q.put((bounds, got.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_from_root(world):
+    """bench.py --input scatter: rank 0 holds the batch, every rank receives its
+    byte range (gloo here, RCCL send/recv on the GPUs)."""
+    nbytes = 4096 * 1001 + 12
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, nbytes, q)) for r in range(world)]
+    [p.start() for p in procs]
+    bounds, got = q.get(timeout=120)
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    full = np.random.default_rng(9).integers(0, 256, nbytes, dtype=np.uint8)
+    words = got.view(np.uint8)
+    pos = 0
+    for r in range(world):  # each rank's range came back as whole int32 words, zero-padded
+        n = bounds[r + 1] - bounds[r]
+        assert np.array_equal(words[pos:pos + n], full[bounds[r]:bounds[r + 1]])
+        pos += (n + 3) // 4 * 4
