@@ -1779,7 +1779,9 @@ __global__ __launch_bounds__(256) void k_frame_np(const uint8_t *__restrict__ sr
 // timing-only build (profiles/r2/framing_store/).  A/B only: 0 = each row
 // stored before it is hashed; 1 = each row stored after it is hashed; 3 = 0
 // with write-back (not nt) stores; 4 = rows 0-2 hashed, the four stores, row 3.
-template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 2>
+// kPol (A/B only): payload stores as buffer stores with cache-policy bits
+// kPol - 1 (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16); 0 = global nt stores.
+template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 2, int kPol = 0>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                            uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
@@ -1852,8 +1854,12 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
     const uint64_t b = p >> lg_groups;
     const uint32_t g = (uint32_t)p & gmask;
     uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
+    uint8_t *const obu = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK - 4;  // wave-uniform
+    const __amdgpu_buffer_rsrc_t orc = __builtin_amdgcn_make_buffer_rsrc(obu, 0, HC_FRAME_BLOCK + 16, 0x00020000);
     auto st16 = [&](u32x4 v, uint8_t *a) {
-      if constexpr (kSt == 3)
+      if constexpr (kPol > 0)
+        __builtin_amdgcn_raw_buffer_store_b128(v, orc, (uint32_t)(a - obu), 0, kPol - 1);
+      else if constexpr (kSt == 3)
         *reinterpret_cast<u32x4_u *>(a) = v;
       else
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(a));

@@ -2,4 +2,4 @@
 OUT=${OUT:-r4c}
 mkdir -p gpurun_out/$OUT
 cd tools || exit 1
-timeout -k 10 300 ./kframe 1000000 6 5 > ../gpurun_out/$OUT/kframe_np1.txt 2>&1 || exit $?
+timeout -k 10 300 ./kframe 1000000 6 5 > ../gpurun_out/$OUT/kframe_pol.txt 2>&1 || exit $?

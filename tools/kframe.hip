@@ -131,6 +131,11 @@ int main(int argc, char **argv) {
   vs.push_back({"NULL k_frame hash then 4 stores", 0, false, FRAME(2, true, lgp, false, 2), {}});
   vs.push_back({"PROD k_unframe depth 2", 1, true, UNFRAME(2, false, lgp), {}});
   vs.push_back({"k_unframe round-2 store order (each row, then hash)", 1, true, UNFRAME(2, false, lgp, false, 0), {}});
+  vs.push_back({"k_unframe buffer stores nt", 1, true, UNFRAME(2, false, lgp, false, 2, 3), {}});
+  vs.push_back({"k_unframe buffer stores sc0|nt", 1, true, UNFRAME(2, false, lgp, false, 2, 4), {}});
+  vs.push_back({"k_unframe buffer stores sc1|nt", 1, true, UNFRAME(2, false, lgp, false, 2, 19), {}});
+  vs.push_back({"k_unframe buffer stores sc0|sc1|nt", 1, true, UNFRAME(2, false, lgp, false, 2, 20), {}});
+  vs.push_back({"k_unframe buffer stores sc1", 1, true, UNFRAME(2, false, lgp, false, 2, 17), {}});
   vs.push_back({"k_unframe stores after rows 0-2", 1, true, UNFRAME(2, false, lgp, false, 4), {}});
   vs.push_back({"NULL k_unframe 4 stores after group", 1, false, UNFRAME(2, true, lgp, false, 2), {}});
   vs.push_back({"k_unframe 4 stores after group, depth 3", 1, true, UNFRAME(3, false, lgp, false, 2), {}});
