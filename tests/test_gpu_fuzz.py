@@ -198,3 +198,37 @@ def test_random_framing_round_trip(cuda, hc, oracle, seed):
             assert g_err is None and g_pay == w_pay and g_fo == w_fo
         else:
             assert g_err is not None and int(g_err.code) == w_rc and hc.last_bad_block() == w_bad
+
+
+N_WAL = 24
+
+
+@pytest.mark.parametrize("seed", range(N_WAL))
+def test_random_wal_replay(cuda, hc, oracle, seed):
+    """Row f3 with the GPU verify (>= 256 blocks): random record-size laws,
+    block sizes 4096/8192/5000 (any BlockSize >= 1024 is valid, config.go:241),
+    start blocks, memtable-full stops and corrupted blocks, against the
+    oracle's sequential wal.go:362-455 restatement."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import walgen
+    rng = np.random.default_rng(7000 + seed)
+    bs = int(rng.choice([4096, 4096, 8192, 5000]))
+    hi = int(rng.choice([2000, 20000, 65536]))
+    plan = walgen.WalPlan(9000 + seed, nrec=int(rng.integers(1500, 6000)), lo=int(rng.choice([17, 64])), hi=hi, bs=bs)
+    img = plan.render(0, plan.nblocks)
+    nb = plan.nblocks
+    for _ in range(3):
+        view = img.copy()
+        for k in range(int(rng.integers(0, 3))):
+            blk = int(rng.integers(0, nb))
+            view[blk * bs + int(rng.integers(4, bs))] ^= 1 << int(rng.integers(0, 8))
+        start = int(rng.choice([0, 0, int(rng.integers(0, nb))]))
+        mr = int(rng.choice([0, 0, int(rng.integers(1, 4000))]))
+        (buf, off, ln), err, bad, pos = hc.wal_replay(view, bs, start, 4, mr, as_arrays=True)
+        want, wrc, wbad, wpos = oracle.wal_replay(view.tobytes(), bs, start, 4, mr)
+        assert (0 if err is None else err.code) == wrc, (bs, start, mr)
+        assert pos == wpos and bad == wbad and len(ln) == len(want)
+        got = buf[: int(off[-1] + ln[-1])].tobytes() if len(ln) else b""
+        assert [int(x) for x in ln] == [len(w) for w in want]
+        assert got == b"".join(want)
