@@ -510,8 +510,11 @@ __global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
 //   * A block that is not 16-B aligned or whose length is not a positive
 //     multiple of 4096 costs one group of dummy rows (re-reads of the current
 //     group, never stored) and is left to k_crc_any (fast_mask 4095).
+// kNib (A/B only): the 4-byte shift of the per-block finalise from nibble
+// tables with 32 replicas (8 conflict-free lookups) instead of byte tables with
+// 4 replicas (4 lookups, 8 lanes of a half-wave on 8 banks); same 16 KiB.
 template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false, bool kBatch = false,
-          bool kXcd = false>
+          bool kXcd = false, bool kNib = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ lens, uint64_t stride,
                                                          uint32_t ulen, uint32_t flags, uint64_t nblocks,
@@ -534,7 +537,13 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   }
   const uint32_t *s4 = &tables->s4[0][0];
   for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
-    const uint32_t v = s4[q];
+    uint32_t v;
+    if constexpr (kNib) {  // nibble k, value n at kLdsMainBytes + k*2048 + n*128 + 4*replica
+      const uint32_t k = q >> 7, n = (q >> 3) & 15u;
+      v = s4[(k >> 1) * 256 + (n << (4 * (k & 1)))];
+    } else {
+      v = s4[q];
+    }
     *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) = make_uint4(v, v, v, v);
   }
   if (tid == 0) s_next = 3 * kFastWaves;  // indices 0 .. 3W-1 are dealt statically below
@@ -555,7 +564,14 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
     const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
     return xor3(xor3(t0, t1, t2), t3, w);
   };
+  const uint32_t N4base = kLdsMainBytes + ((lane & 31u) << 2);
   auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    if constexpr (kNib) {
+      uint32_t t[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) t[k] = lds_u32(lds, N4base + k * 2048u + (((x >> (4 * k)) & 15u) << 7));
+      return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], w));
+    }
     const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
     const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
     const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));

@@ -222,6 +222,17 @@ int main(int argc, char **argv) {
       add("PROD launch_grp (again)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
     } else {
       add("PROD launch_grp", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+      if (std::getenv("KB2_NIB")) {  // nibble shift4 tables (conflict-free finalise)
+        if (B >= 8192) {
+          add("NIB grp XCD C=32", true, GRP(false, true, false, 5, true, false, true, true));
+          add("PROD launch_grp (2)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+          add("NIB grp XCD C=32 (2)", true, GRP(false, true, false, 5, true, false, true, true));
+        } else {
+          add("NIB grp C=64", true, GRP(false, true, false, 6, true, false, false, true));
+          add("PROD launch_grp (2)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
+          add("NIB grp C=64 (2)", true, GRP(false, true, false, 6, true, false, false, true));
+        }
+      }
       add("grp pinned C=64", true, GRP(false, true, false, 6, true));
       add("grp pinned C=128", true, GRP(false, true, false, 7, true));
       add("grp XCD-contiguous C=16", true, GRP(false, true, false, 4, true, false, true));
