@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../hunddb_amd/csrc/hc_kernels.hip"
+#include "ab_kernels.hip"
 #include "r1_kernels.hip"
 
 #define CK(x)                                                                                \

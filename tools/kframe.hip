@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../hunddb_amd/csrc/hc_kernels.hip"
+#include "ab_kernels.hip"
 
 #define CK(x)                                                                                \
   do {                                                                                       \
