@@ -232,3 +232,45 @@ def test_random_wal_replay(cuda, hc, oracle, seed):
         got = buf[: int(off[-1] + ln[-1])].tobytes() if len(ln) else b""
         assert [int(x) for x in ln] == [len(w) for w in want]
         assert got == b"".join(want)
+
+
+N_READ = 16
+
+
+@pytest.mark.parametrize("seed", range(N_READ))
+def test_random_read_from_disk_verified_mask(cuda, hc, oracle, seed):
+    """Row f1 with the block cache's verified bits, random block sizes, start
+    offsets, sizes, mask densities and corruptions (in masked and unmasked
+    blocks), at GPU-batch sizes: the first unmasked corrupt block stops the read,
+    masked blocks are trusted and never hashed, and a clean read returns what the
+    oracle returns for the same bytes with the trusted blocks re-stamped."""
+    rng = np.random.default_rng(8000 + seed)
+    B = int(rng.choice([4096, 8192, 5000, 1024, 16384]))
+    n = int(rng.integers(256, 4000 if B <= 8192 else 1500))
+    raw = rng.integers(0, 256, n * B, dtype=np.uint8)
+    raw.view(np.uint8).reshape(n, B)[:, :4] = oracle.crc32_blocks(raw, stride=B, ulen=B).view(
+        np.uint8).reshape(n, 4)
+    start = int(rng.integers(0, 3 * B))
+    b0 = start // B
+    size = int(rng.integers(1, (n - b0 - 1) * (B - 4)))
+    k = hc.read_blocks_touched(B, start, size)
+    blocks = raw[b0 * B:].copy()
+    masked = rng.random(k) < float(rng.choice([0.0, 0.3, 0.9]))
+    corrupt = sorted(set(int(x) for x in rng.integers(0, k, int(rng.integers(0, 4)))))
+    for c in corrupt:
+        blocks[c * B + int(rng.integers(4, B))] ^= 0x10
+    v = np.zeros((k + 31) // 32, np.uint32)
+    for i in np.flatnonzero(masked):
+        v[i >> 5] |= np.uint32(1 << (int(i) & 31))
+    got, fo, err = hc.ReadFromDisk(blocks.tobytes(), B, start, size, verified=v)
+    live_bad = [c for c in corrupt if not masked[c]]
+    assert hc.last_hashed() == int((~masked).sum())
+    if live_bad:
+        assert str(err) == "CRC mismatch in block" and hc.last_bad_block() == live_bad[0]
+        return
+    assert err is None
+    fixed = blocks.copy()  # the trusted (masked) corrupt blocks re-stamped: the oracle accepts them
+    fixed.reshape(-1, B)[:, :4] = oracle.crc32_blocks(fixed, stride=B, ulen=B).view(np.uint8).reshape(-1, 4)
+    want, wfo, wrc, _ = oracle.read_from_disk(fixed.tobytes(), B, start, size)
+    assert wrc == 0 and got == want and fo == wfo
+    assert np.unpackbits(v.view(np.uint8), bitorder="little")[:k].sum() == k
