@@ -274,3 +274,32 @@ def test_random_read_from_disk_verified_mask(cuda, hc, oracle, seed):
     want, wfo, wrc, _ = oracle.read_from_disk(fixed.tobytes(), B, start, size)
     assert wrc == 0 and got == want and fo == wfo
     assert np.unpackbits(v.view(np.uint8), bitorder="little")[:k].sum() == k
+
+
+N_MULTI = 16
+
+
+@pytest.mark.parametrize("seed", range(N_MULTI))
+def test_random_multi_gpu_plans(cuda, hc, oracle, seed):
+    """The single-process multi-GPU entries on random block layouts and random
+    plans (every range on device 0 of the one-GPU box, each on its own thread
+    and pipeline): CRC words, and verify merged over the ranges, vs the oracle."""
+    kind, buf, off, lens, stride, ulen, n, lead = gen_case(3000 + 3 * seed + (seed % 2))  # uniform / off-len
+    if kind == "messages":
+        kind, buf, off, lens, stride, ulen, n, lead = gen_case(3000 + 3 * seed + 1)
+    rng = np.random.default_rng(seed)
+    ndev = int(rng.integers(1, 9))
+    if rng.random() < 0.5:
+        cuts = np.sort(rng.integers(0, n + 1, ndev - 1))
+        bounds = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+    else:
+        bounds = None  # hc_shard_plan
+    base = buf[lead:]
+    want = oracle.crc32_blocks(base, off=off, lens=lens, stride=stride or 1, ulen=ulen, nblocks=n)
+    got = hc.multi_crc32_blocks(base, [0] * ndev, off=off, lens=lens, stride=stride, ulen=ulen, nblocks=n,
+                                bounds=bounds)
+    assert np.array_equal(got, want), (kind, ndev)
+    err1, bm1, fb1 = hc.verify_blocks(base, off=off, lens=lens, stride=stride, ulen=ulen, nblocks=n)
+    err, bm, fb = hc.multi_verify_blocks(base, [0] * ndev, off=off, lens=lens, stride=stride, ulen=ulen, nblocks=n,
+                                         bounds=bounds)
+    assert np.array_equal(bm, bm1) and fb == fb1 and str(err) == str(err1)
