@@ -325,7 +325,7 @@ struct HostPipe {
   ~HostPipe() { release(); }
 };
 
-// Process-wide pool of pipelines, at most HC_MAX_PIPES (default 4) alive: a
+// Process-wide pool of pipelines, at most HC_MAX_PIPES (default 4) per device: a
 // host batch leases one for the duration of the call and returns it.  cgo runs
 // calls on arbitrary, long-lived OS threads, so per-thread pipelines (each
 // ~240 MiB pinned + ~1 GiB of device buffers) would grow with the thread

@@ -332,7 +332,7 @@ int hc_debug_seg_taken(void);
 int hc_device_count(void);
 /* Host-batch pipelines alive in this process (pinned staging + device buffers
  * + streams).  Host entries lease one per call from a pool of at most
- * HC_MAX_PIPES (default 4); further concurrent callers wait for a free one. */
+ * HC_MAX_PIPES (default 4) per device; further concurrent callers wait for a free one. */
 int hc_host_pipelines(void);
 
 #ifdef __cplusplus
