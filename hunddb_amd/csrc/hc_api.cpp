@@ -199,9 +199,18 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       info.kernel = "k_crc_any";
       info.general_blocks = n;
     }
+  } else if (!off != !len) {
+    // only one of the arrays (hundcrc.h allows either): off[i] with ulen, or
+    // i * stride with len[i].  k_crc_grp's contract is both arrays or neither,
+    // so the whole batch takes k_crc_any, which reads each side as given.
+    e = launch_general(b, 0, gen_grid, s);
+    info.kernel = "k_crc_any";
+    info.general_blocks = n;
   } else {
     uint32_t *seg_ws = nullptr;
-    if (seg_ok && (flags & kFlagMessages) && off && len && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
+    // the stream's only output is crc_out (k_seg_combine): a batch without it
+    // (verify or stamp only) takes k_crc_grp + k_crc_any
+    if (seg_ok && (flags & kFlagMessages) && crc_out && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
       hipDeviceptr_t pb = nullptr;
       size_t ps = 0;
       if (hipMemGetAddressRange(&pb, &ps, const_cast<uint8_t *>(base)) == hipSuccess && ps) {

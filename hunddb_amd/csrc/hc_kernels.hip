@@ -2355,7 +2355,8 @@ uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
                       uint32_t *taken, uint32_t lg_chunk) {
-  if (!b.base || !b.off || !b.len || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages)) return hipErrorInvalidValue;
+  if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
+    return hipErrorInvalidValue;
   const uint64_t n = b.nblocks, nb = (max_units >> kSegScanLg) + 1;
   uint32_t *flag = ws, *first_ev = ws + 64, *unit_raw = first_ev + max_units + 1, *unit_incl = unit_raw + max_units,
            *blk_tot = unit_incl + max_units, *blk_pre = blk_tot + nb, *ev_h = blk_pre + nb;

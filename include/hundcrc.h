@@ -186,9 +186,9 @@ uint64_t hc_read_blocks_touched(uint32_t block_size, uint64_t start_offset, uint
 /* hc_read_from_disk with the block cache's verified bits (row f1): `verified`
  * (optional; ceil(k/32) words, k = hc_read_blocks_touched, bit i = block i
  * relative to `blocks`) marks blocks the caller already verified -- an LRU
- * cache entry that was checked when it was read from disk or written by the
- * engine (BlockManager.ReadBlock, block_manager.go:72-98; lru_cache.go:20-65)
- * -- and they are NOT hashed again.  On return the bits of every block that
+ * cache entry whose bytes were CRC-checked and that no caller can have
+ * changed since (block_manager.go:72-114; lru_cache.go:20-65; the rule is in
+ * INTEGRATION.md section 3) -- and they are NOT hashed again.  On return the bits of every block that
  * this call verified clean are set too, so the cache can record them.
  * *hashed (optional) = blocks whose CRC this call computed. */
 int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_size, uint64_t start_offset,

@@ -6,7 +6,23 @@
 // value becomes *cachedBlock, ReadBlock/WriteBlock fill it, and ReadFromDisk
 // collects the touched blocks and verifies them through
 // crc_util.ReadVerifiedCached.  Not compiled in this repository (no Go
-// toolchain here or on the GPU box); INTEGRATION.md section 3 explains it.
+// toolchain here or on the GPU box); INTEGRATION.md section 3 explains it, and
+// tests/test_block_manager_protocol.py drives the same protocol through the C
+// ABI.
+//
+// The rule: a cache entry is skipped by ReadFromDisk's verify only when its
+// bytes were CRC-checked and no caller can have changed them since.
+//   - WriteBlock caches a COPY of the caller's block and marks it verified only
+//     if crc_util.CheckBlockIntegrity passes on that copy.  A block written
+//     without a CRC (PersistLSM writes lsm.serialize() raw, lsm.go:148-156) or
+//     written back corrupt (wal_test.go:878-898) stays unverified, so the next
+//     ReadFromDisk returns "CRC mismatch in block" exactly as
+//     block_manager.go:215 does.
+//   - ReadBlock hands the cached slice itself to its caller, as the reference
+//     does (block_manager.go:76,88), so the caller may write into it.  The
+//     entry is then marked exposed and is re-verified on every later
+//     ReadFromDisk, as in the reference, until WriteBlock or a disk read
+//     replaces it.
 package block_manager
 
 import (
@@ -18,13 +34,18 @@ import (
 	"sync/atomic"
 )
 
-// cachedBlock is what the block cache holds: the block's bytes and whether
-// their CRC has been checked.  Blocks the engine writes carry a valid CRC by
-// construction (AddCRCsToData / AddCRCToBlockData before WriteBlock), so
-// WriteBlock caches them as verified; blocks read from disk start unverified.
+// cachedBlock is what the block cache holds: the block's bytes, whether their
+// CRC has been checked, and whether a caller holds the slice (ReadBlock).
+// data is never written through by this package.
 type cachedBlock struct {
 	data     []byte
 	verified atomic.Bool
+	exposed  atomic.Bool
+}
+
+// trusted: the bytes were checked and no caller can have changed them since.
+func (cb *cachedBlock) trusted() bool {
+	return cb.verified.Load() && !cb.exposed.Load()
 }
 
 // BlockManager as in block_manager.go:34-38 with the cache value changed.
@@ -36,6 +57,7 @@ type BlockManager struct {
 
 // readCached replaces ReadBlock (block_manager.go:72-98) on the read path: the
 // same cache / file-lock / double-check protocol, returning the cache entry.
+// A block read from disk starts unverified and unexposed.
 func (bm *BlockManager) readCached(location block_location.BlockLocation) (*cachedBlock, error) {
 	if cb, err := bm.blockCache.Get(location); err == nil {
 		return cb, nil
@@ -55,16 +77,20 @@ func (bm *BlockManager) readCached(location block_location.BlockLocation) (*cach
 	return cb, nil
 }
 
-// ReadBlock keeps its signature (block_manager.go:72): the bytes only.
+// ReadBlock keeps its signature and aliasing (block_manager.go:72-98): the
+// cached bytes themselves.  The entry is exposed from here on.
 func (bm *BlockManager) ReadBlock(location block_location.BlockLocation) ([]byte, error) {
 	cb, err := bm.readCached(location)
 	if err != nil {
 		return nil, err
 	}
+	cb.exposed.Store(true)
 	return cb.data, nil
 }
 
-// WriteBlock as block_manager.go:101-114; the written block is cached as verified.
+// WriteBlock as block_manager.go:101-114.  The cache keeps a copy of what went
+// to disk; it is verified only if its CRC checks.  One host CRC per written
+// block (well under 1 us for 4 KiB), which every later read of it then skips.
 func (bm *BlockManager) WriteBlock(location block_location.BlockLocation, data []byte) error {
 	mutex := bm.getFileMutex(location.FilePath)
 	mutex.Lock()
@@ -72,16 +98,16 @@ func (bm *BlockManager) WriteBlock(location block_location.BlockLocation, data [
 	if err := bm.writeBlockToDisk(location, data); err != nil {
 		return errors.New("block not written successfully")
 	}
-	cb := &cachedBlock{data: data}
-	cb.verified.Store(true)
+	cb := &cachedBlock{data: append([]byte(nil), data...)}
+	cb.verified.Store(crc_util.CheckBlockIntegrity(cb.data) == nil)
 	bm.blockCache.Put(location, cb)
 	return nil
 }
 
 // ReadFromDisk (block_manager.go:189-242): same arguments, results and error
-// values; every touched block not yet verified is checked in one batch (GPU from
-// 256 blocks), cached blocks already verified are not hashed again, and blocks
-// verified here are marked in the cache.
+// values; every touched block not trusted is checked in one batch (GPU from
+// 256 blocks), trusted cache entries are not hashed again, and blocks verified
+// here are marked in the cache (an exposed one stays re-checked).
 func (bm *BlockManager) ReadFromDisk(filePath string, startOffset uint64, size uint64) ([]byte, uint64, error) {
 	bs := uint64(bm.blockSize)
 	k := crc_util.ReadBlocksTouched(bm.blockSize, startOffset, size)
@@ -95,7 +121,7 @@ func (bm *BlockManager) ReadFromDisk(filePath string, startOffset uint64, size u
 			return nil, 0, err // the Go loop fails at the first unreadable block too
 		}
 		entries[i] = cb
-		verified[i] = cb.verified.Load()
+		verified[i] = cb.trusted()
 		raw = append(raw, cb.data...)
 	}
 	out, final, err := crc_util.ReadVerifiedCached(raw, bm.blockSize, startOffset, size, verified)

@@ -65,9 +65,9 @@ func CheckRecords(data []byte, off []uint64, lens []uint32, stored []byte) (bool
 	}
 	var valid C.int
 	var nm C.uint64_t
-	var built, other [16]byte
+	var mismBuilt, mismStored [16]byte
 	rc := C.hc_merkle_validate(u8p(levels), C.uint64_t(n), u8p(stored), C.uint64_t(len(stored)), &valid,
-		(*C.uint8_t)(unsafe.Pointer(&built[0])), (*C.uint8_t)(unsafe.Pointer(&other[0])), &nm)
+		(*C.uint8_t)(unsafe.Pointer(&mismBuilt[0])), (*C.uint8_t)(unsafe.Pointer(&mismStored[0])), &nm)
 	if rc != C.HC_OK {
 		return false, nil, fmt.Errorf("failed to validate Merkle tree: %s", C.GoString(C.hc_strerror(rc)))
 	}
@@ -77,5 +77,5 @@ func CheckRecords(data []byte, off []uint64, lens []uint32, stored []byte) (bool
 	if nm == 0 {
 		return false, nil, nil
 	}
-	return false, [][16]byte{built}, nil
+	return false, [][16]byte{mismBuilt}, nil
 }

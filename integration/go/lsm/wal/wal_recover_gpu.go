@@ -95,6 +95,12 @@ func (wal *WAL) recoverMemtable(mt *memtable.MemTable, position *WalPosition) er
 			return fmt.Errorf("failed to process block %s:%d: %w", path(locs[k]), locs[k].block, err)
 		}
 		if readErr != nil {
+			// wal.go:378-380 returns with position on the unreadable block and
+			// Offset as the block before it left it: CRC_SIZE (:393), or the
+			// caller's Offset when it is the first block of the call.  readAt is
+			// an index into locs (the whole call), not into this window, so a
+			// window restarted at a pending fragment (start > 0) still gives
+			// CRC_SIZE, which is what the reference's one pass holds there.
 			off := uint64(crc.CRC_SIZE)
 			if readAt == 0 {
 				off = position.Offset

@@ -16,20 +16,26 @@ import "C"
 
 import (
 	"errors"
+	"sync"
 	"unsafe"
 )
 
-// GPUAvailable reports whether a gfx950 device is visible (checked once at
-// init).  The utils/crc drop-ins work without one (single buffers and
-// AddCRCsToData run on the host CPU then); the batched helpers below
-// (CheckBlocksIntegrity, AddCRCToBlocks, ReadVerified*) return an error
-// instead, never a silent CPU fallback.  A deployment that relies on them
-// should check GPUAvailable at startup rather than discover it mid-flush.
-var GPUAvailable bool
-
-func init() {
-	GPUAvailable = C.hc_device_count() > 0
+// GPUAvailable reports whether a gfx950 device is visible, probed on the first
+// call only (importing the package starts no HIP runtime).  The utils/crc
+// drop-ins work without one (single buffers and AddCRCsToData run on the host
+// CPU then); the batched helpers below (CheckBlocksIntegrity, AddCRCToBlocks,
+// ReadVerified*) return an error instead, never a silent CPU fallback.  A
+// deployment that relies on them should call GPUAvailable at startup rather
+// than discover it mid-flush.
+func GPUAvailable() bool {
+	gpuOnce.Do(func() { gpuAvail = C.hc_device_count() > 0 })
+	return gpuAvail
 }
+
+var (
+	gpuOnce  sync.Once
+	gpuAvail bool
+)
 
 // BLOCK_SIZE keeps the typed-uint64 form and CRC_SIZE the untyped form of
 // crc_util.go:11-12 (CRC_SIZE is used in both int and uint64 contexts).
@@ -185,8 +191,9 @@ func ReadBlocksTouched(blockSize uint16, startOffset, size uint64) int {
 
 // ReadVerifiedCached is ReadVerified with the block cache's verified bits
 // (row f1): verified[i] == true marks block i of raw (relative to
-// startOffset/blockSize) as already checked -- a cache entry verified when it
-// was read from disk or written by the engine -- so it is not hashed again.
+// startOffset/blockSize) as already checked -- a cache entry whose bytes were
+// CRC-checked (on an earlier read, or when WriteBlock cached its copy) and that
+// no caller can have changed since -- so it is not hashed again.
 // On return verified[i] is also true for every block this call verified clean,
 // which the caller records in its cache entries.
 func ReadVerifiedCached(raw []byte, blockSize uint16, startOffset, size uint64, verified []bool) ([]byte, uint64, error) {
@@ -239,13 +246,13 @@ func WalReplay(blocks []byte, blockSize int, startOffset uint64) (WalWindow, err
 	buf := make([]byte, len(blocks)+1)
 	off := make([]uint64, slots)
 	ln := make([]uint64, slots)
-	ends := make([]uint64, slots)
+	endBlk := make([]uint64, slots)
 	pend := make([]uint64, 2)
 	var nrec, posBlock, posOffset C.uint64_t
 	var bad C.int64_t = -1
 	rc := C.hc_wal_replay_v(ptr(blocks), C.uint64_t(nb), C.uint32_t(blockSize), 0, C.uint64_t(startOffset), 0,
 		ptr(buf), C.uint64_t(len(buf)), (*C.uint64_t)(unsafe.Pointer(&off[0])), (*C.uint64_t)(unsafe.Pointer(&ln[0])),
-		(*C.uint64_t)(unsafe.Pointer(&ends[0])), C.uint64_t(slots), &nrec, &posBlock, &posOffset, &bad,
+		(*C.uint64_t)(unsafe.Pointer(&endBlk[0])), C.uint64_t(slots), &nrec, &posBlock, &posOffset, &bad,
 		(*C.uint64_t)(unsafe.Pointer(&pend[0])))
 	w := WalWindow{PendBlock: -1, StopBlock: uint64(posBlock), StopOffset: uint64(posOffset)}
 	if rc < 0 {
@@ -255,7 +262,7 @@ func WalReplay(blocks []byte, blockSize int, startOffset uint64) (WalWindow, err
 	for i := range w.Records {
 		w.Records[i] = buf[off[i] : off[i]+ln[i] : off[i]+ln[i]]
 	}
-	w.EndBlocks = ends[:int(nrec)]
+	w.EndBlocks = endBlk[:int(nrec)]
 	if pend[0] != ^uint64(0) {
 		w.PendBlock, w.PendOffset = int64(pend[0]), pend[1]
 	}

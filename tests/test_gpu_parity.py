@@ -219,6 +219,55 @@ def test_uniform_nonconforming_goes_general(cuda, hc, oracle):
         assert (got == want).all(), (size, stride)
 
 
+def test_off_only_and_len_only(cuda, hc, oracle):
+    """hundcrc.h lets a device batch pass only one of off[] / len[]: off[i]
+    with the uniform length, or block i at i * stride with len[i].  Both go
+    to k_crc_any (k_crc_grp takes both arrays or neither), in block mode,
+    whole-message mode and verify mode."""
+    torch = cuda
+    rng = np.random.default_rng(29)
+    n = 6000
+    # off only: shuffled 4 KiB blocks (the shape k_crc_grp would take with len[])
+    size = 4096
+    host = rng.integers(0, 256, n * size + 64, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    off = (rng.permutation(n).astype(np.uint64) * size) + np.uint64(16)
+    lens = np.full(n, size, dtype=np.uint32)
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    got = dev_crc(torch, hc, buf, n, off=doff, ulen=size)
+    assert hc.last_launch()["kernel"] == "k_crc_any"
+    assert (got == oracle.crc32_blocks(host, off=off, lens=lens, threads=16)).all()
+    got = dev_crc(torch, hc, buf, n, off=doff, ulen=size, flags=hc.HC_F_MESSAGES)
+    assert (got == oracle.crc32_messages(host, off, lens, threads=16)).all()
+    # len only: block i at i * stride, any length up to the stride (0..3 incl.)
+    stride = 9008
+    lens = rng.integers(0, stride + 1, n).astype(np.uint32)
+    lens[:8] = np.arange(8)
+    lens[8:100] = 4096
+    host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    off = np.arange(n, dtype=np.uint64) * stride
+    dlen = torch.from_numpy(lens.view(np.int32)).cuda()
+    got = dev_crc(torch, hc, buf, n, lens=dlen, stride=stride)
+    assert hc.last_launch()["kernel"] == "k_crc_any"
+    want = oracle.crc32_blocks(host, off=off, lens=lens, threads=16)
+    assert (got == want).all()
+    # verify with len only: every block clean except the ones under 4 bytes
+    stamped = host.copy()
+    for i in range(n):
+        if lens[i] >= 4:
+            stamped[i * stride:i * stride + 4] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    buf = torch.from_numpy(stamped).cuda()
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    hc.dev_verify_prepare(bm, fb, n)
+    hc.dev_crc32_blocks(buf, None, lens=dlen, stride=stride, nblocks=n, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    bits = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    assert np.array_equal(np.nonzero(bits)[0], np.nonzero(lens < 4)[0])
+    assert int(fb.item()) == 0
+
+
 def test_messages_mode(cuda, hc, oracle):
     """GetCRC over variable-length records (WAL records 64 B..64 KiB, config 5b)."""
     torch = cuda

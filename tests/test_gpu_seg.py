@@ -112,6 +112,25 @@ def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
     check(torch, hc, oracle, host, buf, packed(small, 0), small, True)
 
 
+def test_seg_without_crc_out(cuda, hc, oracle, seg_all):
+    """crc_out is optional (hundcrc.h): a packed whole-message batch with no
+    crc_out is not offered to the stream, whose only output is crc_out
+    (k_seg_combine), and runs without touching a null pointer."""
+    torch = cuda
+    rng = np.random.default_rng(13)
+    lens = rng.integers(64, 3000, 4000).astype(np.uint64)
+    off = packed(lens, 7)
+    host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 16, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
+    hc.dev_crc32_blocks(buf, None, nblocks=len(off), off=doff, lens=dlen, flags=hc.HC_F_MESSAGES)
+    torch.cuda.synchronize()
+    assert not hc.seg_taken()
+    assert hc.last_launch()["kernel"] == "k_crc_grp+k_crc_any"
+    check(torch, hc, oracle, host, buf, off, lens, True)  # the same batch with crc_out: the stream
+
+
 def test_seg_threshold(cuda, hc, oracle, monkeypatch):
     """Below HC_SEG_MIN_MSGS (default 131072 messages) the batch is not offered
     to the stream."""
