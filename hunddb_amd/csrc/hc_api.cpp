@@ -192,7 +192,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       info.kernel = "k_crc_grp";
       info.fast_blocks = n;
     } else if (fast) {
-      e = launch_fast(b, true, fast_grid, s);
+      e = launch_fast(b, fast_grid, s);
       info.fast_blocks = n;
     } else {
       e = launch_general(b, 0, gen_grid, s);

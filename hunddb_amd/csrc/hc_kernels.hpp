@@ -40,17 +40,13 @@ constexpr uint32_t kFastLdsBytes = kLdsMainBytes + kLdsS4Bytes;
 
 
 // Host launchers; return the hipError_t of the launch.
-// uniform_fast: the host proved every block satisfies the streaming kernel's
-// layout contract (16-B aligned start, length a positive multiple of 1024).
-hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s);
-// fast_mask != 0: process only the blocks a streaming kernel skipped, i.e. all
-// but the 16-B aligned ones whose length is a positive multiple of fast_mask+1
-// (1023: k_crc_fast; 4095: k_crc_grp).  0: every block.
-// Production: 64-message windows handed out per workgroup (launch_general_dyn
-// with one window per hand-out); launch_general_static: round 1's static runs.
+// k_crc_fast: uniform batches only (no off/len arrays), every block 16-B
+// aligned with a length that is a positive multiple of 1024 (refused otherwise).
+hipError_t launch_fast(const Batch &b, int grid, hipStream_t s);
+// k_crc_any.  fast_mask != 0: process only the blocks a streaming kernel
+// skipped, i.e. all but the 16-B aligned ones whose length is a positive
+// multiple of fast_mask+1 (4095: k_crc_grp).  0: every block.
 hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s);
-hipError_t launch_general_static(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s);
-hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s, int lg_chunk = 0);
 // k_crc_grp: 4 KiB-multiple blocks (uniform, or off/len with device-side
 // routing of the others to k_crc_any with fast_mask 4095), per-workgroup
 // dynamic hand-out of chunked blocks.

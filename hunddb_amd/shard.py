@@ -137,6 +137,72 @@ def spawn_ranks(cmd, nproc: int, port: int = 0, env=None, timeout=None) -> int:
     return rc
 
 
+def rank_identity(device=None, kernel_ms=None) -> dict:
+    """What this rank ran on, for a multi-GPU result that proves itself: host,
+    pid, the GPU's PCI address and UUID as the HIP runtime reports them, the
+    number of GPUs the process sees and how many of them libhundcrc accepts
+    (gfx950), and the rank's own mean kernel time.  device=None: a CPU rank."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    ident = {"rank": dist.get_rank() if dist.is_initialized() else 0, "host": socket.gethostname(),
+             "pid": os.getpid()}
+    if device is not None and torch.cuda.is_available():
+        from . import crc
+        dev = torch.device(device)
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(idx)
+        ident.update({"device": idx, "name": p.name,
+                      "bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+                      "uuid": str(p.uuid), "visible_devices": torch.cuda.device_count(),
+                      "hc_devices": crc.device_count()})
+    else:
+        ident.update({"device": "cpu", "name": "cpu", "bus_id": "cpu", "uuid": None,
+                      "visible_devices": 0, "hc_devices": 0})
+    ident["kernel_ms"] = None if kernel_ms is None else round(float(kernel_ms), 4)
+    return ident
+
+
+def gather_identities(ident: dict, group=None) -> list:
+    """Every rank's rank_identity(), in rank order, on every rank."""
+    import torch.distributed as dist
+
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, ident, group=group)
+    return out
+
+
+def device_proof(idents: list, backend: str, group=None) -> dict:
+    """The multi_gpu fields that show which devices the ranks really used:
+    the per-rank table, the number of distinct (host, PCI address) pairs, the
+    communicator size, the RCCL version and the spread of per-rank kernel
+    times.  `rehearsal` is true when ranks share a device (a one-GPU gloo run):
+    such a line is not an N-GPU measurement."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else len(idents)
+    distinct = len({(i["host"], i["bus_id"]) for i in idents})
+    ks = [i["kernel_ms"] for i in idents if i.get("kernel_ms") is not None]
+    ver = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            ver = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception as e:  # noqa: BLE001 (reported, not hidden)
+            ver = f"unknown ({e})"
+    out = {"ranks": idents, "distinct_devices": distinct, "comm_world_size": world, "backend": backend,
+           "rccl_version": ver,
+           "kernel_ms_max": max(ks) if ks else None, "kernel_ms_min": min(ks) if ks else None,
+           "rehearsal": distinct != world}
+    if out["rehearsal"]:
+        out["rehearsal_note"] = (f"{world} ranks on {distinct} distinct device(s): a rehearsal of the N-GPU path, "
+                                 "not an N-GPU measurement")
+    return out
+
+
 def job_timing(wall_s: float, kernel_s: float, local_bytes: float, device=None, group=None):
     """Whole-job numbers for the benchmark: (max wall over ranks, max mean
     kernel time over ranks, sum of bytes over ranks)."""

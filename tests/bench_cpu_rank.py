@@ -6,8 +6,9 @@ per-GPU CRC kernel is replaced by the oracle (the checker), because the CPU
 container has no GPU; everything around it is bench.py's: argument parsing,
 the strong-scaling shard of one global batch (hunddb_amd.shard.index_range),
 the global-index fill, the gloo gather of the words to rank 0, the
-max-over-ranks clock, and one JSON line printed by rank 0 with the gathered
-words' check against a single-process run of the whole batch.
+max-over-ranks clock, the per-rank device table (bench.py's multi_gpu proof
+fields), and one JSON line printed by rank 0 with the gathered words' check
+against a single-process run of the whole batch.
 """
 import json
 import os
@@ -41,6 +42,7 @@ def main():
     t0 = time.perf_counter()
     local = O.crc32_blocks(buf, stride=B, ulen=B)
     dt = time.perf_counter() - t0
+    proof = shard.device_proof(shard.gather_identities(shard.rank_identity(None, dt * 1e3)), "gloo")
     dt, _, tot = shard.job_timing(dt, dt, float(buf.size))
     got = shard.gather_crcs(torch.from_numpy(local.view(np.int32)), counts)
     if rank == 0:
@@ -50,7 +52,8 @@ def main():
         want = O.crc32_blocks(full, stride=B, ulen=B)
         same = bool(np.array_equal(got.numpy().view(np.uint32), want))
         print(json.dumps({"n_gpus": world, "scaling": "strong", "blocks_total": n, "counts": counts,
-                          "bytes": tot, "words_match_1proc": same, "value": tot / dt / 2**30}), flush=True)
+                          "bytes": tot, "words_match_1proc": same, "value": tot / dt / 2**30,
+                          "multi_gpu": proof}), flush=True)
     dist.destroy_process_group()
 
 

@@ -27,6 +27,65 @@ def test_self_launch_strong_scaling_words(world):
     assert res["n_gpus"] == world and res["scaling"] == "strong"
     assert sum(res["counts"]) == 3001 and res["bytes"] == 3001 * 4096
     assert res["words_match_1proc"] is True
+    # the multi_gpu proof fields bench.py prints at N > 1 (hunddb_amd.shard.device_proof)
+    m = res["multi_gpu"]
+    assert [r["rank"] for r in m["ranks"]] == list(range(world))
+    assert len({r["pid"] for r in m["ranks"]}) == world
+    assert all(r["kernel_ms"] is not None and r["bus_id"] == "cpu" for r in m["ranks"])
+    assert m["comm_world_size"] == world and m["backend"] == "gloo" and m["rccl_version"] is None
+    assert m["kernel_ms_min"] <= m["kernel_ms_max"]
+    # every rank on one host and no GPU: flagged as a rehearsal, not an N-GPU run
+    assert m["distinct_devices"] == 1 and m["rehearsal"] is True and "rehearsal" in m["rehearsal_note"]
+
+
+def test_device_proof_distinct_devices():
+    """distinct_devices counts (host, PCI address) pairs: N ranks on N GPUs is
+    not a rehearsal; two ranks on one GPU, or one address on two hosts' ranks
+    seen as the same host, are."""
+    from hunddb_amd import shard
+    ids = [{"rank": r, "host": "h", "bus_id": f"0000:{0x11 + r:02x}:00", "kernel_ms": 1.0 + r} for r in range(8)]
+    p = shard.device_proof(ids, "gloo")
+    assert p["distinct_devices"] == 8 and p["rehearsal"] is False and "rehearsal_note" not in p
+    assert (p["kernel_ms_min"], p["kernel_ms_max"]) == (1.0, 8.0)
+    ids[3]["bus_id"] = ids[2]["bus_id"]
+    p = shard.device_proof(ids, "gloo")
+    assert p["distinct_devices"] == 7 and p["rehearsal"] is True
+
+
+def test_bench_error_line_names_the_rank():
+    """Any exception in a bench rank ends in ONE JSON error line naming the
+    rank, and a non-zero exit."""
+    code = ("import sys, os; sys.path.insert(0, %r); import bench; "
+            "bench.main = lambda: (_ for _ in ()).throw(ValueError('boom')); bench._run()" % ROOT)
+    env = dict(os.environ, RANK="2", WORLD_SIZE="4")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 3
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["rank"] == 2 and res["value"] is None and res["error"] == "rank 2: ValueError: boom"
+
+
+def test_cpu_baseline_reports_cores_it_used(oracle):
+    """cpu_baseline's `cores` is the thread count it timed, cores_available is
+    the affinity set capped by the cgroup quota, and the spread is reported
+    against the median."""
+    import numpy as np
+
+    import bench
+    n, B = 2000, 4096
+    buf = np.random.default_rng(1).integers(0, 256, n * B, dtype=np.uint8)
+    off = np.arange(n, dtype=np.uint64) * B
+    lens = np.full(n, B, dtype=np.uint32)
+    threads = bench.cores_available()
+    assert threads == min(len(os.sched_getaffinity(0)), int(bench.cgroup_cpu_quota() or 1 << 30))
+    res = bench.cpu_baseline(buf, off, lens, threads, 0.5, "test",
+                             gpu_words=oracle.crc32_blocks(buf, stride=B, ulen=B))
+    assert res["cores"] == threads == res["cores_available"]
+    assert res["logical_cpus"] == os.cpu_count() and res["affinity_cpus"] == len(os.sched_getaffinity(0))
+    lo, hi = res["spread_pct"]
+    assert lo <= 0.0 <= hi and res["matches_gpu"] is True
+    assert "nproc" not in res
 
 
 def test_self_launch_parent_never_imports_torch_cuda():

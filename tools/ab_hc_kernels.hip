@@ -1,3 +1,14 @@
+// ab_hc_kernels.hip -- A/B HARNESS SOURCE, NOT THE PRODUCT.  The round-2 product
+// kernel file (hunddb_amd/csrc/hc_kernels.hip at commit d623f6c) with every
+// A/B switch it carried: FastCfg's LDS-DMA ring (kStage), timing-only builds
+// (kNull, kVar bit 3, k_seg_stream kNoEv), k_crc_grp's kDyn/kPin/kBatch/kNib,
+// k_crc_any's kVar bits, k_frame/k_unframe depth, store order and cache policy,
+// and the HC_META_WINDOW=0 scalar-metadata path.  The tool harnesses
+// (kbench, kbench2, kframe, kcopy) include this file instead of the product
+// source, so the variants behind DESIGN.md's A/B tables stay measurable while
+// the product file holds only the production instantiations (round 3).  Its
+// production instantiations are the same code as the product's kernels.
+
 // hc_kernels.hip — hand-written gfx950 (CDNA4) kernels of the batched
 // block-checksum engine.  CRC-32/IEEE exactly as Go's crc32.ChecksumIEEE,
 // applied per block the way /root/reference/utils/crc/crc_util.go:21-33 (stamp)
@@ -32,8 +43,14 @@
 #include <climits>
 #include <cstdint>
 
-#include "hc_kernels.hpp"
-#include "hc_util.hpp"
+#include "../hunddb_amd/csrc/hc_kernels.hpp"
+#include "../hunddb_amd/csrc/hc_util.hpp"
+
+namespace hc {  // the round-2 launchers the product no longer declares
+hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s);
+hipError_t launch_general_static(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s);
+hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s, int lg_chunk = 0);
+}  // namespace hc
 
 namespace hc {
 
@@ -48,6 +65,11 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_a
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // 32x32 GF(2) mat-vec: XOR of col[i] over the set bits i of d.
 __device__ __forceinline__ uint32_t matvec32(const uint32_t (&col)[32], uint32_t d) {
@@ -126,54 +148,101 @@ __device__ __forceinline__ void lane0_atomic_umin64(unsigned long long *p, uint6
 }
 
 // ---------------------------------------------------------------------------
-// k_crc_fast: uniform batches of 16-B aligned blocks whose length is a
-// multiple of 1 KiB but not of 4 KiB (4 KiB multiples take k_crc_grp).
-// Block b goes to wave b % W (W = every wave of the grid), so all waves sweep
-// memory together.  Each wave keeps a ring of kFastRing rows in VGPRs: the row
-// just hashed is refilled at once, so kFastRing - 1 rows stay in flight while
-// one is hashed.  Round 1 (tools/kbench, profiles/r1/glds/): non-temporal
-// loads +17 %, a ring of 4 best, this block order 0-7 % ahead of contiguous
-// runs per wave.  The LDS-staged ring it was measured against, the timing-only
-// build and the round-1 off/len path live in tools/ab_hc_kernels.hip.
-constexpr int kFastRing = 4;
+// Streaming kernel.  Pointer arguments are separate __restrict__ kernel
+// arguments so the per-block metadata reads (off/len) become scalar s_loads
+// (lgkmcnt) instead of vector loads that would drain the row ring (vmcnt(0)).
+//
+// Tunables (FastCfg): waves per workgroup (one workgroup per CU, LDS-bound),
+// ring depth (rows in flight per wave = kRing-1 while one is hashed), load
+// cache policy (0 plain, 1 nontemporal), block order (0: each wave owns a
+// contiguous run of blocks; 1: block b goes to wave b % W -- uniform layout
+// only), kNull (timing-only build: rows are XOR-folded instead of
+// CRC'd, to measure the memory ceiling of exactly this access pattern),
+// kStage (rows land in a per-wave ring of kRing 1 KiB LDS slots by LDS-DMA,
+// global_load_lds_dwordx4, instead of a VGPR ring) and kS4Rep (replicas of
+// the 4-byte shift tables: fewer replicas leave LDS room for the ring; 0 =
+// no table, the shift is a 32x32 GF(2) mat-vec on the VALU).
+template <int W_, int R_, int P_, int O_, bool N_ = false, bool S_ = false, int S4_ = 4>
+struct FastCfg {
+  static constexpr int kWaves = W_, kRing = R_, kPolicy = P_, kOrder = O_;
+  static constexpr bool kNull = N_, kStage = S_;
+  static constexpr int kS4Rep = S4_;
+  static constexpr uint32_t kS4Bytes = 4096u * S4_;  // 0: s4 shift on the VALU
+  static constexpr uint32_t kRingBytes = S_ ? (uint32_t)W_ * R_ * kRowBytes : 0u;
+  static constexpr uint32_t kLdsBytes = kLdsMainBytes + kS4Bytes + kRingBytes;
+  static_assert(kLdsBytes <= 163840u, "LDS budget: 160 KiB per CU");
+  static_assert(S4_ == 0 || S4_ == 1 || S4_ == 2 || S4_ == 4, "s4 replicas");
+  static_assert(!S_ || (P_ == 0 || P_ == 1), "LDS-DMA rows: plain or nt policy");
+};
+// kbench: nt loads +17 %, ring 4 best; interleaved block order (block b ->
+// wave b % W, uniform layouts) 0-7 % over contiguous runs, never slower
+// (profiles/r1/glds/)
+using DefaultFastCfg = FastCfg<kFastWaves, 4, 1, 1>;
 
-// Row load, 16 B per lane, non-temporal (the blocks are read once).
+// Row load, 16 B per lane.  Policy 0: plain global_load_dwordx4; 1: the same
+// with the nontemporal (nt) bit; 2..5: buffer_load_dwordx4 with cache-policy
+// bits (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16) nt, sc0|nt, sc1|nt, sc0|sc1|nt.
+template <int kPolicy>
 __device__ __forceinline__ uint4 load_row(const uint8_t *row, uint32_t lane) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(row + lane * 16u));
+  u32x4 v;
+  if constexpr (kPolicy == 0) {
+    v = *reinterpret_cast<const u32x4 *>(row + lane * 16u);
+  } else if constexpr (kPolicy == 1) {
+    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(row + lane * 16u));
+  } else {
+    constexpr int aux = kPolicy == 2 ? 2 : kPolicy == 3 ? 3 : kPolicy == 4 ? 18 : 19;
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(row), 0, kRowBytes, 0x00020000);
+    v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16u, 0, aux));
+  }
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// The replicated LDS tables every CRC kernel uses: the row-shift tables (main
-// region: table k, byte v, replica r at (k>>1)<<16 | v<<8 | (k&1)<<7 | r<<2,
-// 32 replicas, conflict-free) and the 4-byte shift tables (kLdsMainBytes +
-// (k*256 + v)*16 + r*4, 4 replicas).
-__device__ __forceinline__ void fill_crc_tables(uint32_t *lds, const DeviceTables *tables, uint32_t tid,
-                                                uint32_t nthreads) {
+// Row load by LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at
+// slot + 16 l; the LDS base is wave-uniform (M0).  Policy 1 sets nt.
+template <int kPolicy>
+__device__ __forceinline__ void dma_row(const uint8_t *row, uint8_t *slot, uint32_t lane) {
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(row + lane * 16u), (lds_void_t *)slot, 16, 0,
+                                   kPolicy ? 2 : 0);
+}
+
+template <bool kUniform, class Cfg>
+__global__ __launch_bounds__(Cfg::kWaves * 64) void k_crc_fast(
+    const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+    uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks,
+    uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
+    unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables) {
+  constexpr int kWaves = Cfg::kWaves, kThreads = kWaves * 64, kRing = Cfg::kRing;
+  constexpr bool kInterleave = kUniform && Cfg::kOrder == 1;
+  constexpr uint32_t kS4R = Cfg::kS4Rep;
+  // tables and the row ring are separate LDS variables: their accesses carry
+  // distinct alias scopes, so hipcc's waitcnt pass does not wait for the
+  // in-flight row DMA before a table lookup
+  __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsMainBytes + Cfg::kS4Bytes) / 4];
+  // kS4R == 0: columns of the 4-byte shift (bit i of byte j -> s4[j][1 << (i % 8)]),
+  // wave-uniform
+  uint32_t s4col[32];
+  if constexpr (kS4R == 0) {
+#pragma unroll
+    for (int i = 0; i < 32; i++) s4col[i] = uni(tables->s4[i >> 3][1u << (i & 7)]);
+  }
+  __shared__ __attribute__((aligned(16))) uint8_t ring_lds[Cfg::kStage ? Cfg::kRingBytes : 16];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+
+  // Fill the replicated tables.  Main region address of (table k, byte v,
+  // replica r) = (k>>1)<<16 | v<<8 | (k&1)<<7 | r<<2; s4 region address
+  // = kLdsMainBytes + (k*256 + v)*4*kS4R + (r%kS4R)*4.
   const uint32_t *tg = &tables->tg[0][0];
-  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += nthreads) {
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kThreads) {
     const uint32_t a = q * 16;
     const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
     const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
     *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
   }
   const uint32_t *s4 = &tables->s4[0][0];
-  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += nthreads) {
-    const uint32_t v = s4[q];
-    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) = make_uint4(v, v, v, v);
-  }
-}
-
-__global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, uint64_t stride, uint32_t ulen,
-                                                          uint32_t flags, uint64_t nblocks,
-                                                          uint32_t *__restrict__ crc_out,
-                                                          uint32_t *__restrict__ bad_bitmap,
-                                                          unsigned long long *__restrict__ first_bad,
-                                                          const DeviceTables *__restrict__ tables) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+  for (uint32_t q = tid; q < 1024u * kS4R; q += kThreads) lds[kLdsMainBytes / 4 + q] = s4[q / kS4R];
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
@@ -182,11 +251,12 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
 
   const uint32_t r4 = (lane & 31u) << 2;
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
-  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
+  const uint32_t S4base = kLdsMainBytes + (kS4R ? (lane % (kS4R ? kS4R : 1)) << 2 : 0u);
   const bool msg = (flags & kFlagMessages) != 0;
 
   // c <- shift(c, 1024) ^ w : four conflict-free lookups, one v_perm each.
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (Cfg::kNull) return c ^ w;
     const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
     const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
     const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
@@ -194,64 +264,196 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
     return xor3(xor3(t0, t1, t2), t3, w);
   };
   auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
-    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
-    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
-    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
-    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
+    if constexpr (kS4R == 0) return matvec32(s4col, x) ^ w;
+    constexpr uint32_t E = 4u * kS4R, T = 1024u * kS4R;  // entry, table strides
+    const uint32_t t0 = lds_u32(lds, S4base + (x & 255u) * E);
+    const uint32_t t1 = lds_u32(lds, S4base + T + ((x >> 8) & 255u) * E);
+    const uint32_t t2 = lds_u32(lds, S4base + 2 * T + ((x >> 16) & 255u) * E);
+    const uint32_t t3 = lds_u32(lds, S4base + 3 * T + (x >> 24) * E);
     return xor3(xor3(t0, t1, t2), t3, w);
   };
 
   const uint32_t wave = uni(tid >> 6);
-  const uint64_t step = (uint64_t)gridDim.x * kFastWaves;  // block b -> wave b % step
-  const uint32_t rows = ulen >> 10;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kWaves;
+  const uint64_t b0 = kInterleave ? gw : uni64(nblocks * gw / W);
+  const uint64_t b1 = kInterleave ? nblocks : uni64(nblocks * (gw + 1) / W);
 
-  // ---- producer: cursor over this wave's blocks and the rows of the current one
-  uint64_t pb = (uint64_t)blockIdx.x * kFastWaves + wave;
-  if (pb >= nblocks) return;
-  const uint8_t *pptr = base + pb * stride;
-  uint32_t prow = 0;
-  bool pvalid = true;
-  // Each ring slot carries the wave-uniform tag of the row it holds.  The load
-  // is unconditional (past the wave's last row it re-reads that row, tagged
-  // invalid) so hipcc's wait counting stays exact: vmcnt(kFastRing-1).
+  const uint64_t step = kInterleave ? W : 1;
+  auto conform = [&](uint64_t o, uint32_t l) {
+    return kUniform || ((((uintptr_t)base + o) & 15u) == 0 && (l & 1023u) == 0 && l != 0);
+  };
+
+  // ---- producer ------------------------------------------------------------
+  // Cursor over this wave's blocks (b0, b0+step, ... < b1) and the rows of the
+  // current one.
+  uint64_t pb = 0;
+  const uint8_t *pptr = nullptr;
+  uint32_t prow = 0, prows = 0;
+  bool pvalid = false;
+#ifndef HC_META_WINDOW
+#define HC_META_WINDOW 1
+#endif
+#if HC_META_WINDOW
+  // Metadata (off/len arrays only): a window of 64 blocks lives in 3 VGPRs
+  // (lane j holds block wbase + j*step) and is read per block with
+  // v_readlane.  It is refilled synchronously once per 64 blocks: that one
+  // wait drains the row ring, 1/64 of the per-block stall a scalar or vector
+  // load of every block's entry costs (SMEM returns out of order, so any
+  // pending s_load turns the next LDS-lookup wait into lgkmcnt(0)).
+  uint64_t wbase = ~0ull;
+  uint32_t wo_lo = 0, wo_hi = 0, wl = 0;
+  auto meta = [&](uint64_t i, uint64_t &o, uint32_t &l) {
+    if (wbase == ~0ull || (i - wbase) / step >= 64) {
+      wbase = i;
+      // opaque copy of i: the window address is computed afresh, never
+      // strength-reduced across the inlined call sites
+      uint64_t iw = i;
+      asm volatile("" : "+s"(iw));
+      const uint64_t j = iw + (uint64_t)lane * step;
+      const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
+      wo_lo = (uint32_t)oj;
+      wo_hi = (uint32_t)(oj >> 32);
+      wl = j < b1 ? (lens ? lens[j] : ulen) : 0;
+      // consume the loads here, inside the refill branch, so hipcc's
+      // vmcnt(0) for them is not hoisted to the (per-block) merge point
+      asm volatile("" : "+v"(wo_lo), "+v"(wo_hi), "+v"(wl));
+    }
+    const uint32_t k = uni((uint32_t)((i - wbase) / step));
+    // readlane returns int: each half goes through uint32_t before widening,
+    // or an offset whose low word is >= 2^31 sign-extends into the high word
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(wo_lo, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(wo_hi, k);
+    o = ((uint64_t)hi << 32) | (uint64_t)lo;
+    l = (uint32_t)__builtin_amdgcn_readlane(wl, k);
+  };
+#else
+  // Metadata (off/len arrays only) is read through the constant address
+  // space so hipcc emits scalar s_loads, counted by lgkmcnt -- never by the
+  // vmcnt of the row ring.
+  typedef const __attribute__((address_space(4))) uint64_t *c64p;
+  typedef const __attribute__((address_space(4))) uint32_t *c32p;
+  const c64p coffs = (c64p)offs;
+  const c32p clens = (c32p)lens;
+  auto meta = [&](uint64_t i, uint64_t &o, uint32_t &l) {
+    o = coffs ? coffs[i] : i * stride;
+    l = clens ? clens[i] : ulen;
+  };
+  uint64_t qb = ~0ull, qo = 0;  // prefetched entry (block qb)
+  uint32_t ql = 0;
+#endif
+  auto start_from = [&](uint64_t i) {
+    if constexpr (kUniform) {  // loop-free: keeps hipcc's vmcnt counting exact
+      pvalid = i < b1;
+      if (pvalid) {
+        pb = i;
+        pptr = base + i * stride;
+        prows = ulen >> 10;
+        prow = 0;
+      }
+      return;
+    }
+    for (; i < b1; i += step) {
+      uint64_t o;
+      uint32_t l;
+#if HC_META_WINDOW
+      meta(i, o, l);
+#else
+      if (i == qb) {  // the next block's entry, fetched one block ahead
+        o = qo;
+        l = ql;
+      } else {
+        meta(i, o, l);
+      }
+#endif
+      if (conform(o, l)) {
+        pb = i;
+        pptr = base + o;
+        prows = l >> 10;
+        prow = 0;
+        pvalid = true;
+#if !HC_META_WINDOW
+        qb = i + step;
+        if (qb < b1) meta(qb, qo, ql);
+#endif
+        return;
+      }
+    }
+    pvalid = false;
+  };
+
+  // Each ring slot carries the wave-uniform tag of the row it holds, so the
+  // consumer never touches block metadata.
   struct Tag {
     uint64_t blk;
     const uint8_t *ptr;
-    uint32_t row;
+    uint32_t row, rows;
     bool valid;
   };
-  auto load_next = [&](Tag &t) -> uint4 {
-    const uint4 v = load_row(pptr + (size_t)prow * kRowBytes, lane);
+  // The load is unconditional (past the wave's last row it re-reads that row,
+  // tagged invalid) so hipcc's wait counting stays exact: vmcnt(kRing-1).
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  uint8_t *const wring = ring_lds + (Cfg::kStage ? wave * (uint32_t)(kRing * kRowBytes) : 0u);
+  auto load_next = [&](Tag &t, int slot) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if constexpr (Cfg::kStage) {
+      dma_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, wring + slot * kRowBytes, lane);
+    } else {
+      v = load_row<Cfg::kPolicy>(pptr + (size_t)prow * kRowBytes, lane);
+    }
     t.valid = pvalid;
     t.blk = pb;
     t.ptr = pptr;
     t.row = prow;
-    if (pvalid && ++prow == rows) {
-      if (pb + step < nblocks) {
-        pb += step;
-        pptr = base + pb * stride;
-        prow = 0;
-      } else {  // park on the last row
-        pvalid = false;
-        prow = rows - 1;
+    t.rows = prows;
+    if (pvalid && ++prow == prows) {
+      const uint64_t lb = pb;
+      const uint8_t *lp = pptr;
+      const uint32_t lr = prows;
+      start_from(pb + step);
+      if (!pvalid) {  // park on the last row
+        pb = lb;
+        pptr = lp;
+        prows = lr;
+        prow = lr - 1;
       }
     }
     return v;
   };
-  uint4 ring[kFastRing];
-  Tag tag[kFastRing];
-#pragma unroll
-  for (int u = 0; u < kFastRing; u++) ring[u] = load_next(tag[u]);
 
-  // ---- consumer
+  start_from(b0);
+  if (!pvalid) return;
+  uint4 ring[kRing];
+  Tag tag[kRing];
+#pragma unroll
+  for (int u = 0; u < kRing; u++) ring[u] = load_next(tag[u], u);
+
+  // ---- consumer --------------------------------------------------------------
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
   bool reported = false;  // wave-uniform: this wave already lowered first_bad
   for (;;) {
 #pragma unroll
-    for (int u = 0; u < kFastRing; u++) {
-      // consume slot u, then refill it (same registers: no copies)
+    for (int u = 0; u < kRing; u++) {
+      // consume slot u, then refill it (same registers: no copies, kRing-1
+      // rows stay in flight while this one is hashed)
       const Tag t = tag[u];
-      uint4 v = ring[u];
+      uint4 v;
+      if constexpr (Cfg::kStage) {
+        // slot u's DMA is the oldest of the kRing in flight; the slot read is
+        // inline asm (invisible to hipcc's waitcnt pass, which would wait
+        // vmcnt(0) for the DMA before a visible LDS read); the slot is
+        // refilled as soon as it is in VGPRs, before the row is hashed
+        __builtin_amdgcn_s_waitcnt((kRing - 1) | (7 << 4) | (15 << 8));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 r;
+        const uint32_t la =
+            (uint32_t)(uintptr_t)(lds_void_t *)(wring + u * kRowBytes) + lane * 16u;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(la) : "memory");
+        v = make_uint4(r.x, r.y, r.z, r.w);
+        load_next(tag[u], u);
+      } else {
+        v = ring[u];
+      }
       if (t.row == 0) {
         if (lane == 0) {
           stored = v.x;
@@ -267,10 +469,15 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
         c2 = row_step(c2, v.z);
         c3 = row_step(c3, v.w);
       }
-      ring[u] = load_next(tag[u]);
-      if (t.row + 1 == rows) {
-        const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
-        const uint32_t crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+      if constexpr (!Cfg::kStage) ring[u] = load_next(tag[u], u);
+      if (t.row + 1 == t.rows) {
+        uint32_t crc;
+        if constexpr (Cfg::kNull) {
+          crc = wave_xor(c0 ^ c1 ^ c2 ^ c3);
+        } else {
+          const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
+          crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        }
         if (lane == 0) {
           const uint64_t cb = t.blk;
           if (crc_out) crc_out[cb] = crc;
@@ -288,7 +495,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
         // block, further first_bad atomics cannot lower the minimum (and on a
         // batch of all-bad blocks would serialise every wave on one address)
         if (first_bad && uni(stored) != crc) reported = true;
-        if (!tag[(u + 1) % kFastRing].valid) return;  // the wave's last block is done
+        if (!tag[(u + 1) % kRing].valid) {  // the wave's last block is done
+          // no LDS-DMA may land after the workgroup's LDS is released
+          if constexpr (Cfg::kStage) __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+          return;
+        }
       }
     }
   }
@@ -316,11 +527,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
 //   * A block that is not 16-B aligned or whose length is not a positive
 //     multiple of 4096 costs one group of dummy rows (re-reads of the current
 //     group, never stored) and is left to k_crc_any (fast_mask 4095).
-//   * kXcd: workgroup g runs on XCD g % 8; the chunk slots are renumbered so
-//     that each XCD's workgroups own neighbouring chunks (grp_xcd decides).
-// The variants measured against this one (static deal, batched refills,
-// nibble finalise tables, timing-only build) are in tools/ab_hc_kernels.hip.
-template <bool kArrays, bool kXcd = false>
+// kNib (A/B only): the 4-byte shift of the per-block finalise from nibble
+// tables with 32 replicas (8 conflict-free lookups) instead of byte tables with
+// 4 replicas (4 lookups, 8 lanes of a half-wave on 8 banks); same 16 KiB.
+template <bool kArrays, bool kDyn = true, bool kNull = false, bool kPin = false, bool kBatch = false,
+          bool kXcd = false, bool kNib = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ lens, uint64_t stride,
                                                          uint32_t ulen, uint32_t flags, uint64_t nblocks,
@@ -334,7 +545,24 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    uint32_t v;
+    if constexpr (kNib) {  // nibble k, value n at kLdsMainBytes + k*2048 + n*128 + 4*replica
+      const uint32_t k = q >> 7, n = (q >> 3) & 15u;
+      v = s4[(k >> 1) * 256 + (n << (4 * (k & 1)))];
+    } else {
+      v = s4[q];
+    }
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) = make_uint4(v, v, v, v);
+  }
   if (tid == 0) s_next = 3 * kFastWaves;  // indices 0 .. 3W-1 are dealt statically below
   uint32_t col[32];
 #pragma unroll
@@ -346,13 +574,21 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
   const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (kNull) return c ^ w;
     const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
     const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
     const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
     const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
     return xor3(xor3(t0, t1, t2), t3, w);
   };
+  const uint32_t N4base = kLdsMainBytes + ((lane & 31u) << 2);
   auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    if constexpr (kNib) {
+      uint32_t t[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) t[k] = lds_u32(lds, N4base + k * 2048u + (((x >> (4 * k)) & 15u) << 7));
+      return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], w));
+    }
     const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
     const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
     const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
@@ -362,7 +598,8 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
 
   const uint32_t wave = uni(tid >> 6);
   const uint64_t G = gridDim.x;
-  // kXcd: each XCD's workgroups own neighbouring chunk slots (G a multiple of 8)
+  // kXcd (A/B only): workgroup g runs on XCD g % 8; renumber so that each
+  // XCD's workgroups own neighbouring chunk slots (G a multiple of 8)
   const uint64_t wg = kXcd && (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   // k-th block of this workgroup's sequence, increasing in k: the first one
@@ -414,16 +651,19 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   Blk cur = meta_sync(i0);
   Blk n1 = meta_sync(blk_of(k1));
   uint64_t i2 = blk_of(k2);
-  uint32_t k3v = 0;  // VGPR: the LDS hand-out result, read one block end later
+  uint32_t k3v = 0;                        // VGPR: the LDS hand-out result, read one block end later
+  uint32_t kstat = 3 * kFastWaves + wave;  // static deal (kDyn = false: timing comparison only)
   meta_issue(i2);
   // the group the row registers hold; a skipped first block reads 4 KiB of the
   // constant image instead (always mapped, never consumed)
   const uint8_t *gp = cur.skip ? reinterpret_cast<const uint8_t *>(tables) : cur.p;
   static_assert(sizeof(DeviceTables) >= 4096, "dummy group reads 4 KiB of the table image");
   uint32_t g = 0, gc = cur.skip ? 1u : cur.groups;
-  uint4 q0 = load_row(gp, lane), q1 = load_row(gp + 1024, lane), q2 = load_row(gp + 2048, lane),
-        q3 = load_row(gp + 3072, lane);
-  if (lane == 0) k3v = atomicAdd(&s_next, 1u);
+  uint4 q0 = load_row<1>(gp, lane), q1 = load_row<1>(gp + 1024, lane), q2 = load_row<1>(gp + 2048, lane),
+        q3 = load_row<1>(gp + 3072, lane);
+  if constexpr (kDyn) {
+    if (lane == 0) k3v = atomicAdd(&s_next, 1u);
+  }
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
   uint64_t reported = ~0ull;  // wave-uniform: lowest block this wave has put into first_bad
   for (;;) {
@@ -457,42 +697,70 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
       } else {
         n1 = make_blk(i2, i2 * stride, ulen);
       }
-      const uint32_t k3 = uni(k3v);
-      if (lane == 0) k3v = atomicAdd(&s_next, 1u);
+      uint32_t k3;
+      if constexpr (kDyn) {
+        k3 = uni(k3v);
+        if (lane == 0) k3v = atomicAdd(&s_next, 1u);
+      } else {
+        k3 = kstat;
+        kstat += kFastWaves;
+      }
       i2 = blk_of(k3);
     }
-    // Each refill right after its row's hash (the sched_barriers keep hipcc
-    // from pairing them two rows late: +0.3-0.8 %); issuing a group's four
-    // refills together after its last row, as a plain read stream does, was
-    // 0.3-1 % slower (profiles/r2/ab_refill/).
-    meta_issue(i2);
-    q0 = load_row(np, lane);
-    __builtin_amdgcn_sched_barrier(0);
+    // kPin: keep each refill right after its row's hash (hipcc otherwise pairs
+    // them, two rows late)
+    auto pin = [&] {
+      if constexpr (kPin) __builtin_amdgcn_sched_barrier(0);
+    };
+    // kBatch (A/B only): the group's 4 refills issued together after its last
+    // row, as a plain read stream does, instead of each right after its row
+    if constexpr (!kBatch) {
+      meta_issue(i2);
+      q0 = load_row<1>(np, lane);
+      pin();
+    }
     c0 = row_step(c0, q1.x);
     c1 = row_step(c1, q1.y);
     c2 = row_step(c2, q1.z);
     c3 = row_step(c3, q1.w);
-    __builtin_amdgcn_sched_barrier(0);
-    q1 = load_row(np + 1024, lane);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!kBatch) {
+      pin();
+      q1 = load_row<1>(np + 1024, lane);
+      pin();
+    }
     c0 = row_step(c0, q2.x);
     c1 = row_step(c1, q2.y);
     c2 = row_step(c2, q2.z);
     c3 = row_step(c3, q2.w);
-    __builtin_amdgcn_sched_barrier(0);
-    q2 = load_row(np + 2048, lane);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!kBatch) {
+      pin();
+      q2 = load_row<1>(np + 2048, lane);
+      pin();
+    }
     c0 = row_step(c0, q3.x);
     c1 = row_step(c1, q3.y);
     c2 = row_step(c2, q3.z);
     c3 = row_step(c3, q3.w);
-    __builtin_amdgcn_sched_barrier(0);
-    q3 = load_row(np + 3072, lane);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!kBatch) {
+      pin();
+      q3 = load_row<1>(np + 3072, lane);
+      pin();
+    } else {
+      meta_issue(i2);
+      q0 = load_row<1>(np, lane);
+      q1 = load_row<1>(np + 1024, lane);
+      q2 = load_row<1>(np + 2048, lane);
+      q3 = load_row<1>(np + 3072, lane);
+    }
     if (last) {  // block cur is complete
       if (!cur.skip) {
-        const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
-        const uint32_t crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        uint32_t crc;
+        if constexpr (kNull) {
+          crc = wave_xor(c0 ^ c1 ^ c2 ^ c3);
+        } else {
+          const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
+          crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+        }
         const uint64_t b = cur.i;
         if (crc_out) lane0_store_u32(crc_out + b, crc);
         if (flags & kFlagStamp) lane0_store_u32(const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(cur.p)), crc);
@@ -571,19 +839,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_range(const void *p, uint3
 
 // Pipelined per wave over its messages (blocks in block mode): the edge rows
 // of message i+1 (and its stored word) are loaded while message i is
-// finalised, and message i's first body batch (issued only when the message
-// has body rows) together with its edge rows, during the previous message's
-// finalise (profiles/r1/s5/kmsg_variants2.txt: best or within 1 % of the best
-// on config 5b, equal-size messages and 4092-B off/len blocks).  Body rows go
-// kAnyBatch at a time.  Windows of 64 messages are handed out like k_crc_grp's
-// blocks: workgroup g owns the chunks of 2^lg_chunk consecutive windows
-// c*G + g, its waves take windows one at a time from an LDS counter (+1.5-4.5 %
-// over one static run per wave, profiles/r2/any/).  kSmallLanes (whole-message
-// batches): records of <= 1020 bytes are hashed one per lane (below).  The
-// measured alternatives (static runs, other batch sizes, issue orders, the
-// timing-only build) are in tools/ab_hc_kernels.hip.
-constexpr int kAnyBatch = 4;
-template <bool kSmallLanes>
+// finalised, and message i's first body batch while its edge rows are hashed.
+// kVar (A/B, tools/kmsg): bit 0 = issue the first body batch only when the
+// message has body rows (else out-of-range loads); bit 1 = issue it together
+// with the message's edge rows (during the previous message's finalise).
+// Production: 3 (profiles/r1/s5/kmsg_variants2.txt: best or within 1 % of the
+// best on config 5b, equal-size messages and 4092-B off/len blocks).
+// kDyn: windows of 64 messages are handed out like k_crc_grp's blocks
+// (workgroup g owns the chunks of 2^lg_chunk consecutive windows c*G + g, its
+// waves take windows one at a time from an LDS counter) instead of one static
+// contiguous run per wave.
+template <int kBatch, int kVar = 0, bool kDyn = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
@@ -595,7 +861,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = uni(tid >> 6);
-  const uint64_t b1 = nblocks;
+  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
+  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
+  const uint64_t b0 = kDyn ? 0 : uni64(nblocks * gw / W), b1 = kDyn ? nblocks : uni64(nblocks * (gw + 1) / W);
   const uint64_t G = gridDim.x, wg = blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   // first message of the workgroup's k-th window (increasing in k)
@@ -610,7 +878,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   if (fast_mask) {
     bool any = false;
     for (uint32_t kk = wave;; kk += kFastWaves) {
-      const uint64_t g0 = win_of(kk);
+      const uint64_t g0 = kDyn ? win_of(kk) : b0 + (uint64_t)(kk - wave) / kFastWaves * 64;
       if (g0 >= b1 || any) break;
       const uint64_t j = g0 + lane;
       const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
@@ -620,7 +888,19 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     }
     if (!__syncthreads_or(any)) return;
   }
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
+  }
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
@@ -631,7 +911,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
   const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
   const bool msg = (flags & kFlagMessages) != 0;
+  // kVar bit 3 (A/B, timing only): the LDS arithmetic replaced by an XOR fold
+  constexpr bool kNullMath = (kVar & 8) != 0;
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (kNullMath) return c ^ w;
     const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
     const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
     const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
@@ -639,6 +922,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     return xor3(xor3(t0, t1, t2), t3, w);
   };
   auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
+    if constexpr (kNullMath) return x ^ w;
     const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
     const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
     const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
@@ -646,7 +930,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     return xor3(xor3(t0, t1, t2), t3, w);
   };
 
-  // ---- small records, one per lane (kSmallLanes, whole-message mode) --------
+  // ---- small records, one per lane (kVar bit 4, whole-message mode) ---------
   // A window's records of <= 1020 bytes (one row) are hashed lane-parallel:
   // lane k takes record g+k (its metadata is already in this lane) and runs
   // the Horner chain c <- shift4(c) ^ V_i over the 4-byte words of the
@@ -739,11 +1023,13 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   // The metadata of 64 messages g .. g+63 sits one per lane (one coalesced
   // load); `todo` ballots the ones this kernel must do (only_nonfast: those
   // the streaming kernel skipped).  Entries are read with v_readlane.
-  uint64_t g = win_of(wave), todo = 0;
+  uint64_t g = kDyn ? win_of(wave) : b0, todo = 0;
   bool loaded = false;
   uint32_t wo_lo = 0, wo_hi = 0, wl = 0;
-  uint32_t knv = 0;  // LDS hand-out result for the next window, read one window later
-  if (lane == 0) knv = atomicAdd(&s_next, 1u);
+  uint32_t knv = 0;  // LDS hand-out result for the next window (kDyn), read one window later
+  if constexpr (kDyn) {
+    if (lane == 0) knv = atomicAdd(&s_next, 1u);
+  }
   struct Msg {
     uint64_t blk;
     const uint8_t *p;  // block / message start
@@ -766,8 +1052,12 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
         return;
       }
       if (loaded) {
-        g = win_of(uni(knv));
-        if (lane == 0) knv = atomicAdd(&s_next, 1u);
+        if constexpr (kDyn) {
+          g = win_of(uni(knv));
+          if (lane == 0) knv = atomicAdd(&s_next, 1u);
+        } else {
+          g += 64;
+        }
       }
       loaded = true;
       if (g >= b1) {
@@ -791,7 +1081,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       // blocks whose length is a positive multiple of fast_mask + 1
       const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & fast_mask) == 0 && lj != 0;
       todo = __ballot(j < b1 && !(fast_mask && fast));
-      if constexpr (kSmallLanes) {
+      if constexpr ((kVar & 16) != 0) {
         if (msg) {
           const uint64_t sm = __ballot(j < b1 && !(fast_mask && fast) && lj <= kSmallMax);
           if (sm) {
@@ -853,16 +1143,16 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   // load per lane through the range [row 2, row `rows`); rows past the end are
   // out of range (zeros, no memory access).
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  auto issue_body = [&](const __amdgpu_buffer_rsrc_t rb_, uint32_t r0, u32x4 (&v)[kAnyBatch]) {
+  auto issue_body = [&](const __amdgpu_buffer_rsrc_t rb_, uint32_t r0, u32x4 (&v)[kBatch]) {
 #pragma unroll
-    for (int b = 0; b < kAnyBatch; b++) {
+    for (int b = 0; b < kBatch; b++) {
       const uint4 t = buf_load16(rb_, (r0 + b - 2) * kRowBytes + 16u * lane);
       v[b] = u32x4{t.x, t.y, t.z, t.w};
     }
   };
-  auto hash_body = [&](const Geo &e, uint32_t r0, const u32x4 (&v)[kAnyBatch], uint32_t (&c)[4]) {
+  auto hash_body = [&](const Geo &e, uint32_t r0, const u32x4 (&v)[kBatch], uint32_t (&c)[4]) {
 #pragma unroll
-    for (int b = 0; b < kAnyBatch; b++)
+    for (int b = 0; b < kBatch; b++)
       if (r0 + b < e.rows) {
         c[0] = row_step(c[0], v[b].x);
         c[1] = row_step(c[1], v[b].y);
@@ -881,15 +1171,17 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     const uintptr_t A0 = e.Abase + e.q * 4 + e.rb;
     return buf_range((const void *)(A0 + 2 * kRowBytes), e.rows > 2 ? (e.rows - 2) * kRowBytes : 0u);
   };
-  u32x4 VA[kAnyBatch];
+  u32x4 VA[kBatch];
   auto issue_first = [&](const Geo &e) {
-    if (e.rows > 2) issue_body(body_range(e), 2, VA);
+    if (!(kVar & 1) || e.rows > 2) issue_body(body_range(e), 2, VA);
   };
   issue_edge(cur, ge, ch, sw);
-  issue_first(ge);
+  if constexpr ((kVar & 2) != 0) issue_first(ge);
   bool reported = false;  // wave-uniform: this wave already lowered first_bad (see k_crc_fast)
   for (;;) {
     const __amdgpu_buffer_rsrc_t rbody = body_range(ge);
+    // the first body batch goes out before the edge rows are hashed
+    if constexpr ((kVar & 2) == 0) issue_first(ge);
     // edge rows
     uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -920,6 +1212,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     // below and drains the queue there (vmcnt(0))
     asm volatile("" ::"v"(ch[0].x), "v"(ch[1].x), "v"(ch[2].x), "v"(ch[3].x), "v"(sw));
     const uint32_t dsw = uni(sw);
+    // body rows, the next batch in flight while one is hashed
+    // (no early exit: a second half past the end loads out of range and hashes
+    // nothing, so every path through the loop has the same VMEM sequence)
     // body rows, one batch at a time.  tools/kmsg measured this against a
     // double-buffered loop (the next batch in flight while one is hashed):
     // single batches were 4-12 % faster -- more bytes in flight per wave than
@@ -929,7 +1224,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     // (a double-buffered body -- the next batch in flight while one is hashed,
     // the batch past the end out of range, no branch -- was 7-10 % slower:
     // profiles/r2/any_double/)
-    for (uint32_t r0 = 2; r0 < ge.rows; r0 += kAnyBatch) {
+    for (uint32_t r0 = 2; r0 < ge.rows; r0 += kBatch) {
       if (r0 > 2) issue_body(rbody, r0, VA);
       hash_body(ge, r0, VA, c);
     }
@@ -939,10 +1234,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     next(cur);
     ge = geo(cur);
     issue_edge(cur, ge, ch, sw);
-    issue_first(ge);
+    if constexpr ((kVar & 2) != 0) issue_first(ge);
 
     const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-    const uint32_t crcv = dshort ? 0u : wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    const uint32_t crcv = dshort ? 0u : wave_xor(kNullMath ? dd : matvec32(col, dd)) ^ 0xFFFFFFFFu;
     const bool bad = !msg && first_bad && (dshort || dsw != crcv);  // wave-uniform
     if (crc_out) lane0_store_u32(crc_out + done.blk, crcv);
     if (!msg && !dshort && (flags & kFlagStamp))  // PutUint32LE(block[0:4], crc)
@@ -971,10 +1266,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 // of 2^lg_chunk consecutive blocks c*G + g and its waves take them one at a
 // time from an LDS counter (tools/kcopy2: a persistent read+write stream went
 // from 5.0-5.5 TB/s with static deals to 5.9 TB/s this way).
-// Two interior blocks per wave: one prefetched while one is framed (a third
-// in flight, other chunk sizes, XCD-contiguous chunk slots, other store orders
-// and the timing-only build measured the same or slower: DESIGN.md 4.4a,
-// tools/kframe with tools/ab_hc_kernels.hip).
+// kDepth: interior blocks in flight per wave (2: one prefetched while one is
+// framed; 3: two).  kNull: timing-only build, the CRC replaced by an XOR fold
+// (tools/kframe measures the memory pattern alone).  kXcd (A/B only): XCD-
+// contiguous chunk slots as in k_crc_grp.
 // Edge blocks of AddCRCsToData framing (the first, whose row 0 would start 4
 // bytes before src, and the last, whose payload may end mid-row): aligned
 // loads predicated on the payload range + funnel shift + byte masks -- never
@@ -997,8 +1292,8 @@ __device__ __forceinline__ void frame_edge_rows(uint64_t b, const uint8_t *__res
   for (int r = 0; r < 4; r++) {
     const uintptr_t X0 = Ab + (uintptr_t)r * kRowBytes + 16u * lane, X1 = X0 + 16;
     ch0[r] = ch1[r] = make_uint4(0, 0, 0, 0);
-    if (X0 + 16 > P && X0 < P + len) ch0[r] = load_row(reinterpret_cast<const uint8_t *>(X0), 0);
-    if (X1 + 16 > P && X1 < P + len) ch1[r] = load_row(reinterpret_cast<const uint8_t *>(X1), 0);
+    if (X0 + 16 > P && X0 < P + len) ch0[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X0), 0);
+    if (X1 + 16 > P && X1 < P + len) ch1[r] = load_row<1>(reinterpret_cast<const uint8_t *>(X1), 0);
   }
   keep = make_uint4(0, 0, 0, 0);
   uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK;
@@ -1027,7 +1322,10 @@ __device__ __forceinline__ void frame_edge_rows(uint64_t b, const uint8_t *__res
   }
 }
 
-// Each row is stored before it is hashed (the other orders: +-0.6 %).
+// kSt (A/B only, tools/kframe): 0 = each row stored before it is hashed
+// (production); 2 = the block's four rows hashed, then its four stores;
+// 4 = the four stores, then the hashing.
+template <int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 0>
 __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
                                                          uint8_t *__restrict__ dst, uint64_t nblk, uint32_t lg_chunk,
                                                          uint32_t *__restrict__ crc_out,
@@ -1035,8 +1333,20 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) s_next = 2 * kFastWaves;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+  if (tid == 0) s_next = kDepth * kFastWaves;
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
+  }
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
@@ -1094,7 +1404,8 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
   // masks -- and the next block's 4 rows are in flight while this one is hashed.
   // Interior index i (block i + 1) of the workgroup's k-th hand-out:
   const uint64_t ni = nblk > 2 ? nblk - 2 : 0;
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint64_t G = gridDim.x;
+  const uint64_t wg = kXcd && (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
   uint64_t c = blk_of(wave);
@@ -1112,13 +1423,19 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
     const uint64_t b = i + 1;
     uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
     uint32_t cc[4];
+    u32x4 sv[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       u32x4 v = cur[r];
       // every lane stores (no divergent branch between the loads and their
       // use); lane 0 writes zeros to bytes 0..3 and the CRC over them below
       if (r == 0) v.x = lane == 0 ? 0u : v.x;
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+      sv[r] = v;
+      if constexpr (kSt == 0) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+    }
+    if constexpr (kSt == 4) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -1126,10 +1443,19 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
       if (r == 0) v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : row_step(cc[k], w[k]);
+      for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : (kNull ? cc[k] ^ w[k] : row_step(cc[k], w[k]));
     }
-    const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
-    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    if constexpr (kSt == 2) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+    }
+    uint32_t crcv;
+    if constexpr (kNull) {
+      crcv = wave_xor(cc[0] ^ cc[1] ^ cc[2] ^ cc[3]);
+    } else {
+      const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
+      crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+    }
     // binary.LittleEndian.PutUint32(block[:4], crc): lane 0's ob is the block start
     lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);
     if (crc_out) lane0_store_u32(crc_out + b, crcv);
@@ -1144,20 +1470,45 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
   // holds.  The first block is peeled so that the loop header is entered with
   // the same VMEM sequence from both edges ([next rows loaded][4 row stores]);
   // a mismatch there makes the waitcnt pass wait for the stores as well.
-  u32x4 A[4], B[4];
-  load4(c, A);
-  load4(n1 < ni ? n1 : c, B);
-  frame(c, A);
-  while (n1 < ni) {
-    c = n1;
-    n1 = nextb();
-    load4(n1 < ni ? n1 : c, A);
-    frame(c, B);
-    if (n1 >= ni) break;
-    c = n1;
-    n1 = nextb();
+  if constexpr (kDepth == 2) {
+    u32x4 A[4], B[4];
+    load4(c, A);
     load4(n1 < ni ? n1 : c, B);
     frame(c, A);
+    while (n1 < ni) {
+      c = n1;
+      n1 = nextb();
+      load4(n1 < ni ? n1 : c, A);
+      frame(c, B);
+      if (n1 >= ni) break;
+      c = n1;
+      n1 = nextb();
+      load4(n1 < ni ? n1 : c, B);
+      frame(c, A);
+    }
+  } else {
+    // loop invariant: B holds n1, C holds n2, A is free
+    uint64_t n2 = blk_of(2 * kFastWaves + wave);
+    u32x4 A[4], B[4], C[4];
+    load4(c, A);
+    load4(n1 < ni ? n1 : c, B);
+    load4(n2 < ni ? n2 : c, C);
+    frame(c, A);
+    while (n1 < ni) {
+      const uint64_t n3 = nextb();
+      load4(n3 < ni ? n3 : n1, A);
+      frame(n1, B);
+      if (n2 >= ni) break;
+      const uint64_t n4 = nextb();
+      load4(n4 < ni ? n4 : n2, B);
+      frame(n2, C);
+      if (n3 >= ni) break;
+      const uint64_t n5 = nextb();
+      load4(n5 < ni ? n5 : n3, C);
+      frame(n3, A);
+      n1 = n4;
+      n2 = n5;
+    }
   }
 }
 
@@ -1168,14 +1519,19 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 // back (block b's block[4:B] at out + b*(B-4)) -- the inverse of k_frame, one
 // read of the blocks and one write of the payload.  B = 4096 << lg_groups.
 // A wave walks its blocks in 4 KiB groups (4 rows of 1 KiB), the next group's
-// rows in flight while the current one is hashed and stored.  Payload stores are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
+// rows in flight while the current one is hashed and stored (the four stores
+// after the group's hashing, kSt).  Payload stores are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
 // block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
 // overlapping lane 1's store with identical bytes.
-// Store order: the group's four rows are hashed, then its four payload stores
-// (global nt) are issued together -- +3.9 % over storing each row before
-// hashing it, at the speed of the timing-only build (profiles/r2/framing_store/;
-// the other orders and cache policies are in tools/ab_hc_kernels.hip).
-template <uint32_t lg_groups>
+// kSt: store order.  Production 2: the group's four rows are hashed, then its
+// four payload stores are issued together -- +3.9 % over storing each row
+// before hashing it (round-2 production), on two boxes, at the speed of the
+// timing-only build (profiles/r2/framing_store/).  A/B only: 0 = each row
+// stored before it is hashed; 1 = each row stored after it is hashed; 3 = 0
+// with write-back (not nt) stores; 4 = rows 0-2 hashed, the four stores, row 3.
+// kPol (A/B only): payload stores as buffer stores with cache-policy bits
+// kPol - 1 (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16); 0 = global nt stores.
+template <uint32_t lg_groups, int kDepth = 2, bool kNull = false, bool kXcd = false, int kSt = 2, int kPol = 0>
 __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                            uint32_t lg_chunk, uint8_t *__restrict__ out,
                                                            uint32_t *__restrict__ crc_out,
@@ -1186,7 +1542,19 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
   __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   if (tid == 0) s_next = 2 * kFastWaves;  // two hand-outs per wave before the counter
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) =
+        make_uint4(v, v, v, v);
+  }
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
@@ -1217,7 +1585,8 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
   // blocks handed out as in k_crc_grp (chunks of 2^lg_chunk consecutive blocks
   // per workgroup, one block at a time per wave from an LDS counter); a wave
   // walks a block's 4 KiB groups in order
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
+  const uint64_t G = gridDim.x;
+  const uint64_t wg = kXcd && (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
   auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
   const uint64_t bstart = blk_of(wave);
@@ -1235,6 +1604,16 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
     const uint64_t b = p >> lg_groups;
     const uint32_t g = (uint32_t)p & gmask;
     uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
+    uint8_t *const obu = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK - 4;  // wave-uniform
+    const __amdgpu_buffer_rsrc_t orc = __builtin_amdgcn_make_buffer_rsrc(obu, 0, HC_FRAME_BLOCK + 16, 0x00020000);
+    auto st16 = [&](u32x4 v, uint8_t *a) {
+      if constexpr (kPol > 0)
+        __builtin_amdgcn_raw_buffer_store_b128(v, orc, (uint32_t)(a - obu), 0, kPol - 1);
+      else if constexpr (kSt == 3)
+        *reinterpret_cast<u32x4_u *>(a) = v;
+      else
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(a));
+    };
     u32x4 sv[4];
     uint8_t *sa[4];
 #pragma unroll
@@ -1251,15 +1630,29 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
         sv[r] = v;
         sa[r] = ob + r * kRowBytes;
       }
+      if constexpr (kSt == 0 || kSt == 3) st16(sv[r], sa[r]);
+      if constexpr (kSt == 4)
+        if (r == 3)
+#pragma unroll
+          for (int q = 0; q < 4; q++) st16(sv[q], sa[q]);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = (r == 0 && g == 0) ? w[k] : row_step(c[k], w[k]);
+      for (int k = 0; k < 4; k++)
+        c[k] = (r == 0 && g == 0) ? w[k] : (kNull ? c[k] ^ w[k] : row_step(c[k], w[k]));
+      if constexpr (kSt == 1) st16(sv[r], sa[r]);
     }
+    if constexpr (kSt == 2) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
+      for (int r = 0; r < 4; r++) st16(sv[r], sa[r]);
+    }
     if (g == gmask) {
-      const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-      const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      uint32_t crcv;
+      if constexpr (kNull) {
+        crcv = wave_xor(c[0] ^ c[1] ^ c[2] ^ c[3]);
+      } else {
+        const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
+        crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      }
       if (crc_out) lane0_store_u32(crc_out + b, crcv);
       if (first_bad && crcv != stored) {  // wave-uniform
         if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
@@ -1294,22 +1687,51 @@ __global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restr
     return pv ? (pb << lg_groups) + pg : fallback;
   };
   uint64_t p = bstart << lg_groups;
-  u32x4 A[4], Bv[4];
-  load4(p, A);
-  bool qv;
-  uint64_t q = pnext(p, qv);
-  load4(q, Bv);
-  group(p, A);
-  while (qv) {
-    p = q;
-    q = pnext(p, qv);
-    load4(q, A);
-    group(p, Bv);
-    if (!qv) break;
-    p = q;
-    q = pnext(p, qv);
+  if constexpr (kDepth == 2) {
+    u32x4 A[4], Bv[4];
+    load4(p, A);
+    bool qv;
+    uint64_t q = pnext(p, qv);
     load4(q, Bv);
     group(p, A);
+    while (qv) {
+      p = q;
+      q = pnext(p, qv);
+      load4(q, A);
+      group(p, Bv);
+      if (!qv) break;
+      p = q;
+      q = pnext(p, qv);
+      load4(q, Bv);
+      group(p, A);
+    }
+  } else {
+    // loop invariant: Bv holds group q1, C holds q2, A is free
+    u32x4 A[4], Bv[4], C[4];
+    load4(p, A);
+    bool v1, v2, v3, v4, v5;
+    uint64_t q1 = pnext(p, v1);
+    load4(q1, Bv);
+    uint64_t q2 = pnext(p, v2);
+    load4(q2, C);
+    group(p, A);
+    while (v1) {
+      const uint64_t q3 = pnext(q1, v3);
+      load4(q3, A);
+      group(q1, Bv);
+      if (!v2) break;
+      const uint64_t q4 = pnext(q2, v4);
+      load4(q4, Bv);
+      group(q2, C);
+      if (!v3) break;
+      const uint64_t q5 = pnext(q3, v5);
+      load4(q5, C);
+      group(q3, A);
+      q1 = q4;
+      v1 = v4;
+      q2 = q5;
+      v2 = v5;
+    }
   }
 }
 
@@ -1429,8 +1851,9 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
   if (__ballot(bad)) lane0_atomic_or(flag, 1u);
 }
 
-// (its timing-only builds -- rows XOR-folded, or no event work at all -- are in
-// tools/ab_hc_kernels.hip)
+// kNull (A/B only): rows XOR-folded instead of CRC'd; kNoEv (A/B only): no event
+// processing at all (the memory pattern alone)
+template <bool kNull = false, bool kNoEv = false>
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
                                                             uint32_t lg_chunk, const uint32_t *__restrict__ flag,
@@ -1441,7 +1864,18 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+  const uint32_t *tg = &tables->tg[0][0];
+  for (uint32_t q = tid; q < kLdsMainBytes / 16; q += kFastThreads) {
+    const uint32_t a = q * 16;
+    const uint32_t k = ((a >> 16) << 1) | ((a >> 7) & 1u);
+    const uint32_t v = tg[k * 256 + ((a >> 8) & 255u)];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + a) = make_uint4(v, v, v, v);
+  }
+  const uint32_t *s4 = &tables->s4[0][0];
+  for (uint32_t q = tid; q < kLdsS4Bytes / 16; q += kFastThreads) {
+    const uint32_t v = s4[q];
+    *reinterpret_cast<uint4 *>(reinterpret_cast<char *>(lds) + kLdsMainBytes + q * 16) = make_uint4(v, v, v, v);
+  }
   if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
   uint32_t col[32];
 #pragma unroll
@@ -1453,6 +1887,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
   const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
+    if constexpr (kNull) return c ^ w;
     const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
     const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
     const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
@@ -1578,7 +2013,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     c1 = row_step(c1, w.y);
     c2 = row_step(c2, w.z);
     c3 = row_step(c3, w.w);
-    const uint64_t evm = __ballot(wpos >= rs && wpos < rs + 1024u);
+    const uint64_t evm = kNoEv ? 0 : __ballot(wpos >= rs && wpos < rs + 1024u);
     uint4 we = w;
     // the folds complete before the refill (else they sink past the event
     // branch's join and the refill needs a fresh register: see pin below)
@@ -1803,30 +2238,46 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
 
 }  // namespace
 
-// uniform batches of 16-B aligned 1 KiB-multiple blocks (k_crc_fast)
-hipError_t launch_fast(const Batch &b, int grid, hipStream_t s) {
-  if (!b.base || b.off || b.len || b.ulen == 0 || (b.ulen & 1023u) != 0 || (b.stride & 15u) != 0 ||
-      (reinterpret_cast<uintptr_t>(b.base) & 15u) != 0)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_crc_fast, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.stride, b.ulen, b.flags, b.nblocks,
-                     b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+hipError_t launch_fast(const Batch &b, bool uniform_fast, int grid, hipStream_t s) {
+  if (!b.base || (uniform_fast && (b.ulen == 0 || (b.ulen & 1023u) != 0))) return hipErrorInvalidValue;
+  using C = DefaultFastCfg;
+  if (uniform_fast)
+    hipLaunchKernelGGL((k_crc_fast<true, C>), dim3(grid), dim3(C::kWaves * 64), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap,
+                       b.first_bad, b.tables);
+  else
+    hipLaunchKernelGGL((k_crc_fast<false, C>), dim3(grid), dim3(C::kWaves * 64), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, b.crc_out, b.bad_bitmap,
+                       b.first_bad, b.tables);
   return hipGetLastError();
 }
 
-// k_crc_any: 64-message windows handed out one at a time (tools/kbench2,
-// profiles/r2/any/: 2M records, config 5b +4.5 %, equal 9815-B records
-// +2.7 %, 4092-B blocks +2 % over static runs per wave).  Whole-message
-// batches hash their records of <= 1020 bytes lane-parallel (1.77x on small
-// records, neutral on config 5b and on large ones, profiles/r2/any_small_lanes/);
-// block mode keeps the leaner build.
+// Production: 64-message windows handed out one at a time (kDyn, chunk = 1
+// window).  tools/kbench2 (profiles/r2/any/): 2M records, config 5b +4.5 %,
+// equal 9815-B records +2.7 %, 4092-B blocks +2 % over static runs per wave;
+// larger chunks lose, and at 200k records chunks of 4+ windows lose 13 %.
 hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s) {
-  if (!b.base) return hipErrorInvalidValue;
+  return launch_general_dyn(b, fast_mask, grid, s, 0);
+}
+
+// static contiguous runs per wave (round 1; kept for A/B)
+hipError_t launch_general_static(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_crc_any<4, 3>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+                     b.ulen, b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_general_dyn(const Batch &b, uint32_t fast_mask, int grid, hipStream_t s, int lg_chunk) {
+  const uint32_t lg = lg_chunk >= 0 ? (uint32_t)lg_chunk : 0u;
+  // whole-message batches hash their records of <= 1020 bytes lane-parallel
+  // (kVar bit 4: 1.77x on small records, neutral on config 5b and on large
+  // ones, profiles/r2/any_small_lanes/); block mode keeps the leaner build
   if (b.flags & kFlagMessages)
-    hipLaunchKernelGGL(k_crc_any<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+    hipLaunchKernelGGL((k_crc_any<4, 19, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
   else
-    hipLaunchKernelGGL(k_crc_any<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+    hipLaunchKernelGGL((k_crc_any<4, 3, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
+                       b.ulen, b.flags, b.nblocks, fast_mask, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
   return hipGetLastError();
 }
 
@@ -1864,14 +2315,17 @@ hipError_t launch_grp(const Batch &b, int grid, hipStream_t s) {
     return hipErrorInvalidValue;
   const uint32_t lg = grp_lg_chunk(b.nblocks, grid, (b.off || b.len) ? 0u : b.ulen);
   if (b.off || b.len)
-    hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                       b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+    hipLaunchKernelGGL((k_crc_grp<true, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables, b.seg_flag);
   else if (grp_xcd(b.ulen, grid, b.nblocks))  // each XCD's workgroups own neighbouring chunk slots
-    hipLaunchKernelGGL((k_crc_grp<false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                       b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+    hipLaunchKernelGGL((k_crc_grp<false, true, false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s,
+                       b.base, b.off, b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap,
+                       b.first_bad, b.tables);
   else
-    hipLaunchKernelGGL((k_crc_grp<false>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                       b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);
+    hipLaunchKernelGGL((k_crc_grp<false, true, false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off,
+                       b.len, b.stride, b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad,
+                       b.tables);
   return hipGetLastError();
 }
 
@@ -1880,7 +2334,7 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
   const uint64_t ni = nblk > 2 ? nblk - 2 : 1;
-  hipLaunchKernelGGL(k_frame, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, grp_lg_chunk(ni, grid, 4096), crc_out,
+  hipLaunchKernelGGL((k_frame<2>), dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, grp_lg_chunk(ni, grid, 4096), crc_out,
                      tables);
   return hipGetLastError();
 }
@@ -1928,7 +2382,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint64_t pg = (n + 256) / 256;
   hipLaunchKernelGGL(k_seg_plan, dim3((unsigned)(pg < 16384 ? pg : 16384)), dim3(256), 0, s, b.base, b.off, b.len, n,
                      max_units, flag, first_ev);
-  hipLaunchKernelGGL(k_seg_stream, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
+  hipLaunchKernelGGL((k_seg_stream<false, false>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
                      flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_scan_units, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, unit_incl,
                      blk_tot, st);

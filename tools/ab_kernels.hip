@@ -1,6 +1,6 @@
 // ab_kernels.hip -- A/B kernels measured in round 2 and kept OUT of the product
 // (tools/kbench2.hip and tools/kframe.hip include this file after
-// hunddb_amd/csrc/hc_kernels.hip, in the same namespace, so they reuse its
+// ab_hc_kernels.hip (the round-2 product source), in the same namespace, so they reuse its
 // helpers).  Results: DESIGN.md section 4.1a (k_crc_piece, not kept: +0-0.5 %)
 // and section 4.4a (k_frame_np, not kept: 8-37 % slower).
 namespace hc {

@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#include "../hunddb_amd/csrc/hc_kernels.hip"
+#include "ab_hc_kernels.hip"
 #include "r1_kernels.hip"
 
 #define CK(x)                                                                          \
