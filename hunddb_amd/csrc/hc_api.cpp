@@ -1225,13 +1225,12 @@ int hc_dev_read_blocks(int device, const void *blocks, uint64_t nblocks, uint32_
   if (st != HC_OK) return st;
   DeviceGuard g(device);
   DeviceState &d = g_dev[device];
-  const int grid =
-      (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.cus, (nblocks + kFastWaves - 1) / kFastWaves));
-  hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4), (uint32_t)grid, kFastThreads,
-                      kFastLdsBytes};
+  const uint64_t per_wg = 4ull * std::max<uint32_t>(1u, kUnframeWaveGroups >> lg);
+  hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4),
+                      (uint32_t)std::min<uint64_t>((nblocks + per_wg - 1) / per_wg, 0xFFFFFFFFull), 256, 0};
   t_last = info;
   return launch_unframe(static_cast<const uint8_t *>(blocks), nblocks, lg, static_cast<uint8_t *>(payload_out),
-                        crc_out, bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), d.dtab, grid,
+                        crc_out, bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), d.dtab,
                         static_cast<hipStream_t>(stream)) == hipSuccess
              ? HC_OK
              : HC_E_HIP;

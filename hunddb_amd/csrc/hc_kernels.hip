@@ -1162,154 +1162,141 @@ __global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restric
 }
 
 // ---------------------------------------------------------------------------
+// The row step without LDS (k_unframe): a 32x32 GF(2) mat-vec M.c is the XOR
+// of five 64-entry tables T_j[6-bit chunk j of c] (bits 0..29) and the two
+// columns of bits 30, 31.  Each table sits in ONE VGPR -- lane v holds T_j[v]
+// -- and is read by ds_bpermute_b32, the cross-lane gather: no LDS allocation,
+// no bank conflicts, no table fill, so a kernel built on it can run as
+// short-lived 4-wave workgroups.  The columns come from the
+// constant image: column i of shift(., 1024) is tg[i/8][1 << i%8], of
+// shift(., 4) s4[i/8][1 << i%8].  ds_bpermute reads only address bits 7..2,
+// so the chunk addresses need no mask.
+struct XTab {
+  uint32_t t[5];
+  uint32_t c30, c31;  // wave-uniform
+};
+__device__ __forceinline__ XTab make_xtab(const uint32_t (*tab)[256], uint32_t lane) {
+  XTab r;
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    uint32_t e = 0;
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      const int i = 6 * j + b;
+      const uint32_t m = 0u - ((lane >> b) & 1u);
+      e = __builtin_amdgcn_bitop3_b32(m, tab[i >> 3][1u << (i & 7)], e, 0x6A);  // (m & col) ^ e
+    }
+    r.t[j] = e;
+  }
+  r.c30 = tab[3][1u << 6];
+  r.c31 = tab[3][1u << 7];
+  return r;
+}
+// M.c ^ w
+__device__ __forceinline__ uint32_t xapply(const XTab &T, uint32_t c, uint32_t w) {
+  uint32_t g[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++)
+    g[j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j == 0 ? (c << 2) : (c >> (6 * j - 2))), (int)T.t[j]);
+  const uint32_t m30 = (uint32_t)((int32_t)(c << 1) >> 31), m31 = (uint32_t)((int32_t)c >> 31);
+  uint32_t a = __builtin_amdgcn_bitop3_b32(m30, T.c30, w, 0x6A);
+  a = __builtin_amdgcn_bitop3_b32(m31, T.c31, a, 0x6A);
+  return xor3(xor3(g[0], g[1], g[2]), g[3], xor3(g[4], a, 0u));
+}
+
+// ---------------------------------------------------------------------------
 // Batched ReadFromDisk on device (lsm/block_manager/block_manager.go:203-235,
 // row f1): verify every block of a contiguous run (CheckBlockIntegrity,
 // crc_util.go:88-100) and strip the CRC words, writing the payloads back to
 // back (block b's block[4:B] at out + b*(B-4)) -- the inverse of k_frame, one
 // read of the blocks and one write of the payload.  B = 4096 << lg_groups.
-// A wave walks its blocks in 4 KiB groups (4 rows of 1 KiB), the next group's
-// rows in flight while the current one is hashed and stored.  Payload stores are 16-B unaligned stores (output is shifted 4 bytes per block); lane 0 of a
-// block's first row stores bytes 4..19 instead (lane 1's first word via DPP),
-// overlapping lane 1's store with identical bytes.
-// Store order: the group's four rows are hashed, then its four payload stores
-// (global nt) are issued together -- +3.9 % over storing each row before
-// hashing it, at the speed of the timing-only build (profiles/r2/framing_store/;
-// the other orders and cache policies are in tools/ab_hc_kernels.hip).
+//   * 4-wave workgroups, each wave kUnframeWaveGroups (hc_kernels.hpp) 4 KiB groups (K = 4 blocks
+//     of 4 KiB, 2 of 8 KiB, 1 of 16 KiB) in order, the next group's rows in
+//     flight while the current one is hashed and stored, then exit.  The
+//     persistent 16-wave version with 144 KiB of LDS tables ran 5.0-5.2 TB/s;
+//     this one 5.45-5.57 (tools/kframe3, profiles/r3/framing/: +5-8 % on two
+//     boxes), at the copy rate of the same geometry.
+//   * Row steps and the stream combine through XTab (ds_bpermute); the lane
+//     placement is the 32x32 mat-vec on the VALU against the lane's 32
+//     columns of the constant image.
+//   * Payload stores are 16-B unaligned stores (output is shifted 4 bytes per
+//     block); lane 0 of a block's first row stores bytes 4..19 instead (lane
+//     1's first word via DPP), overlapping lane 1's store with identical bytes.
+//     A group's four rows are hashed, then its four stores are issued together
+//     (+3.9 % over storing each row before hashing it, profiles/r2/framing_store/).
+//   * first_bad: a wave lowers it at most once, and only after reading it
+//     (a batch of all-bad blocks would otherwise put ~nblk/4 atomics on one word).
 template <uint32_t lg_groups>
-__global__ __launch_bounds__(kFastThreads) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
-                                                           uint32_t lg_chunk, uint8_t *__restrict__ out,
-                                                           uint32_t *__restrict__ crc_out,
-                                                           uint32_t *__restrict__ bad_bitmap,
-                                                           unsigned long long *__restrict__ first_bad,
-                                                           const DeviceTables *__restrict__ tables) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
-  __shared__ uint32_t s_next;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) s_next = 2 * kFastWaves;  // two hand-outs per wave before the counter
-  fill_crc_tables(lds, tables, tid, kFastThreads);
+__global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
+                                                 uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
+                                                 uint32_t *__restrict__ bad_bitmap,
+                                                 unsigned long long *__restrict__ first_bad,
+                                                 const DeviceTables *__restrict__ tables) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  constexpr uint32_t kGroups = 1u << lg_groups, gmask = kGroups - 1u;
+  constexpr uint32_t K = kUnframeWaveGroups >> lg_groups > 0 ? kUnframeWaveGroups >> lg_groups : 1u;  // blocks per wave
+  constexpr uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * K;
+  if (b0 >= nblk) return;
+  const uint64_t p_end = (b0 + K < nblk ? b0 + K : nblk) << lg_groups;  // this wave's groups [p0, p_end)
+  uint64_t p = b0 << lg_groups;
+  const uint32_t w0 = tables->w0;
+  u32x4 v[4];
+  auto load4 = [&](uint64_t q) {
+    const uint8_t *S = blocks + q * HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
+  };
+  load4(p);
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  const uint32_t w0 = tables->w0;
-  __syncthreads();
-  const uint32_t r4 = (lane & 31u) << 2;
-  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
-  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
-  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
-    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
-    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
-    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
-    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
-    return xor3(xor3(t0, t1, t2), t3, w);
-  };
-  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
-    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
-    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
-    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
-    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
-    return xor3(xor3(t0, t1, t2), t3, w);
-  };
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef u32x4 u32x4_u __attribute__((aligned(1)));
-  const uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
-  const uint32_t gmask = (1u << lg_groups) - 1u;
-  const uint32_t wave = uni(tid >> 6);
-  // blocks handed out as in k_crc_grp (chunks of 2^lg_chunk consecutive blocks
-  // per workgroup, one block at a time per wave from an LDS counter); a wave
-  // walks a block's 4 KiB groups in order
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
-  const uint32_t cmask = (1u << lg_chunk) - 1u;
-  auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
-  const uint64_t bstart = blk_of(wave);
-  if (bstart >= nblk) return;
-  auto load4 = [&](uint64_t p, u32x4 (&v)[4]) {
-    const uint8_t *S = blocks + p * HC_FRAME_BLOCK + 16u * lane;
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
-  };
+  const XTab TM = make_xtab(tables->tg, lane);
+  const XTab TS = make_xtab(tables->s4, lane);
   uint32_t c[4] = {0, 0, 0, 0};
   uint32_t stored = 0;
   bool reported = false;  // wave-uniform: this wave already lowered first_bad
-  auto group = [&](uint64_t p, const u32x4 (&cur)[4]) {
+  for (; p < p_end; p++) {
     const uint64_t b = p >> lg_groups;
     const uint32_t g = (uint32_t)p & gmask;
+    u32x4 cur[4] = {v[0], v[1], v[2], v[3]};
+    if (p + 1 < p_end) load4(p + 1);  // the next group in flight
     uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
     u32x4 sv[4];
     uint8_t *sa[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      u32x4 v = cur[r];
+      u32x4 t = cur[r];
       if (r == 0 && g == 0) {
-        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, v.x, 0x101, 0xF, 0xF, false);  // lane+1's x
-        stored = __builtin_amdgcn_readfirstlane(v.x);                   // LE32(block[0:4])
-        const u32x4 first = {v.y, v.z, v.w, nx};
-        sv[r] = lane == 0 ? first : v;
+        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, t.x, 0x101, 0xF, 0xF, false);  // lane+1's x
+        stored = __builtin_amdgcn_readfirstlane(t.x);                                         // LE32(block[0:4])
+        const u32x4 first = {t.y, t.z, t.w, nx};
+        sv[r] = lane == 0 ? first : t;
         sa[r] = ob + (lane == 0 ? 4 : 0);
-        v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
+        t.x = lane == 0 ? w0 : t.x;  // Go's init in place of the CRC field
       } else {
-        sv[r] = v;
+        sv[r] = t;
         sa[r] = ob + r * kRowBytes;
       }
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t w[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = (r == 0 && g == 0) ? w[k] : row_step(c[k], w[k]);
+      for (int k = 0; k < 4; k++) c[k] = (r == 0 && g == 0) ? w[k] : xapply(TM, c[k], w[k]);
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
     if (g == gmask) {
-      const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-      const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
+      const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
+      const uint32_t crcv = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
       if (crc_out) lane0_store_u32(crc_out + b, crcv);
       if (first_bad && crcv != stored) {  // wave-uniform
         if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
-        if (!reported) lane0_atomic_umin64(first_bad, b);
-        reported = true;  // blocks come in increasing order (see k_crc_fast)
+        if (!reported && b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+          lane0_atomic_umin64(first_bad, b);
+        reported = true;  // a wave's blocks come in increasing order
       }
     }
-  };
-  // group stream of this wave: (block, group) pairs; the producer cursor runs
-  // one group ahead of the group being stored and hashed
-  uint64_t pb = bstart, nb = blk_of(kFastWaves + wave);
-  uint32_t pg = 0;
-  bool pv = true;
-  uint32_t knv = 0;  // LDS hand-out result for the block after nb, read one block later
-  if (lane == 0) knv = atomicAdd(&s_next, 1u);
-  auto padv = [&]() {  // producer -> next group of the stream (pv = false past the end)
-    if (pg < gmask) {
-      pg++;
-      return;
-    }
-    pb = nb;
-    pg = 0;
-    pv = pb < nblk;
-    nb = blk_of(uni(knv));
-    if (lane == 0) knv = atomicAdd(&s_next, 1u);
-  };
-  // first group peeled: both edges into the loop header carry the same VMEM
-  // sequence (see k_frame); past the end a wave re-reads its current group
-  auto pnext = [&](uint64_t fallback, bool &valid) {  // the producer's next group (or fallback)
-    padv();
-    valid = pv;
-    return pv ? (pb << lg_groups) + pg : fallback;
-  };
-  uint64_t p = bstart << lg_groups;
-  u32x4 A[4], Bv[4];
-  load4(p, A);
-  bool qv;
-  uint64_t q = pnext(p, qv);
-  load4(q, Bv);
-  group(p, A);
-  while (qv) {
-    p = q;
-    q = pnext(p, qv);
-    load4(q, A);
-    group(p, Bv);
-    if (!qv) break;
-    p = q;
-    q = pnext(p, qv);
-    load4(q, Bv);
-    group(p, A);
   }
 }
 
@@ -1887,11 +1874,14 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
 
 hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_groups, uint8_t *out,
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
-                          const DeviceTables *tables, int grid, hipStream_t s) {
+                          const DeviceTables *tables, hipStream_t s) {
   if (nblk == 0) return hipSuccess;
-  const uint32_t lgc = grp_lg_chunk(nblk, grid, 4096u << lg_groups);
+  if (!blocks || !out || lg_groups > 2) return hipErrorInvalidValue;
+  const uint64_t per_wg = 4ull * (kUnframeWaveGroups >> lg_groups ? kUnframeWaveGroups >> lg_groups : 1u);  // blocks
+  const uint64_t grid = (nblk + per_wg - 1) / per_wg;
+  if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #define HC_UNFRAME(L)                                                                                      \
-  hipLaunchKernelGGL((k_unframe<L>), dim3(grid), dim3(kFastThreads), 0, s, blocks, nblk, lgc, out, crc_out, bad_bitmap, \
+  hipLaunchKernelGGL((k_unframe<L>), dim3((unsigned)grid), dim3(256), 0, s, blocks, nblk, out, crc_out, bad_bitmap, \
                      first_bad, tables)
   if (lg_groups == 0)
     HC_UNFRAME(0);

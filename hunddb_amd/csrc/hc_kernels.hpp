@@ -57,11 +57,13 @@ hipError_t launch_grp(const Batch &b, int grid, hipStream_t s);
 constexpr uint32_t HC_FRAME_BLOCK = 4096;
 hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
                         const DeviceTables *tables, int grid, hipStream_t s);
+constexpr uint32_t kUnframeWaveGroups = 4;  // k_unframe: 4 KiB groups per wave (16 KiB)
 // Batched ReadFromDisk: verify nblk blocks of 4096 << lg_groups bytes at `blocks`
-// (16-B aligned) and write their payloads back to back at `out`.
+// (16-B aligned) and write their payloads back to back at `out`.  Its own grid
+// (4-wave workgroups, 16 KiB of blocks per wave).
 hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_groups, uint8_t *out,
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
-                          const DeviceTables *tables, int grid, hipStream_t s);
+                          const DeviceTables *tables, hipStream_t s);
 // synthetic workload: buffer block i = block first + i of the seeded batch
 hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
                        uint32_t ulen, uint64_t n, uint64_t seed, int grid, hipStream_t s, uint64_t first = 0);

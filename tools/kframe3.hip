@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256) void k_frame_xh(const uint8_t *__restrict__ sr
 // Interior blocks only (1 .. nblk-2), no edge path (its funnel-shift
 // registers raised the kernel to 160+ VGPRs): K blocks per wave, kW waves per
 // workgroup; the two edge blocks go to k_frame_edges_xh (one small launch).
-template <int K, int kW>
-__global__ __launch_bounds__(kW * 64) void k_frame_xi(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+template <int K, int kW, int kOcc = 1>
+__global__ __attribute__((amdgpu_waves_per_eu(kOcc))) __launch_bounds__(kW * 64) void k_frame_xi(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                       uint64_t nblk, uint32_t *__restrict__ crc_out,
                                                       const XbCols *__restrict__ xc,
                                                       const hc::DeviceTables *__restrict__ tables) {
@@ -287,8 +287,8 @@ __global__ __launch_bounds__(128) void k_frame_edges_xh(const uint8_t *__restric
 }
 
 // Hybrid ReadFromDisk of 4 KiB blocks (as k_unframe_xb, Tab5 + per-lane placement).
-template <int K, int kW = 4>
-__global__ __launch_bounds__(kW * 64) void k_unframe_xh(const uint8_t *__restrict__ blocks, uint64_t nblk,
+template <int K, int kW = 4, int kOcc = 1>
+__global__ __attribute__((amdgpu_waves_per_eu(kOcc))) __launch_bounds__(kW * 64) void k_unframe_xh(const uint8_t *__restrict__ blocks, uint64_t nblk,
                                                     uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
                                                     uint32_t *__restrict__ bad_bitmap,
                                                     unsigned long long *__restrict__ first_bad,
@@ -615,7 +615,7 @@ int main(int argc, char **argv) {
   std::vector<Variant> vs;
   auto prod_frame = [&](hipStream_t st) { CK(hc::launch_frame(src, npay, framed, crc, dt, cus, st)); };
   auto prod_unframe = [&](hipStream_t st) {
-    CK(hc::launch_unframe(blocks, nblk, 0, pay, crc, bitmap, fb, dt, cus, st));
+    CK(hc::launch_unframe(blocks, nblk, 0, pay, crc, bitmap, fb, dt, st));
   };
 #define XB(K, M)                                                                                                    \
   [&](hipStream_t st) {                                                                                             \
@@ -639,17 +639,17 @@ int main(int argc, char **argv) {
     const uint64_t g_ = (nblk + 4 * (K)-1) / (4 * (K));                                                         \
     hipLaunchKernelGGL((xb::k_frame_xh<K>), dim3((unsigned)g_), dim3(256), 0, st, src, npay, framed, nblk, crc, xc, dt); \
   }
-#define XHU(K, W)                                                                                                 \
+#define XHU(K, W, ...)                                                                                            \
   [&](hipStream_t st) {                                                                                              \
     const uint64_t g_ = (nblk + (W) * (K)-1) / ((W) * (K));                                                          \
-    hipLaunchKernelGGL((xb::k_unframe_xh<K, W>), dim3((unsigned)g_), dim3((W) * 64), 0, st, blocks, nblk, pay, crc,   \
+    hipLaunchKernelGGL((xb::k_unframe_xh<K, W __VA_OPT__(,) __VA_ARGS__>), dim3((unsigned)g_), dim3((W) * 64), 0, st, blocks, nblk, pay, crc,   \
                        bitmap, fb, xc, dt);                                                                          \
   }
-#define XI(K, W)                                                                                                     \
+#define XI(K, W, ...)                                                                                                \
   [&](hipStream_t st) {                                                                                             \
     hipLaunchKernelGGL(xb::k_frame_edges_xh, dim3(1), dim3(128), 0, st, src, npay, framed, nblk, crc, xc, dt);        \
     const uint64_t g_ = (nblk - 2 + (W) * (K)-1) / ((W) * (K));                                                      \
-    hipLaunchKernelGGL((xb::k_frame_xi<K, W>), dim3((unsigned)g_), dim3((W) * 64), 0, st, src, framed, nblk, crc, xc, \
+    hipLaunchKernelGGL((xb::k_frame_xi<K, W __VA_OPT__(,) __VA_ARGS__>), dim3((unsigned)g_), dim3((W) * 64), 0, st, src, framed, nblk, crc, xc, \
                        dt);                                                                                         \
   }
   vs.push_back({"PROD k_frame (persistent, LDS tables)", 0, true, prod_frame, {}});
@@ -660,6 +660,9 @@ int main(int argc, char **argv) {
   vs.push_back({"hybrid frame interior K=16 W=4", 0, true, XI(16, 4), {}});
   vs.push_back({"hybrid frame interior K=4 W=8", 0, true, XI(4, 8), {}});
   vs.push_back({"hybrid frame interior K=4 W=2", 0, true, XI(4, 2), {}});
+  vs.push_back({"hybrid frame interior K=4 W=4 occ5", 0, true, XI(4, 4, 5), {}});
+  vs.push_back({"hybrid frame interior K=8 W=4 occ5", 0, true, XI(8, 4, 5), {}});
+  vs.push_back({"hybrid frame interior K=8 W=4 occ6", 0, true, XI(8, 4, 6), {}});
   vs.push_back({"NULL np frame K=1 (memory pattern)", 0, false, XBN(1), {}});
   vs.push_back({"NULL np frame K=4 (memory pattern)", 0, false, XBN(4), {}});
   vs.push_back({"PROD k_unframe (persistent, LDS tables)", 1, true, prod_unframe, {}});
@@ -669,6 +672,9 @@ int main(int argc, char **argv) {
   vs.push_back({"hybrid unframe K=16 W=4", 1, true, XHU(16, 4), {}});
   vs.push_back({"hybrid unframe K=4 W=8", 1, true, XHU(4, 8), {}});
   vs.push_back({"hybrid unframe K=4 W=2", 1, true, XHU(4, 2), {}});
+  vs.push_back({"hybrid unframe K=4 W=4 occ5", 1, true, XHU(4, 4, 5), {}});
+  vs.push_back({"hybrid unframe K=8 W=4 occ5", 1, true, XHU(8, 4, 5), {}});
+  vs.push_back({"hybrid unframe K=8 W=4 occ6", 1, true, XHU(8, 4, 6), {}});
   vs.push_back({"PROD k_frame (again)", 0, true, prod_frame, {}});
   vs.push_back({"PROD k_unframe (again)", 1, true, prod_unframe, {}});
 
