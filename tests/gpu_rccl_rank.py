@@ -1,7 +1,8 @@
 """Child process of tests/test_gpu_rccl.py: one rank of a "nccl" (RCCL) process
 group on cuda:0.  It hashes its shard of a global batch with the HIP path,
-all-gathers the words with shard.gather_crcs and runs the float64 MAX/SUM
-all-reduces that shard.job_timing issues at N > 1, then prints one JSON line.
+all-gathers the words with shard.gather_crcs, runs the float64 MAX/SUM
+all-reduces that shard.job_timing issues at N > 1 and the device-identity
+all-gather of bench.py's multi_gpu proof, then prints one JSON line.
 On a one-GPU box the group has one rank: no xGMI traffic, but every RCCL call
 bench.py makes at N > 1 runs (communicator init, all_gather, all_reduce)."""
 import json
@@ -36,8 +37,10 @@ def main():
     b = torch.tensor([float(hi - lo)], dtype=torch.float64, device=dev)
     dist.all_reduce(b, op=dist.ReduceOp.SUM)
     torch.cuda.synchronize()
+    # bench.py's multi_gpu proof fields over RCCL (object all-gather on the device)
+    proof = shard.device_proof(shard.gather_identities(shard.rank_identity(dev, 1.25)), "nccl")
     res = {"backend": dist.get_backend(), "world": world, "kernel": crc.last_launch()["kernel"],
-           "max": t.cpu().tolist(), "sum": float(b.item())}
+           "max": t.cpu().tolist(), "sum": float(b.item()), "proof": proof}
     if rank == 0:
         res["words"] = got.cpu().numpy().view(np.uint32).tolist()
         res["gathered_device"] = str(got.device)

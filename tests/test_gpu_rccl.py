@@ -33,6 +33,12 @@ def test_rccl_gather_and_reduce_one_rank(cuda, oracle):
     assert res["kernel"] == "k_crc_grp"
     assert res["gathered_device"].startswith("cuda")  # all_gather ran on device tensors
     assert res["max"] == [1.5, 2.5] and res["sum"] == float(n)
+    p = res["proof"]  # bench.py's multi_gpu proof fields, gathered over RCCL
+    assert p["comm_world_size"] == 1 and p["distinct_devices"] == 1 and p["rehearsal"] is False
+    assert p["backend"] == "nccl" and p["rccl_version"] and not p["rccl_version"].startswith("unknown")
+    r0 = p["ranks"][0]
+    assert r0["rank"] == 0 and r0["device"] == 0 and r0["kernel_ms"] == 1.25
+    assert r0["hc_devices"] >= 1 and len(r0["bus_id"].split(":")) == 3
     B = 8192
     host, _, _ = oracle.fill_blocks(0x5EED, n, B)
     want = oracle.crc32_blocks(host, stride=B, ulen=B)

@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void k_frame_xh(const uint8_t *__restrict__ sr
 // Interior blocks only (1 .. nblk-2), no edge path (its funnel-shift
 // registers raised the kernel to 160+ VGPRs): K blocks per wave, kW waves per
 // workgroup; the two edge blocks go to k_frame_edges_xh (one small launch).
-template <int K, int kW, int kOcc = 1>
+template <int K, int kW, int kOcc = 1, int kOrd = 0>
 __global__ __attribute__((amdgpu_waves_per_eu(kOcc))) __launch_bounds__(kW * 64) void k_frame_xi(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                       uint64_t nblk, uint32_t *__restrict__ crc_out,
                                                       const XbCols *__restrict__ xc,
@@ -232,14 +232,20 @@ __global__ __attribute__((amdgpu_waves_per_eu(kOcc))) __launch_bounds__(kW * 64)
     const uint64_t b = b0 + k;
     if (b >= bend) break;
     uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+    auto stores = [&](const u32x4 (&src4)[4]) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      u32x4 t = v[r];
-      if (r == 0) t.x = lane == 0 ? 0u : t.x;
-      __builtin_nontemporal_store(t, reinterpret_cast<u32x4 *>(ob + r * hc::kRowBytes));
-    }
+      for (int r = 0; r < 4; r++) {
+        u32x4 t = src4[r];
+        if (r == 0) t.x = lane == 0 ? 0u : t.x;
+        __builtin_nontemporal_store(t, reinterpret_cast<u32x4 *>(ob + r * hc::kRowBytes));
+      }
+    };
+    // kOrd 0: stores, next loads, hash; 1: next loads, stores, hash;
+    // 2: next loads, hash, stores (k_unframe's order)
+    if (kOrd == 0) stores(v);
     u32x4 cur[4] = {v[0], v[1], v[2], v[3]};
     if (k + 1 < K && b + 1 < bend) load4(b + 1);
+    if (kOrd == 1) stores(cur);
     uint32_t c[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -249,6 +255,7 @@ __global__ __attribute__((amdgpu_waves_per_eu(kOcc))) __launch_bounds__(kW * 64)
 #pragma unroll
       for (int q = 0; q < 4; q++) c[q] = r == 0 ? wd[q] : apply5(TM, c[q], wd[q]);
     }
+    if (kOrd == 2) stores(cur);
     const uint32_t d = apply5(TS, apply5(TS, apply5(TS, c[0], c[1]), c[2]), c[3]);
     const uint32_t crc = hc::wave_xor(hc::matvec32(col, d)) ^ 0xFFFFFFFFu;
     hc::lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crc);
@@ -653,30 +660,19 @@ int main(int argc, char **argv) {
                        dt);                                                                                         \
   }
   vs.push_back({"PROD k_frame (persistent, LDS tables)", 0, true, prod_frame, {}});
-  vs.push_back({"hybrid frame K=4 (edge path inline)", 0, true, XH(4), {}});
-  vs.push_back({"hybrid frame interior K=2 W=4", 0, true, XI(2, 4), {}});
-  vs.push_back({"hybrid frame interior K=4 W=4", 0, true, XI(4, 4), {}});
-  vs.push_back({"hybrid frame interior K=8 W=4", 0, true, XI(8, 4), {}});
-  vs.push_back({"hybrid frame interior K=16 W=4", 0, true, XI(16, 4), {}});
-  vs.push_back({"hybrid frame interior K=4 W=8", 0, true, XI(4, 8), {}});
-  vs.push_back({"hybrid frame interior K=4 W=2", 0, true, XI(4, 2), {}});
-  vs.push_back({"hybrid frame interior K=4 W=4 occ5", 0, true, XI(4, 4, 5), {}});
-  vs.push_back({"hybrid frame interior K=8 W=4 occ5", 0, true, XI(8, 4, 5), {}});
-  vs.push_back({"hybrid frame interior K=8 W=4 occ6", 0, true, XI(8, 4, 6), {}});
+  vs.push_back({"hybrid frame interior K=4 W=4 st,ld,hash", 0, true, XI(4, 4), {}});
+  vs.push_back({"hybrid frame interior K=4 W=4 ld,st,hash", 0, true, XI(4, 4, 1, 1), {}});
+  vs.push_back({"hybrid frame interior K=4 W=4 ld,hash,st", 0, true, XI(4, 4, 1, 2), {}});
+  vs.push_back({"hybrid frame interior K=8 W=4 ld,hash,st", 0, true, XI(8, 4, 1, 2), {}});
+  vs.push_back({"hybrid frame interior K=4 W=8 ld,hash,st", 0, true, XI(4, 8, 1, 2), {}});
+  vs.push_back({"hybrid frame interior K=1 W=4 st,ld,hash", 0, true, XI(1, 4), {}});
+  vs.push_back({"hybrid frame interior K=2 W=8 ld,hash,st", 0, true, XI(2, 8, 1, 2), {}});
   vs.push_back({"NULL np frame K=1 (memory pattern)", 0, false, XBN(1), {}});
   vs.push_back({"NULL np frame K=4 (memory pattern)", 0, false, XBN(4), {}});
-  vs.push_back({"PROD k_unframe (persistent, LDS tables)", 1, true, prod_unframe, {}});
-  vs.push_back({"hybrid unframe K=2 W=4", 1, true, XHU(2, 4), {}});
-  vs.push_back({"hybrid unframe K=4 W=4", 1, true, XHU(4, 4), {}});
-  vs.push_back({"hybrid unframe K=8 W=4", 1, true, XHU(8, 4), {}});
-  vs.push_back({"hybrid unframe K=16 W=4", 1, true, XHU(16, 4), {}});
+  vs.push_back({"PROD k_unframe (round 3: LDS-free, 4-wave WGs)", 1, true, prod_unframe, {}});
   vs.push_back({"hybrid unframe K=4 W=8", 1, true, XHU(4, 8), {}});
-  vs.push_back({"hybrid unframe K=4 W=2", 1, true, XHU(4, 2), {}});
-  vs.push_back({"hybrid unframe K=4 W=4 occ5", 1, true, XHU(4, 4, 5), {}});
-  vs.push_back({"hybrid unframe K=8 W=4 occ5", 1, true, XHU(8, 4, 5), {}});
-  vs.push_back({"hybrid unframe K=8 W=4 occ6", 1, true, XHU(8, 4, 6), {}});
   vs.push_back({"PROD k_frame (again)", 0, true, prod_frame, {}});
-  vs.push_back({"PROD k_unframe (again)", 1, true, prod_unframe, {}});
+  vs.push_back({"PROD k_unframe (round 3, again)", 1, true, prod_unframe, {}});
 
   // reference outputs: production frame, production unframe (words, bytes, bitmap, first bad)
   std::vector<uint32_t> cref_f(N), cref_u(N), got(N), bm_ref((N + 31) / 32), bm(bm_ref.size());
