@@ -43,6 +43,15 @@ struct DeviceState {
   DeviceTables *dtab = nullptr;  // device copy of the constant image
   SegTables *dseg = nullptr;     // the packed-record path's tables (k_seg_*)
   uint32_t *seg_last = nullptr;  // 1 when the last packed-record stream took its batch
+  // the packed-record stream's workspace for calls on the null stream, kept
+  // across calls: that stream orders every use after the previous one and is
+  // never destroyed.  Calls on other streams (which may be destroyed and their
+  // handles reused) or under graph capture take one from the stream-ordered
+  // allocator per call.  An event ordering a kept workspace across streams
+  // costs what the allocator pair does (profiles/r3/seg/).
+  std::mutex seg_mu;
+  uint32_t *seg_ws = nullptr;
+  uint64_t seg_ws_bytes = 0;
 };
 
 constexpr int kMaxDevices = 64;
@@ -154,12 +163,37 @@ namespace {
 // launch_seg): it takes the batch when its messages lie back to back
 // (off[i+1] = off[i] + len[i]) and mostly at least 64 B long, and raises a
 // device flag otherwise, on which k_crc_grp + k_crc_any run as before.  The
-// decision is made on the device (no host sync); the workspace comes from the
-// stream-ordered allocator.  The span is bounded by the allocation holding
+// decision is made on the device (no host sync).  On the null stream the
+// workspace is kept across calls (seg_cached_ws: a per-call hipMallocAsync /
+// hipFreeAsync pair cost 4-17 us a call, tools/kseg3.hip); other streams take
+// one from the stream-ordered allocator per call.  The span is bounded by the allocation holding
 // `base` (a batch reaching past it is not packed for the stream).
 uint64_t seg_min_msgs() {
   const char *v = std::getenv("HC_SEG_MIN_MSGS");
   return v && *v ? std::strtoull(v, nullptr, 10) : (1ull << 17);
+}
+
+// The kept workspace (null stream only), grown to `need` bytes on that stream,
+// so the free is ordered after every earlier use.  The lock is held from here
+// until the caller has enqueued the launches that use it.  nullptr: allocate
+// per call.
+uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::unique_lock<std::mutex> &lk) {
+  if (s != nullptr) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  lk = std::unique_lock<std::mutex>(d.seg_mu);
+  if (d.seg_ws && d.seg_ws_bytes >= need) return d.seg_ws;
+  if (d.seg_ws) (void)hipFreeAsync(d.seg_ws, s);
+  d.seg_ws = nullptr;
+  d.seg_ws_bytes = 0;
+  const uint64_t bytes = need + need / 4;  // headroom for a slightly larger next batch
+  if (hipMallocAsync(reinterpret_cast<void **>(&d.seg_ws), bytes, s) != hipSuccess) {
+    d.seg_ws = nullptr;
+    lk.unlock();
+    return nullptr;
+  }
+  d.seg_ws_bytes = bytes;
+  return d.seg_ws;
 }
 
 int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
@@ -207,7 +241,8 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
     info.kernel = "k_crc_any";
     info.general_blocks = n;
   } else {
-    uint32_t *seg_ws = nullptr;
+    uint32_t *seg_ws = nullptr;           // a per-call workspace (else the kept one, under seg_lock)
+    std::unique_lock<std::mutex> seg_lock;  // held while the kept workspace's launches are enqueued
     // the stream's only output is crc_out (k_seg_combine): a batch without it
     // (verify or stamp only) takes k_crc_grp + k_crc_any
     if (seg_ok && (flags & kFlagMessages) && crc_out && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
@@ -216,10 +251,11 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       if (hipMemGetAddressRange(&pb, &ps, const_cast<uint8_t *>(base)) == hipSuccess && ps) {
         const uint64_t lo = reinterpret_cast<uintptr_t>(base) & ~uint64_t(1023);
         const uint64_t mu = seg_max_units(reinterpret_cast<uintptr_t>(pb) + ps - lo);
-        if (hipMallocAsync(reinterpret_cast<void **>(&seg_ws), seg_workspace_bytes(n, mu), s) != hipSuccess)
-          seg_ws = nullptr;
-        else if ((e = launch_seg(b, d.dseg, seg_ws, mu, fast_grid, s, d.seg_last)) == hipSuccess)
-          b.seg_flag = seg_ws;  // word 0: raised when the stream did not take the batch
+        const uint64_t need = seg_workspace_bytes(n, mu);
+        uint32_t *ws = seg_cached_ws(d, s, need, seg_lock);
+        if (!ws && hipMallocAsync(reinterpret_cast<void **>(&seg_ws), need, s) == hipSuccess) ws = seg_ws;
+        if (ws && (e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last)) == hipSuccess)
+          b.seg_flag = ws;  // word 0: raised when the stream did not take the batch
       }
     }
     // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk

@@ -142,12 +142,21 @@ inline Mat32 shift_mat(const Gf2 &g, uint64_t n) {
 //   pw[k][j][b]  = shift(b << 8j, 1024 * 2^k)     shift by whole rows
 //   inv[k][j][b] = shift^-1(b << 8j, 2^k)          inverse shift by bytes
 //   ones[d-1]    = shift(0xFFFFFFFF, d), d = 1..1024
+//   rs[s-1][j][b] = shift(b << 8j, 1024 * s), s = 1..16    (k_seg_combine: one
+//                   multiply per row shift inside a unit)
+//   iv[..][j][b]  = shift^-1(b << 8j, e) for the octal digits of e - 1,
+//                   e = 1..1024 (kSegIvD0..: 8 + 7 + 7 + 1 tables)
+// pw and inv (binary digits) serve the A/B builds under tools/.
 constexpr int kSegPw = 29;   // rows up to 2^29 (2^39 bytes)
 constexpr int kSegInv = 11;  // byte distances 1 .. 1024
+constexpr int kSegRs = 16;   // row shifts 1 .. 16 (one unit)
+constexpr int kSegIvD1 = 8, kSegIvD2 = 15, kSegIvD3 = 22, kSegIv = 23;
 struct SegTables {
   uint32_t pw[kSegPw][4][256];
   uint32_t inv[kSegInv][4][256];
   uint32_t ones[1024];
+  uint32_t rs[kSegRs][4][256];
+  uint32_t iv[kSegIv][4][256];
 };
 
 inline void build_seg_tables(SegTables &t) {
@@ -166,6 +175,19 @@ inline void build_seg_tables(SegTables &t) {
     fill(t.inv[k], v);
     v = mat_mul(v, v);
   }
+  for (int r = 1; r <= kSegRs; r++) fill(t.rs[r - 1], shift_mat(g, (uint64_t)kRowBytes * r));
+  // inverse shifts: digit 0 by v + 1 bytes (v = 0..7), digit 1 by 8v, digit 2
+  // by 64v (v = 1..7), digit 3 by 512
+  Mat32 ip[1025];
+  ip[0] = shift_mat(g, 0);
+  ip[1] = mat_inverse(shift_mat(g, 1));
+  for (int e = 2; e <= 1024; e++) ip[e] = mat_mul(ip[e - 1], ip[1]);
+  for (int v = 0; v < 8; v++) fill(t.iv[v], ip[v + 1]);
+  for (int v = 1; v < 8; v++) {
+    fill(t.iv[kSegIvD1 + v - 1], ip[8 * v]);
+    fill(t.iv[kSegIvD2 + v - 1], ip[64 * v]);
+  }
+  fill(t.iv[kSegIvD3], ip[512]);
   uint32_t c = 0xFFFFFFFFu;
   for (int d = 1; d <= 1024; d++) {
     c = g.shift_bytes(c, 1);

@@ -1349,12 +1349,14 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 // ---------------------------------------------------------------------------
 // Packed whole-message batches (records back to back: off[i+1] = off[i] +
 // len[i], GetCRC of each; config 5's per-record variant) by ONE stream over
-// their span instead of one wave per record.  With G(x) = raw(A0 .. x) over the
-// span from the 1 KiB-aligned origin A0, every record [a, b) is
-//     ChecksumIEEE = G(b) ^ shift(G(a) ^ ~0, b - a) ^ ~0,
-// so the stream only has to leave G at the record boundaries ("events").
+// their span instead of one wave per record.  raw is linear, so every record
+// [a, b) is ChecksumIEEE = raw(a .. b) ^ shift(~0, b - a) ^ ~0 with raw(a .. b)
+// from the span's raw CRCs at a and b relative to any common origin; the stream
+// only has to leave them at the record boundaries ("events"), relative to the
+// 16 KiB unit holding each event.
 //   k_seg_plan     events -> first event of every 16 KiB unit; checks that the
-//                  batch is packed (else a flag sends it to k_crc_any)
+//                  batch is packed and no record exceeds kSegMaxRecord (else a
+//                  flag, stored by k_seg_stream, sends it to k_crc_grp + k_crc_any)
 //   k_seg_stream   k_crc_grp's rows, groups and hand-out over the span's units;
 //                  per unit its raw CRC, and at every row holding events
 //                  H(x) = shift(raw(unit .. x), re - x) (re = the row's end):
@@ -1362,14 +1364,12 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 //                  bytes before x placed at the row end (lane placement of the
 //                  whole lane chunks before x by an exclusive XOR scan, of the
 //                  event's own lane chunk masked at x)
-//   k_seg_scan_*   G at every unit start (prefix within blocks of 1024 units,
-//                  over the blocks, then per unit)
-//   k_seg_combine  per event: G(x) advanced to its row end = K(x) =
-//                  shift(G(unit), re - unit) ^ H(x); per record
-//                  shift(crc ^ ~0, re_b - b) = K(b) ^ shift(K(a) ^ shift(~0, re_a - a), re_b - re_a)
-//                  and one inverse shift by re_b - b (SegTables).
+//   k_seg_combine  per record: H(a) and H(b) plus the raw CRCs of the whole
+//                  units between them, advanced to re_b, then one inverse
+//                  shift by re_b - b (SegTables: 6 table multiplies a record).
 constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups
-constexpr uint32_t kSegScanLg = 10;  // units per scan block
+constexpr uint32_t kSegMaxRecord = 1u << 24;  // longest record the stream takes (16 MiB)
+constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's grid cap: one "bad" slot per workgroup
 
 struct SegGeo {
   uint64_t a0, pend, units;
@@ -1383,17 +1383,16 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
   return g;
 }
 
-// shift by a byte-table multiply (4 lookups in a SegTables table)
-__device__ __forceinline__ uint32_t seg_tmul(const uint32_t (*t)[256], uint32_t v) {
-  return xor3(t[0][v & 255u], t[1][(v >> 8) & 255u], t[2][(v >> 16) & 255u]) ^ t[3][v >> 24];
-}
 // Events: position j = base + off[j] (j < n) and the span's end (j = n).
 // first_ev[u] = first event in unit u (u = 0 .. units; first_ev[units] = n + 1).
-// The flag is raised when the batch is not packed, exceeds max_units, or has
-// more than 64 events in one 4 KiB group (records under ~64 B: k_crc_any).
+// Workgroup w writes plan_bad[w] = 1 when its events find the batch not packed,
+// over max_units, with a record over kSegMaxRecord, or with more than 64 events
+// in one 4 KiB group (records under ~64 B: k_crc_any), else 0.  Every slot is
+// written, so the dispatch needs no memset: k_seg_stream's workgroups OR the
+// slots and its workgroup 0 stores the flag the later kernels read.
 __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
-                                                  uint32_t *__restrict__ flag, uint32_t *__restrict__ first_ev) {
+                                                  uint32_t *__restrict__ plan_bad, uint32_t *__restrict__ first_ev) {
   const SegGeo g = seg_geo(base, offs, lens, n);
   bool bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0;
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
@@ -1403,6 +1402,7 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
     if (j > 0) {
       const uint64_t pp = (uint64_t)base + offs[j - 1];
       if ((j < n && offs[j] != offs[j - 1] + lens[j - 1]) || pj < pp) bad = true;
+      if (lens[j - 1] > kSegMaxRecord) bad = true;  // k_seg_combine's unit chain stays <= 1025 units
       ulo = ((pp - g.a0) >> kSegUnitLg) + 1;
     }
     if (j >= 64 && ((pj - g.a0) >> 12) == (((uint64_t)base + offs[j - 64] - g.a0) >> 12)) bad = true;
@@ -1413,14 +1413,16 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
     if (j == n)
       for (uint64_t u = uj + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(n + 1);
   }
-  if (__ballot(bad)) lane0_atomic_or(flag, 1u);
+  const int any_bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) plan_bad[blockIdx.x] = any_bad ? 1u : 0u;  // every slot written: no memset
 }
 
 // (its timing-only builds -- rows XOR-folded, or no event work at all -- are in
 // tools/ab_hc_kernels.hip)
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint32_t lg_chunk, const uint32_t *__restrict__ flag,
+                                                            uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
+                                                            uint32_t plan_wgs, uint32_t *__restrict__ flag,
                                                             const uint32_t *__restrict__ first_ev,
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
                                                             const DeviceTables *__restrict__ tables) {
@@ -1433,8 +1435,11 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  __syncthreads();
-  if (*flag) return;  // not a packed batch: k_crc_any takes it
+  uint32_t bad = 0;
+  for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) bad |= plan_bad[i];
+  if (__syncthreads_or((int)bad)) bad = 1;
+  if (blockIdx.x == 0 && tid == 0) *flag = bad;  // read by k_seg_combine and the fallback kernels
+  if (bad) return;                                // not a packed batch: k_crc_any takes it
 
   const uint32_t r4 = (lane & 31u) << 2;
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
@@ -1609,131 +1614,54 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   }
 }
 
-// LDS copy of SegTables::pw[k0 .. k0+nk) at tl[0 ..) (1024 words per table)
-__device__ __forceinline__ void seg_lds_pw(uint32_t *tl, const SegTables *st, int k0, int nk) {
-  const uint32_t *src = &st->pw[k0][0][0];
-  for (uint32_t i = threadIdx.x; i < (uint32_t)nk * 1024u; i += blockDim.x) tl[i] = src[i];
-}
 __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) {
   return xor3(t[v & 255u], t[256 + ((v >> 8) & 255u)], t[512 + ((v >> 16) & 255u)]) ^ t[768 + (v >> 24)];
 }
 
-// unit_incl[u] = raw of units [block start .. u] (blocks of 1024 units), and
-// blk_tot = each block's total: Hillis-Steele in LDS, persistent grid, the
-// shift tables (2^k units, k < 10) in LDS.
-__global__ __launch_bounds__(1024) void k_seg_scan_units(const uint8_t *base, const uint64_t *__restrict__ offs,
-                                                         const uint32_t *__restrict__ lens, uint64_t n,
-                                                         const uint32_t *__restrict__ flag,
-                                                         const uint32_t *__restrict__ unit_raw,
-                                                         uint32_t *__restrict__ unit_incl, uint32_t *__restrict__ blk_tot,
-                                                         const SegTables *__restrict__ st) {
-  constexpr int kPw0 = kSegUnitLg - 10;  // one unit = 2^4 rows
-  __shared__ uint32_t tl[kSegScanLg * 1024];
-  __shared__ uint32_t sv[1u << kSegScanLg];
-  seg_lds_pw(tl, st, kPw0, kSegScanLg);
-  __syncthreads();
-  if (*flag) return;
-  const SegGeo geo = seg_geo(base, offs, lens, n);
-  const uint32_t t = threadIdx.x;
-  for (uint64_t b = blockIdx.x; (b << kSegScanLg) < geo.units; b += gridDim.x) {
-    const uint64_t u = (b << kSegScanLg) + t;
-    uint32_t v = u < geo.units ? unit_raw[u] : 0u;
-    for (uint32_t k = 0; k < kSegScanLg; k++) {
-      sv[t] = v;
-      __syncthreads();
-      if (t >= (1u << k)) v ^= seg_lds_tmul(tl + k * 1024, sv[t - (1u << k)]);
-      __syncthreads();
-    }
-    if (u < geo.units) unit_incl[u] = v;
-    if (t == (1u << kSegScanLg) - 1) blk_tot[b] = v;
-  }
-}
-
-// blk_pre[b] = raw(A0 .. block b's first unit): one workgroup, runs of
-// consecutive blocks per thread, Hillis-Steele over the run totals (the
-// tables of 2^14 .. 2^28 rows in LDS).
-__global__ __launch_bounds__(1024) void k_seg_scan_blocks(const uint8_t *base, const uint64_t *__restrict__ offs,
-                                                          const uint32_t *__restrict__ lens, uint64_t n,
-                                                          const uint32_t *__restrict__ flag,
-                                                          const uint32_t *__restrict__ blk_tot,
-                                                          uint32_t *__restrict__ blk_pre,
-                                                          const SegTables *__restrict__ st) {
-  constexpr int kBlkPw = (int)(kSegUnitLg - 10 + kSegScanLg);  // one block = 2^14 rows
-  __shared__ uint32_t tl[(kSegPw - kBlkPw) * 1024];
-  __shared__ uint32_t sv[1024];
-  seg_lds_pw(tl, st, kBlkPw, kSegPw - kBlkPw);
-  __syncthreads();
-  if (*flag) return;
-  const SegGeo geo = seg_geo(base, offs, lens, n);
-  const uint64_t nb = (geo.units + (1u << kSegScanLg) - 1) >> kSegScanLg;
-  const uint64_t per = (nb + 1023) / 1024;
-  const uint32_t t = threadIdx.x;
-  const uint64_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
-  auto shift_blocks = [&](uint32_t v, uint64_t blocks) {
-    for (int k = 0; blocks; k++, blocks >>= 1)
-      if (blocks & 1u) v = seg_lds_tmul(tl + k * 1024, v);
-    return v;
-  };
-  uint32_t v = 0;
-  for (uint64_t i = lo; i < hi; i++) v = seg_lds_tmul(tl, v) ^ blk_tot[i];
-  for (uint32_t k = 0; k < 10; k++) {
-    sv[t] = v;
-    __syncthreads();
-    if (t >= (1u << k)) v ^= shift_blocks(sv[t - (1u << k)], per << k);
-    __syncthreads();
-  }
-  sv[t] = v;
-  __syncthreads();
-  uint32_t p = t ? sv[t - 1] : 0u;
-  for (uint64_t i = lo; i < hi; i++) {
-    blk_pre[i] = p;
-    p = seg_lds_tmul(tl, p) ^ blk_tot[i];
-  }
-}
-
-// unit_g[u] = G(unit u's start) = shift(blk_pre[b], i units) ^ unit_incl[u - 1]
-// (u = 1024 b + i; written over unit_raw), persistent grid, tables in LDS.
-__global__ __launch_bounds__(1024) void k_seg_scan_final(const uint8_t *base, const uint64_t *__restrict__ offs,
-                                                         const uint32_t *__restrict__ lens, uint64_t n,
-                                                         const uint32_t *__restrict__ flag,
-                                                         const uint32_t *__restrict__ unit_incl,
-                                                         const uint32_t *__restrict__ blk_pre, uint32_t *__restrict__ unit_g,
-                                                         const SegTables *__restrict__ st) {
-  constexpr int kPw0 = kSegUnitLg - 10;
-  __shared__ uint32_t tl[kSegScanLg * 1024];
-  seg_lds_pw(tl, st, kPw0, kSegScanLg);
-  __syncthreads();
-  if (*flag) return;
-  const SegGeo geo = seg_geo(base, offs, lens, n);
-  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < geo.units;
-       u += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t i = (uint32_t)(u & ((1u << kSegScanLg) - 1));
-    uint32_t v = blk_pre[u >> kSegScanLg];
-#pragma unroll
-    for (int k = 0; k < (int)kSegScanLg; k++)
-      if ((i >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
-    if (i) v ^= unit_incl[u - 1];
-    unit_g[u] = v;
-  }
-}
-
-// Per event x: K(x) = shift(G(x), re - x) = shift(G(U), re - U) ^ H(x) (re - U:
-// 1 .. 16 rows); per record [a, b) from K(a), K(b).  Waves work independently
-// (persistent grid, two workgroups per CU, no barrier after the table fill):
-// an iteration of a wave covers kSub sub-passes of 64 events (K per lane) and
-// 63 records (K(b) from the next lane by a shuffle), with every sub-pass's loads
-// issued before the first is used.  The tables of row shifts up to 63 rows and
-// every inverse byte shift in LDS (68 KiB).
+// Per record [a, b) (events j and j+1), with U_x = x's unit, re_x = x's row
+// end and H(x) = shift(raw(U_x .. x), re_x - x) from k_seg_stream:
+//   shift(crc ^ ~0, re_b - b) = H(b) ^ shift(X, re_b - re_a),  X = H(a) ^ shift(~0, re_a - a)
+// (raw(a||b) = shift(raw(a), |b|) ^ raw(b), and raw(W0) = ~0).  A record that
+// starts and ends in one unit (70 % of config 5b's) shifts X by re_b - re_a
+// <= 15 rows.  One that spans units carries X to its unit's end (<= 15 rows),
+// chains the raw CRCs of the units it crosses (Horner, 16 rows per step) and
+// shifts the result from U_b to re_b (1 .. 16 rows); no prefix over the whole
+// span is needed (round 2 computed one with three scan kernels, 54 us at 2M
+// records).  k_seg_plan caps records at kSegMaxRecord (1024 units).  Then one
+// inverse shift by re_b - b in [1, 1024] bytes, by the octal digits of
+// re_b - b - 1.  Every row shift is ONE table multiply (SegTables::rs) and the
+// inverse shift four (SegTables::iv): 6 multiplies a record where the binary
+// digits took 22 (round 3's first build, 38.6 us at 2M records), all tables in
+// LDS (156 KiB, one workgroup per CU).  Waves work independently (persistent
+// grid, no barrier after the table fill): an iteration of a wave covers kSub
+// sub-passes of 64 events (H per lane) and 63 records (the end event's values
+// from the next lane by a shuffle), every sub-pass's loads issued before the
+// first is used.
 __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ lens, uint64_t n,
                                                       const uint32_t *__restrict__ flag,
-                                                      const uint32_t *__restrict__ unit_g,
+                                                      const uint32_t *__restrict__ unit_raw,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken) {
-  constexpr int kPwL = 6, kInv0 = kPwL * 1024, kSub = 4;
-  __shared__ uint32_t tl[(kPwL + kSegInv) * 1024];
-  seg_lds_pw(tl, st, 0, kPwL);
-  for (uint32_t i = threadIdx.x; i < kSegInv * 1024; i += blockDim.x) tl[kInv0 + i] = (&st->inv[0][0][0])[i];
+  constexpr int kSub = 4, kIv0 = kSegRs * 1024;
+  constexpr uint32_t kUnitRows = 1u << (kSegUnitLg - 10);
+  __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024];
+  {  // rs and iv are contiguous in SegTables: every load issued before the first store
+    static_assert(offsetof(SegTables, iv) == offsetof(SegTables, rs) + sizeof(SegTables::rs), "rs, iv adjacent");
+    constexpr uint32_t kQ = (kSegRs + kSegIv) * 256, kPer = (kQ + 1023) / 1024;  // uint4s; per thread
+    const uint4 *src = reinterpret_cast<const uint4 *>(&st->rs[0][0][0]);
+    uint4 t[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      const uint32_t i = threadIdx.x + k * 1024u;
+      t[k] = i < kQ ? src[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      const uint32_t i = threadIdx.x + k * 1024u;
+      if (i < kQ) reinterpret_cast<uint4 *>(tl)[i] = t[k];
+    }
+  }
   if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
   __syncthreads();
   if (*flag) return;
@@ -1741,9 +1669,12 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  auto rsh = [&](uint32_t v, uint32_t rows) {  // rows in [0, 16]
+    return rows ? seg_lds_tmul(tl + (rows - 1u) * 1024u, v) : v;
+  };
   for (uint64_t c = wv * 63u * kSub; c < n; c += nw * 63u * kSub) {
     uint64_t x[kSub];
-    uint32_t eh[kSub], ug[kSub], kv[kSub], re[kSub];
+    uint32_t eh[kSub];
 #pragma unroll
     for (int p = 0; p < kSub; p++) {  // event c + 63p + lane (past n: the span's end again)
       const uint64_t j = c + 63u * p + lane, jj = j < n ? j : n;
@@ -1751,37 +1682,29 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
       eh[p] = ev_h[jj];
     }
 #pragma unroll
-    for (int p = 0; p < kSub; p++) ug[p] = unit_g[x[p] >> kSegUnitLg];
-#pragma unroll
-    for (int p = 0; p < kSub; p++) {
-      re[p] = (uint32_t)(x[p] >> 10) + 1u;  // the row end, in rows from A0
-      const uint32_t r = re[p] - (uint32_t)((x[p] >> kSegUnitLg) << (kSegUnitLg - 10));  // 1 .. 16 rows
-      uint32_t v = ug[p];
-#pragma unroll
-      for (int k = 0; k <= (int)(kSegUnitLg - 10); k++)
-        if ((r >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
-      kv[p] = v ^ eh[p];
-    }
-#pragma unroll
     for (int p = 0; p < kSub; p++) {
       const uint64_t j = c + 63u * p + lane;
-      const uint32_t kb = __shfl_down(kv[p], 1), rb = __shfl_down(re[p], 1);
+      const uint32_t re = (uint32_t)(x[p] >> 10) + 1u;  // the row end, in rows from A0
+      const uint32_t kb = __shfl_down(eh[p], 1), rb = __shfl_down(re, 1);
       const uint64_t xb = __shfl_down((unsigned long long)x[p], 1);
       if (lane < 63 && j < n) {
-        const uint32_t ra = re[p];
-        const uint32_t da = (uint32_t)(((uint64_t)ra << 10) - x[p]), db = (uint32_t)(((uint64_t)rb << 10) - xb);
-        uint32_t v = kv[p] ^ st->ones[da - 1];  // K(a) ^ shift(~0, d_a), advanced to re_b
-        uint32_t rows = rb - ra;
-#pragma unroll
-        for (int k = 0; k < kPwL; k++)
-          if ((rows >> k) & 1u) v = seg_lds_tmul(tl + k * 1024, v);
-        rows >>= kPwL;
-        for (int k = kPwL; rows; k++, rows >>= 1)
-          if (rows & 1u) v = seg_tmul(st->pw[k], v);
+        const uint32_t da = (uint32_t)(((uint64_t)re << 10) - x[p]), db = (uint32_t)(((uint64_t)rb << 10) - xb);
+        const uint64_t ua = x[p] >> kSegUnitLg, ub = xb >> kSegUnitLg;
+        const uint32_t X = eh[p] ^ st->ones[da - 1];
+        const uint32_t ue = (uint32_t)(ua + 1) * kUnitRows;  // a's unit end, in rows
+        uint32_t v = rsh(X, ua < ub ? ue - re : rb - re);
+        if (ua < ub) {  // the units a .. b-1 (Horner, 16 rows a step), then U_b -> re_b
+          v ^= unit_raw[ua];
+          for (uint64_t u = ua + 1; u < ub; u++) v = seg_lds_tmul(tl + (kUnitRows - 1u) * 1024u, v) ^ unit_raw[u];
+          v = rsh(v, rb - (uint32_t)ub * kUnitRows);
+        }
         uint32_t y = kb ^ v;
-#pragma unroll
-        for (int k = 0; k < kSegInv; k++)
-          if ((db >> k) & 1u) y = seg_lds_tmul(tl + kInv0 + k * 1024, y);
+        const uint32_t e = db - 1u;  // inverse shift by db = 1 + e: octal digits of e
+        const uint32_t *ti = tl + kIv0;
+        y = seg_lds_tmul(ti + (e & 7u) * 1024u, y);
+        if ((e >> 3) & 7u) y = seg_lds_tmul(ti + (kSegIvD1 - 1u + ((e >> 3) & 7u)) * 1024u, y);
+        if ((e >> 6) & 7u) y = seg_lds_tmul(ti + (kSegIvD2 - 1u + ((e >> 6) & 7u)) * 1024u, y);
+        if (e >> 9) y = seg_lds_tmul(ti + kSegIvD3 * 1024u, y);
         crc_out[j] = y ^ 0xFFFFFFFFu;
       }
     }
@@ -1902,30 +1825,23 @@ hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, 
 uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
 
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
-  const uint64_t nb = (max_units >> kSegScanLg) + 1;
-  return 4 * (64 + (max_units + 1) + 2 * max_units + 2 * nb + n + 1);
+  return 4 * (64 + kSegPlanMaxWgs + (max_units + 1) + max_units + n + 1);
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
                       uint32_t *taken, uint32_t lg_chunk) {
   if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
     return hipErrorInvalidValue;
-  const uint64_t n = b.nblocks, nb = (max_units >> kSegScanLg) + 1;
-  uint32_t *flag = ws, *first_ev = ws + 64, *unit_raw = first_ev + max_units + 1, *unit_incl = unit_raw + max_units,
-           *blk_tot = unit_incl + max_units, *blk_pre = blk_tot + nb, *ev_h = blk_pre + nb;
-  hipError_t e = hipMemsetAsync(flag, 0, 4, s);
-  if (e != hipSuccess) return e;
+  const uint64_t n = b.nblocks;
+  uint32_t *flag = ws, *plan_bad = ws + 64, *first_ev = plan_bad + kSegPlanMaxWgs, *unit_raw = first_ev + max_units + 1,
+           *ev_h = unit_raw + max_units;
   const uint64_t pg = (n + 256) / 256;
-  hipLaunchKernelGGL(k_seg_plan, dim3((unsigned)(pg < 16384 ? pg : 16384)), dim3(256), 0, s, b.base, b.off, b.len, n,
-                     max_units, flag, first_ev);
-  hipLaunchKernelGGL(k_seg_stream, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
-                     flag, first_ev, unit_raw, ev_h, b.tables);
-  hipLaunchKernelGGL(k_seg_scan_units, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, unit_incl,
-                     blk_tot, st);
-  hipLaunchKernelGGL(k_seg_scan_blocks, dim3(1), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, blk_tot, blk_pre, st);
-  hipLaunchKernelGGL(k_seg_scan_final, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_incl, blk_pre,
-                     unit_raw, st);  // G per unit, over the raw words
-  hipLaunchKernelGGL(k_seg_combine, dim3(2 * grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
+  const uint32_t plan_wgs = (uint32_t)(pg < kSegPlanMaxWgs ? pg : kSegPlanMaxWgs);
+  hipLaunchKernelGGL(k_seg_plan, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
+                     first_ev);
+  hipLaunchKernelGGL(k_seg_stream, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
+                     plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
+  hipLaunchKernelGGL(k_seg_combine, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
                      b.crc_out, st, taken);
   return hipGetLastError();
 }

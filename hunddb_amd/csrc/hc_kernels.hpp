@@ -79,8 +79,8 @@ hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 // one stream over their span (k_seg_*, hc_kernels.hip).  max_units bounds the
 // span's 16 KiB units (seg_max_units of a byte bound on the span); ws holds
 // seg_workspace_bytes(n, max_units) bytes.  A batch that is not packed, is
-// larger than the bound or holds records under ~64 B raises ws[0] on the
-// device and writes nothing (k_crc_any's launch then takes it).
+// larger than the bound, holds records under ~64 B or over 16 MiB raises ws[0]
+// on the device and writes nothing (k_crc_grp + k_crc_any then take it).
 uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
 // taken (optional, device word): 1 when the stream took the batch, else 0.

@@ -112,6 +112,22 @@ def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
     check(torch, hc, oracle, host, buf, packed(small, 0), small, True)
 
 
+def test_seg_record_cap(cuda, hc, oracle, seg_all):
+    """k_seg_combine chains the raw CRCs of the whole units a record spans, so
+    the stream takes records up to 16 MiB (1024 units) and a batch with a
+    longer one falls back to k_crc_grp + k_crc_any on the device."""
+    torch = cuda
+    rng = np.random.default_rng(17)
+    total = 40 << 20
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    for big, taken in [((1 << 24), True), ((1 << 24) + 1, False), ((1 << 24) - 3, True)]:
+        lens = np.array([1000] * 300 + [big] + [777, 64, 5000] * 100, dtype=np.uint64)
+        off = packed(lens, 9)
+        assert int(off[-1] + lens[-1]) <= total
+        check(torch, hc, oracle, host, buf, off, lens, taken)
+
+
 def test_seg_without_crc_out(cuda, hc, oracle, seg_all):
     """crc_out is optional (hundcrc.h): a packed whole-message batch with no
     crc_out is not offered to the stream, whose only output is crc_out
@@ -177,3 +193,33 @@ def test_seg_config5b_size(cuda, hc, oracle):
     got3, was3 = run(torch, hc, buf, g, l3)
     assert not was3
     assert (got3[:-1] == got[:-1]).all()
+
+
+def test_seg_workspace_streams(cuda, hc, oracle, seg_all):
+    """On the null stream the workspace is kept across calls and grown there
+    (hc_api.cpp seg_cached_ws); calls on other streams allocate per call.
+    Batches of growing and shrinking size alternate between the null stream and
+    a side stream, each launched without waiting for the other's, and every
+    word is checked."""
+    torch = cuda
+    rng = np.random.default_rng(23)
+    streams = [torch.cuda.default_stream(), torch.cuda.Stream()]
+    assert streams[0].cuda_stream == 0
+    jobs = []
+    for i, n in enumerate([3000, 9000, 2000, 30000, 40000, 5000, 60000, 1000]):
+        lens = rng.integers(64, 6000, n).astype(np.uint64)
+        off = packed(lens, 1 + i)
+        host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 16, dtype=np.uint8)
+        s = streams[i % 2]
+        with torch.cuda.stream(s):
+            buf = torch.from_numpy(host).cuda()
+            doff = torch.from_numpy(off.view(np.int64)).cuda()
+            dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
+            out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            hc.dev_crc32_blocks(buf, out, nblocks=n, off=doff, lens=dlen, flags=hc.HC_F_MESSAGES, stream=s)
+        assert hc.last_launch()["kernel"].startswith("k_seg_stream")
+        jobs.append((host, off, lens, out, buf, doff, dlen))
+    torch.cuda.synchronize()
+    for host, off, lens, out, *_ in jobs:
+        want = oracle.crc32_messages(host, off, lens.astype(np.uint32), threads=16)
+        assert (u32(out) == want).all()
