@@ -1241,8 +1241,8 @@ int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t
   DeviceGuard g(device);
   DeviceState &d = g_dev[device];
   const uint64_t nblk = (n + kPayloadPerBlock - 1) / kPayloadPerBlock;
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)d.cus, (nblk + kFastWaves - 1) / kFastWaves));
-  hc_launch_info info{"k_frame", nblk, 0, n + nblk * HC_BLOCK_SIZE, (uint32_t)grid, kFastThreads, kFastLdsBytes};
+  const int grid = (int)std::min<uint64_t>(nblk > 2 ? (nblk - 2 + 3) / 4 : 0, 0x7FFFFFFF);  // k_frame: one interior block per wave
+  hc_launch_info info{"k_frame", nblk, 0, n + nblk * HC_BLOCK_SIZE, (uint32_t)grid, 256, kLaneQWords * 4};
   t_last = info;
   return launch_frame(static_cast<const uint8_t *>(src), n, static_cast<uint8_t *>(dst), crc_out, d.dtab, grid,
                       static_cast<hipStream_t>(stream)) == hipSuccess
@@ -1263,7 +1263,7 @@ int hc_dev_read_blocks(int device, const void *blocks, uint64_t nblocks, uint32_
   DeviceState &d = g_dev[device];
   const uint64_t per_wg = 4ull * std::max<uint32_t>(1u, kUnframeWaveGroups >> lg);
   hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4),
-                      (uint32_t)std::min<uint64_t>((nblocks + per_wg - 1) / per_wg, 0xFFFFFFFFull), 256, 0};
+                      (uint32_t)std::min<uint64_t>((nblocks + per_wg - 1) / per_wg, 0xFFFFFFFFull), 256, kLaneQWords * 4};
   t_last = info;
   return launch_unframe(static_cast<const uint8_t *>(blocks), nblocks, lg, static_cast<uint8_t *>(payload_out),
                         crc_out, bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), d.dtab,

@@ -64,17 +64,20 @@ struct Gf2 {
   }
 };
 
-// Device constant image (one per device, 12 KiB), uploaded once.
+// Device constant image (one per device, 20 KiB), uploaded once.
 //   tg[k][b]   = shift(b << 8k, kRowBytes)        Horner step across a row
 //   s4[k][b]   = shift(b << 8k, 4)                lane stream combine
 //   lane[l][i] = shift(1 << i, kRowBytes - 12 - 16 l)   lane placement
 //   w0         = shift^-1(0xFFFFFFFF, 4)           Go's init as a prefix word
+//   lane_q[q][l][r] = lane[l][4q + r]              the placement columns regrouped
+//                    for a workgroup-shared LDS copy read by ds_read_b128
 struct DeviceTables {
   uint32_t tg[4][256];
   uint32_t s4[4][256];
   uint32_t lane[kLanes][32];
   uint32_t w0;
   uint32_t pad[63];
+  uint32_t lane_q[8][kLanes][4];
 };
 static_assert(sizeof(DeviceTables) % 256 == 0, "keep the image 256-B multiple");
 
@@ -89,6 +92,9 @@ inline void build_device_tables(DeviceTables &d) {
     for (int i = 0; i < 32; i++) d.lane[l][i] = g.shift_bytes(1u << i, kRowBytes - 12 - 16 * l);
   d.w0 = g.unshift4(0xFFFFFFFFu);
   for (auto &p : d.pad) p = 0;
+  for (int q = 0; q < 8; q++)
+    for (uint32_t l = 0; l < kLanes; l++)
+      for (int r = 0; r < 4; r++) d.lane_q[q][l][r] = d.lane[l][4 * q + r];
 }
 
 // 32x32 GF(2) matrix by columns: c[i] = M e_i (host side only).

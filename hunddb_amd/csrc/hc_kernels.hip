@@ -1027,140 +1027,6 @@ __device__ __forceinline__ void frame_edge_rows(uint64_t b, const uint8_t *__res
   }
 }
 
-// Each row is stored before it is hashed (the other orders: +-0.6 %).
-__global__ __launch_bounds__(kFastThreads) void k_frame(const uint8_t *__restrict__ src, uint64_t n,
-                                                         uint8_t *__restrict__ dst, uint64_t nblk, uint32_t lg_chunk,
-                                                         uint32_t *__restrict__ crc_out,
-                                                         const DeviceTables *__restrict__ tables) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
-  __shared__ uint32_t s_next;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) s_next = 2 * kFastWaves;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
-  uint32_t col[32];
-#pragma unroll
-  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  const uint32_t w0 = tables->w0;
-  __syncthreads();
-  const uint32_t r4 = (lane & 31u) << 2;
-  const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
-  const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
-  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t {
-    const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(c, B0, 0x0c020400u));
-    const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(c, B1, 0x0c020500u));
-    const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(c, B2, 0x0c020600u));
-    const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(c, B3, 0x0c020700u));
-    return xor3(xor3(t0, t1, t2), t3, w);
-  };
-  auto shift4 = [&](uint32_t x, uint32_t w) -> uint32_t {
-    const uint32_t t0 = lds_u32(lds, S4base + ((x & 255u) << 4));
-    const uint32_t t1 = lds_u32(lds, S4base + 4096u + (((x >> 8) & 255u) << 4));
-    const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
-    const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
-    return xor3(xor3(t0, t1, t2), t3, w);
-  };
-  constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef u32x4 u32x4_u __attribute__((aligned(1)));
-  const uint32_t wave = uni(tid >> 6);
-  const uint64_t gw = (uint64_t)blockIdx.x * kFastWaves + wave;
-  const uint64_t W = (uint64_t)gridDim.x * kFastWaves;
-
-  // CRC of one framed block from its 4 rows (lane 0's row-0 word 0 = W0) and the
-  // store of lane 0's first 16 bytes with the CRC in front.
-  auto finish = [&](uint64_t b, const uint32_t (&c)[4], uint4 keep) {
-    const uint32_t dd = shift4(shift4(shift4(c[0], c[1]), c[2]), c[3]);
-    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
-    if (lane == 0) {
-      keep.x = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
-      *reinterpret_cast<uint4 *>(dst + b * (uint64_t)HC_FRAME_BLOCK) = keep;
-      if (crc_out) crc_out[b] = crcv;
-    }
-  };
-
-  auto edge_block = [&](uint64_t b) {
-    uint32_t c[4];
-    uint4 keep;
-    frame_edge_rows(b, src, n, dst, lane, w0, row_step, c, keep);
-    finish(b, c, keep);
-  };
-
-  if (gw == 0) edge_block(0);
-  if (nblk > 1 && gw == (W > 1 ? 1 : 0)) edge_block(nblk - 1);
-
-  // Interior blocks 1 .. nblk-2: every row window [S0 + 1024r + 16l, +16) lies
-  // inside src, so each lane reads its 16 output bytes with ONE unaligned
-  // 16-byte load (gfx950 runs in unaligned-access mode) -- no funnel, no
-  // masks -- and the next block's 4 rows are in flight while this one is hashed.
-  // Interior index i (block i + 1) of the workgroup's k-th hand-out:
-  const uint64_t ni = nblk > 2 ? nblk - 2 : 0;
-  const uint64_t G = gridDim.x, wg = blockIdx.x;
-  const uint32_t cmask = (1u << lg_chunk) - 1u;
-  auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };
-  uint64_t c = blk_of(wave);
-  if (c >= ni) return;
-  uint64_t n1 = blk_of(kFastWaves + wave);
-  uint32_t knv = 0;  // LDS hand-out result for the block after n1, read one block later
-  if (lane == 0) knv = atomicAdd(&s_next, 1u);
-  auto load4 = [&](uint64_t i, u32x4 (&v)[4]) {
-    const uint8_t *S = src + (i + 1) * kPay - 4 + 16u * lane;
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-      v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * kRowBytes));
-  };
-  auto frame = [&](uint64_t i, const u32x4 (&cur)[4]) {
-    const uint64_t b = i + 1;
-    uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
-    uint32_t cc[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      u32x4 v = cur[r];
-      // every lane stores (no divergent branch between the loads and their
-      // use); lane 0 writes zeros to bytes 0..3 and the CRC over them below
-      if (r == 0) v.x = lane == 0 ? 0u : v.x;
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      u32x4 v = cur[r];
-      if (r == 0) v.x = lane == 0 ? w0 : v.x;  // Go's init in place of the CRC field
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 4; k++) cc[k] = r == 0 ? w[k] : row_step(cc[k], w[k]);
-    }
-    const uint32_t dd = shift4(shift4(shift4(cc[0], cc[1]), cc[2]), cc[3]);
-    const uint32_t crcv = wave_xor(matvec32(col, dd)) ^ 0xFFFFFFFFu;
-    // binary.LittleEndian.PutUint32(block[:4], crc): lane 0's ob is the block start
-    lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);
-    if (crc_out) lane0_store_u32(crc_out + b, crcv);
-  };
-  auto nextb = [&]() {  // the next hand-out (requested one block earlier)
-    const uint64_t r = blk_of(uni(knv));
-    if (lane == 0) knv = atomicAdd(&s_next, 1u);
-    return r;
-  };
-  // Register sets with rotating roles (no copies that would wait on the
-  // prefetch); unconditional loads: past the end a wave re-reads a block it
-  // holds.  The first block is peeled so that the loop header is entered with
-  // the same VMEM sequence from both edges ([next rows loaded][4 row stores]);
-  // a mismatch there makes the waitcnt pass wait for the stores as well.
-  u32x4 A[4], B[4];
-  load4(c, A);
-  load4(n1 < ni ? n1 : c, B);
-  frame(c, A);
-  while (n1 < ni) {
-    c = n1;
-    n1 = nextb();
-    load4(n1 < ni ? n1 : c, A);
-    frame(c, B);
-    if (n1 >= ni) break;
-    c = n1;
-    n1 = nextb();
-    load4(n1 < ni ? n1 : c, B);
-    frame(c, A);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // The row step without LDS (k_unframe): a 32x32 GF(2) mat-vec M.c is the XOR
 // of five 64-entry tables T_j[6-bit chunk j of c] (bits 0..29) and the two
@@ -1204,21 +1070,142 @@ __device__ __forceinline__ uint32_t xapply(const XTab &T, uint32_t c, uint32_t w
   return xor3(xor3(g[0], g[1], g[2]), g[3], xor3(g[4], a, 0u));
 }
 
+// The lane placement's 32 columns shared by a 4-wave workgroup: one 8 KiB LDS
+// copy of DeviceTables::lane_q (every load issued before the first store), read
+// back with 8 ds_read_b128 per placement (lane l's 16 B of each quarter are
+// consecutive: no bank conflicts).  Loading the 128 B of columns per lane from
+// L2 instead (8 KiB per wave) held the framing kernels at one block per wave
+// to 4.56 TB/s; shared, one block per wave is the fastest geometry
+// (tools/kframe3, profiles/r3/framing_lq/).
+__device__ __forceinline__ void fill_lane_q(uint32_t *lq, const DeviceTables *__restrict__ tables) {
+  constexpr uint32_t kQ = kLaneQWords / 4, kPer = kQ / 256;  // uint4s; per thread of 256
+  static_assert(kQ % 256 == 0, "lane_q copy: whole uint4s per thread");
+  const uint4 *g = reinterpret_cast<const uint4 *>(&tables->lane_q[0][0][0]);
+  uint4 t[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) t[k] = g[threadIdx.x + k * 256u];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) reinterpret_cast<uint4 *>(lq)[threadIdx.x + k * 256u] = t[k];
+}
+// the 32x32 mat-vec of lane `lane`'s placement matrix with d (matvec32 against LDS columns)
+__device__ __forceinline__ uint32_t place_lq(const uint32_t *lq, uint32_t lane, uint32_t d) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 c4 = reinterpret_cast<const uint4 *>(lq)[q * kLanes + lane];
+    const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t m = (uint32_t)((int32_t)(d << (31 - (4 * q + r))) >> 31);  // bit 4q+r of d, spread
+      acc = __builtin_amdgcn_bitop3_b32(m, cq[r], acc, 0x6A);                   // (m & col) ^ acc
+    }
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Fused AddCRCsToData (utils/crc/crc_util.go:41-64, row f2): payload slices of
+// 4092 B -> 4096-B blocks with the CRC in front, one read of the payload and
+// one write of the blocks.  Two launches (launch_frame):
+//   k_frame_edges  the first block (row 0 would start 4 bytes before src) and
+//                  the last (ragged payload): aligned, range-predicated loads,
+//                  funnel shift and byte masks, one wave each -- no byte
+//                  outside src is touched.
+//   k_frame        interior blocks 1 .. nblk-2: every row window lies inside
+//                  src, so each lane reads its 16 output bytes with ONE
+//                  unaligned 16-byte load (gfx950 runs in unaligned-access
+//                  mode).  One block per wave, 4-wave workgroups that exit:
+//                  row steps and the stream combine through XTab (no LDS
+//                  tables to fill), the lane placement against the
+//                  workgroup's LDS copy of its columns.  The row stores go out
+//                  before the hash (the other orders within +-0.5 %).
+// Round 2's kernel (persistent 16-wave workgroups, 144 KiB of LDS tables)
+// ran 5.10-5.24 TB/s; this one 5.26-5.48 on the same boxes (tools/kframe3).
+__global__ __launch_bounds__(128) void k_frame_edges(const uint8_t *__restrict__ src, uint64_t n,
+                                                     uint8_t *__restrict__ dst, uint64_t nblk,
+                                                     uint32_t *__restrict__ crc_out,
+                                                     const DeviceTables *__restrict__ tables) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (wv == 1 && nblk < 2) return;
+  const uint64_t b = wv == 0 ? 0 : nblk - 1;
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  const XTab TM = make_xtab(tables->tg, lane);
+  const XTab TS = make_xtab(tables->s4, lane);
+  auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t { return xapply(TM, c, w); };
+  uint32_t c[4];
+  uint4 keep;
+  frame_edge_rows(b, src, n, dst, lane, tables->w0, row_step, c, keep);
+  const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
+  const uint32_t crcv = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+  if (lane == 0) {
+    keep.x = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
+    *reinterpret_cast<uint4 *>(dst + b * (uint64_t)HC_FRAME_BLOCK) = keep;
+    if (crc_out) crc_out[b] = crcv;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                               uint64_t nblk, uint32_t *__restrict__ crc_out,
+                                               const DeviceTables *__restrict__ tables) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
+  __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // interior block
+  const bool mine = b + 1 < nblk;
+  u32x4 v[4];
+  if (mine) {  // the block's rows first: the table work below overlaps their latency
+    const uint8_t *S = src + b * kPay - 4 + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * kRowBytes));
+  }
+  fill_lane_q(lq, tables);
+  const XTab TM = make_xtab(tables->tg, lane);
+  const XTab TS = make_xtab(tables->s4, lane);
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+  if (!mine) return;
+  uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {  // lane 0 writes zeros to bytes 0..3 and the CRC over them below
+    u32x4 t = v[r];
+    if (r == 0) t.x = lane == 0 ? 0u : t.x;
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
+  }
+  uint32_t c[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    u32x4 t = v[r];
+    if (r == 0) t.x = lane == 0 ? w0 : t.x;  // Go's init in place of the CRC field
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : xapply(TM, c[k], w[k]);
+  }
+  const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
+  const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
+  lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);  // lane 0's ob is the block start
+  if (crc_out) lane0_store_u32(crc_out + b, crcv);
+}
+
 // ---------------------------------------------------------------------------
 // Batched ReadFromDisk on device (lsm/block_manager/block_manager.go:203-235,
 // row f1): verify every block of a contiguous run (CheckBlockIntegrity,
 // crc_util.go:88-100) and strip the CRC words, writing the payloads back to
 // back (block b's block[4:B] at out + b*(B-4)) -- the inverse of k_frame, one
 // read of the blocks and one write of the payload.  B = 4096 << lg_groups.
-//   * 4-wave workgroups, each wave kUnframeWaveGroups (hc_kernels.hpp) 4 KiB groups (K = 4 blocks
-//     of 4 KiB, 2 of 8 KiB, 1 of 16 KiB) in order, the next group's rows in
-//     flight while the current one is hashed and stored, then exit.  The
-//     persistent 16-wave version with 144 KiB of LDS tables ran 5.0-5.2 TB/s;
-//     this one 5.45-5.57 (tools/kframe3, profiles/r3/framing/: +5-8 % on two
-//     boxes), at the copy rate of the same geometry.
+//   * 4-wave workgroups, each wave one block (kUnframeWaveGroups = 1 in
+//     hc_kernels.hpp: 1, 2 or 4 groups of 4 KiB) in order, the next group's
+//     rows in flight while the current one is hashed and stored, then exit.
+//     The persistent 16-wave version with 144 KiB of LDS tables ran 5.0-5.2
+//     TB/s; four blocks per wave with the placement columns loaded per lane
+//     5.45-5.62; one block per wave with them shared in LDS 6.04
+//     (tools/kframe3, profiles/r3/framing/, profiles/r3/framing_lq/).
 //   * Row steps and the stream combine through XTab (ds_bpermute); the lane
-//     placement is the 32x32 mat-vec on the VALU against the lane's 32
-//     columns of the constant image.
+//     placement is the 32x32 mat-vec against the workgroup's LDS copy of its
+//     columns (place_lq).
 //   * Payload stores are 16-B unaligned stores (output is shifted 4 bytes per
 //     block); lane 0 of a block's first row stores bytes 4..19 instead (lane
 //     1's first word via DPP), overlapping lane 1's store with identical bytes.
@@ -1237,9 +1224,9 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blo
   constexpr uint32_t kGroups = 1u << lg_groups, gmask = kGroups - 1u;
   constexpr uint32_t K = kUnframeWaveGroups >> lg_groups > 0 ? kUnframeWaveGroups >> lg_groups : 1u;  // blocks per wave
   constexpr uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
+  __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * K;
-  if (b0 >= nblk) return;
   const uint64_t p_end = (b0 + K < nblk ? b0 + K : nblk) << lg_groups;  // this wave's groups [p0, p_end)
   uint64_t p = b0 << lg_groups;
   const uint32_t w0 = tables->w0;
@@ -1249,12 +1236,11 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blo
 #pragma unroll
     for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
   };
-  load4(p);
-  uint32_t col[32];
-#pragma unroll
-  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  if (p < p_end) load4(p);  // the first group's rows before the table work
+  fill_lane_q(lq, tables);
   const XTab TM = make_xtab(tables->tg, lane);
   const XTab TS = make_xtab(tables->s4, lane);
+  __syncthreads();
   uint32_t c[4] = {0, 0, 0, 0};
   uint32_t stored = 0;
   bool reported = false;  // wave-uniform: this wave already lowered first_bad
@@ -1262,7 +1248,7 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blo
     const uint64_t b = p >> lg_groups;
     const uint32_t g = (uint32_t)p & gmask;
     u32x4 cur[4] = {v[0], v[1], v[2], v[3]};
-    if (p + 1 < p_end) load4(p + 1);  // the next group in flight
+    if ((K << lg_groups) > 1 && p + 1 < p_end) load4(p + 1);  // the next group in flight (none: one group a wave)
     uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
     u32x4 sv[4];
     uint8_t *sa[4];
@@ -1288,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blo
     for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
     if (g == gmask) {
       const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
-      const uint32_t crcv = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+      const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
       if (crc_out) lane0_store_u32(crc_out + b, crcv);
       if (first_bad && crcv != stored) {  // wave-uniform
         if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
@@ -1789,9 +1775,12 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
                         const DeviceTables *tables, int grid, hipStream_t s) {
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
-  const uint64_t ni = nblk > 2 ? nblk - 2 : 1;
-  hipLaunchKernelGGL(k_frame, dim3(grid), dim3(kFastThreads), 0, s, src, n, dst, nblk, grp_lg_chunk(ni, grid, 4096), crc_out,
-                     tables);
+  hipLaunchKernelGGL(k_frame_edges, dim3(1), dim3(128), 0, s, src, n, dst, nblk, crc_out, tables);
+  if (nblk > 2) {
+    const uint64_t wgs = (nblk - 2 + 3) / 4;  // one interior block per wave
+    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, dst, nblk, crc_out, tables);
+  }
   return hipGetLastError();
 }
 

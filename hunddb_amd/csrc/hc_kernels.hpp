@@ -53,11 +53,13 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
 bool grp_xcd(uint32_t block_bytes, int grid, uint64_t nblocks);
 uint32_t grp_lg_chunk(uint64_t nblocks, int grid, uint32_t block_bytes);
 hipError_t launch_grp(const Batch &b, int grid, hipStream_t s);
-// Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B blocks.
+// Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B
+// blocks (k_frame_edges + k_frame; `grid` is unused: one interior block per wave).
 constexpr uint32_t HC_FRAME_BLOCK = 4096;
 hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
                         const DeviceTables *tables, int grid, hipStream_t s);
-constexpr uint32_t kUnframeWaveGroups = 4;  // k_unframe: 4 KiB groups per wave (16 KiB)
+constexpr uint32_t kLaneQWords = 8 * kLanes * 4;  // k_frame / k_unframe: LDS copy of DeviceTables::lane_q
+constexpr uint32_t kUnframeWaveGroups = 1;  // k_unframe: 4 KiB groups per wave, at least one block
 // Batched ReadFromDisk: verify nblk blocks of 4096 << lg_groups bytes at `blocks`
 // (16-B aligned) and write their payloads back to back at `out`.  Its own grid
 // (4-wave workgroups, 16 KiB of blocks per wave).

@@ -176,6 +176,10 @@ def test_debug_tables_consistent(hc):
     t = hc.debug_tables()
     tg, s4 = t[0:1024].reshape(4, 256), t[1024:2048].reshape(4, 256)
     lane, w0 = t[2048:4096].reshape(64, 32), int(t[4096])
+    # the placement columns regrouped for the workgroup-shared LDS copy (k_frame, k_unframe)
+    lane_q = t[4160:4160 + 2048].reshape(8, 64, 4)
+    assert t.size == 4160 + 2048
+    assert (lane_q.transpose(1, 0, 2).reshape(64, 32) == lane).all()
 
     def tab(T, c):
         return T[0][c & 255] ^ T[1][(c >> 8) & 255] ^ T[2][(c >> 16) & 255] ^ T[3][c >> 24]

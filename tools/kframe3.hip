@@ -48,6 +48,11 @@ using hc::HC_FRAME_BLOCK;
 constexpr int kMats = 8;  // 0: row step, 1: S4, 2..7: T_0..T_5
 struct XbCols {
   uint32_t col[kMats][32];
+  // the lane placement's per-lane columns (DeviceTables::lane) regrouped for a
+  // workgroup-shared LDS copy read by ds_read_b128: lq[q][l][r] = lane[l][4q + r]
+  uint32_t lq[8][64][4];
+  // Tab5 contents of the row step (0) and shift(., 4) (1): tq[m][j][v] = T_j[v]
+  uint32_t tq[2][5][64];
 };
 
 inline void build_cols(XbCols &x) {
@@ -55,6 +60,19 @@ inline void build_cols(XbCols &x) {
   const uint64_t n[kMats] = {1024, 4, 16, 32, 64, 128, 256, 512};
   for (int m = 0; m < kMats; m++)
     for (int i = 0; i < 32; i++) x.col[m][i] = g.shift_bytes(1u << i, n[m]);
+  hc::DeviceTables h;
+  hc::build_device_tables(h);
+  for (int q = 0; q < 8; q++)
+    for (int l = 0; l < 64; l++)
+      for (int r = 0; r < 4; r++) x.lq[q][l][r] = h.lane[l][4 * q + r];
+  for (int m = 0; m < 2; m++)
+    for (int j = 0; j < 5; j++)
+      for (uint32_t v = 0; v < 64; v++) {
+        uint32_t e = 0;
+        for (int b = 0; b < 6; b++)
+          if ((v >> b) & 1u) e ^= x.col[m][6 * j + b];
+        x.tq[m][j][v] = e;
+      }
 }
 
 __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
@@ -260,6 +278,218 @@ __global__ __attribute__((amdgpu_waves_per_eu(kOcc))) __launch_bounds__(kW * 64)
     const uint32_t crc = hc::wave_xor(hc::matvec32(col, d)) ^ 0xFFFFFFFFu;
     hc::lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crc);
     if (crc_out) hc::lane0_store_u32(crc_out + b, crc);
+  }
+}
+
+// k_frame_xi with the lane placement's columns shared by the workgroup in LDS
+// (8 KiB copied once per workgroup, read with 8 ds_read_b128 per block) instead
+// of 128 B loaded per lane: per-wave setup drops to the two Tab5 builds, so
+// short-lived waves (K = 1-2 blocks) no longer pay 8 KiB of L2 reads per 8 KiB
+// of HBM traffic.
+template <int K, int kW, int kOrd = 2, bool kTabLds = false>
+__global__ __launch_bounds__(kW * 64) void k_frame_xl(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                      uint64_t nblk, uint32_t *__restrict__ crc_out,
+                                                      const XbCols *__restrict__ xc,
+                                                      const hc::DeviceTables *__restrict__ tables) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  constexpr uint64_t kPay = 4092;
+  __shared__ __attribute__((aligned(16))) uint32_t lc[8 * 64 * 4 + (kTabLds ? 2 * 5 * 64 : 0)];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = 1 + ((uint64_t)blockIdx.x * kW + (threadIdx.x >> 6)) * K;
+  const uint64_t bend = nblk - 1;
+  u32x4 v[4];
+  auto load4 = [&](uint64_t b) {
+    const uint8_t *S = src + b * kPay - 4 + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * hc::kRowBytes));
+  };
+  if (b0 < bend) load4(b0);
+  {  // lq (8 KiB) and, with kTabLds, tq (2.5 KiB) are contiguous in XbCols
+    constexpr int kQ = kTabLds ? 512 + 160 : 512, kT = kW * 64, kPer = (kQ + kT - 1) / kT;
+    const uint4 *g = reinterpret_cast<const uint4 *>(&xc->lq[0][0][0]);
+    uint4 t[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (threadIdx.x + k * kT < kQ) t[k] = g[threadIdx.x + k * kT];
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (threadIdx.x + k * kT < kQ) reinterpret_cast<uint4 *>(lc)[threadIdx.x + k * kT] = t[k];
+  }
+  Tab5 TM, TS;
+  if (!kTabLds) {
+    uint32_t msk[6];
+#pragma unroll
+    for (int b = 0; b < 6; b++) msk[b] = 0u - ((lane >> b) & 1u);
+    TM = make_tab5(xc->col[0], msk);
+    TS = make_tab5(xc->col[1], msk);
+  } else {
+    TM.c30 = xc->col[0][30];
+    TM.c31 = xc->col[0][31];
+    TS.c30 = xc->col[1][30];
+    TS.c31 = xc->col[1][31];
+  }
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+  if (kTabLds) {
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      TM.t[j] = lc[2048 + j * 64 + lane];
+      TS.t[j] = lc[2048 + 320 + j * 64 + lane];
+    }
+  }
+  if (b0 >= bend) return;
+  auto place = [&](uint32_t d) -> uint32_t {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint4 c4 = reinterpret_cast<const uint4 *>(lc)[q * 64 + lane];
+      const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t m = (uint32_t)((int32_t)(d << (31 - (4 * q + r))) >> 31);
+        acc = __builtin_amdgcn_bitop3_b32(m, cq[r], acc, 0x6A);  // (m & c) ^ acc
+      }
+    }
+    return acc;
+  };
+  for (int k = 0; k < K; k++) {
+    const uint64_t b = b0 + k;
+    if (b >= bend) break;
+    uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+    auto stores = [&](const u32x4 (&src4)[4]) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        u32x4 t = src4[r];
+        if (r == 0) t.x = lane == 0 ? 0u : t.x;
+        __builtin_nontemporal_store(t, reinterpret_cast<u32x4 *>(ob + r * hc::kRowBytes));
+      }
+    };
+    if (kOrd == 0) stores(v);
+    u32x4 cur[4] = {v[0], v[1], v[2], v[3]};
+    if (k + 1 < K && b + 1 < bend) load4(b + 1);
+    if (kOrd == 1) stores(cur);
+    uint32_t c[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 t = cur[r];
+      if (r == 0) t.x = lane == 0 ? w0 : t.x;
+      const uint32_t wd[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) c[q] = r == 0 ? wd[q] : apply5(TM, c[q], wd[q]);
+    }
+    if (kOrd == 2) stores(cur);
+    const uint32_t d = apply5(TS, apply5(TS, apply5(TS, c[0], c[1]), c[2]), c[3]);
+    const uint32_t crc = hc::wave_xor(place(d)) ^ 0xFFFFFFFFu;
+    hc::lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crc);
+    if (crc_out) hc::lane0_store_u32(crc_out + b, crc);
+  }
+}
+
+// The production k_unframe (4 KiB blocks) with the lane placement's columns
+// shared by the workgroup in LDS (as k_frame_xl) and K blocks per wave.
+template <int K, int kW, bool kStoreFirst = false>
+__global__ __launch_bounds__(kW * 64) void k_unframe_xl(const uint8_t *__restrict__ blocks, uint64_t nblk,
+                                                        uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
+                                                        uint32_t *__restrict__ bad_bitmap,
+                                                        unsigned long long *__restrict__ first_bad,
+                                                        const XbCols *__restrict__ xc,
+                                                        const hc::DeviceTables *__restrict__ tables) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  constexpr uint64_t B = HC_FRAME_BLOCK, Bp = B - 4;
+  __shared__ __attribute__((aligned(16))) uint32_t lc[8 * 64 * 4];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = ((uint64_t)blockIdx.x * kW + (threadIdx.x >> 6)) * K;
+  const uint64_t p_end = b0 + K < nblk ? b0 + K : nblk;
+  uint64_t p = b0;
+  const uint32_t w0 = tables->w0;
+  u32x4 v[4];
+  auto load4 = [&](uint64_t q) {
+    const uint8_t *S = blocks + q * HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * hc::kRowBytes));
+  };
+  if (p < p_end) load4(p);
+  {
+    constexpr int kT = kW * 64, kPer = 512 / kT;
+    const uint4 *g = reinterpret_cast<const uint4 *>(&xc->lq[0][0][0]);
+    uint4 t[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) t[k] = g[threadIdx.x + k * kT];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) reinterpret_cast<uint4 *>(lc)[threadIdx.x + k * kT] = t[k];
+  }
+  const hc::XTab TM = hc::make_xtab(tables->tg, lane);
+  const hc::XTab TS = hc::make_xtab(tables->s4, lane);
+  __syncthreads();
+  auto place = [&](uint32_t d) -> uint32_t {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint4 c4 = reinterpret_cast<const uint4 *>(lc)[q * 64 + lane];
+      const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t m = (uint32_t)((int32_t)(d << (31 - (4 * q + r))) >> 31);
+        acc = __builtin_amdgcn_bitop3_b32(m, cq[r], acc, 0x6A);
+      }
+    }
+    return acc;
+  };
+  bool reported = false;
+  for (; p < p_end; p++) {
+    const uint64_t b = p;
+    u32x4 cur[4] = {v[0], v[1], v[2], v[3]};
+    if (K > 1 && p + 1 < p_end) load4(p + 1);
+    uint8_t *ob = out + b * Bp + 16u * lane - 4;
+    u32x4 sv[4];
+    uint8_t *sa[4];
+    uint32_t c[4], stored = 0;
+    if (kStoreFirst) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const u32x4 t = cur[r];
+        if (r == 0) {
+          const uint32_t nx = __builtin_amdgcn_update_dpp(0u, t.x, 0x101, 0xF, 0xF, false);
+          const u32x4 first = {t.y, t.z, t.w, nx};
+          __builtin_nontemporal_store(lane == 0 ? first : t, reinterpret_cast<u32x4_u *>(ob + (lane == 0 ? 4 : 0)));
+        } else {
+          __builtin_nontemporal_store(t, reinterpret_cast<u32x4_u *>(ob + r * hc::kRowBytes));
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 t = cur[r];
+      if (r == 0) {
+        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, t.x, 0x101, 0xF, 0xF, false);
+        stored = __builtin_amdgcn_readfirstlane(t.x);
+        const u32x4 first = {t.y, t.z, t.w, nx};
+        sv[r] = lane == 0 ? first : t;
+        sa[r] = ob + (lane == 0 ? 4 : 0);
+        t.x = lane == 0 ? w0 : t.x;
+      } else {
+        sv[r] = t;
+        sa[r] = ob + r * hc::kRowBytes;
+      }
+      const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : hc::xapply(TM, c[k], w[k]);
+    }
+    if (!kStoreFirst) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
+    }
+    const uint32_t d = hc::xapply(TS, hc::xapply(TS, hc::xapply(TS, c[0], c[1]), c[2]), c[3]);
+    const uint32_t crcv = hc::wave_xor(place(d)) ^ 0xFFFFFFFFu;
+    if (crc_out) hc::lane0_store_u32(crc_out + b, crcv);
+    if (first_bad && crcv != stored) {
+      if (bad_bitmap) hc::lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+      if (!reported && b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        hc::lane0_atomic_umin64(first_bad, b);
+      reported = true;
+    }
   }
 }
 
@@ -659,6 +889,37 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((xb::k_frame_xi<K, W __VA_OPT__(,) __VA_ARGS__>), dim3((unsigned)g_), dim3((W) * 64), 0, st, src, framed, nblk, crc, xc, \
                        dt);                                                                                         \
   }
+#define XL(K, W, ...)                                                                                                \
+  [&](hipStream_t st) {                                                                                             \
+    hipLaunchKernelGGL(xb::k_frame_edges_xh, dim3(1), dim3(128), 0, st, src, npay, framed, nblk, crc, xc, dt);        \
+    const uint64_t g_ = (nblk - 2 + (W) * (K)-1) / ((W) * (K));                                                      \
+    hipLaunchKernelGGL((xb::k_frame_xl<K, W __VA_OPT__(,) __VA_ARGS__>), dim3((unsigned)g_), dim3((W) * 64), 0, st, src, framed, nblk, crc, xc, \
+                       dt);                                                                                         \
+  }
+#define XLU(K, W, ...)                                                                                               \
+  [&](hipStream_t st) {                                                                                             \
+    const uint64_t g_ = (nblk + (W) * (K)-1) / ((W) * (K));                                                          \
+    hipLaunchKernelGGL((xb::k_unframe_xl<K, W __VA_OPT__(,) __VA_ARGS__>), dim3((unsigned)g_), dim3((W) * 64), 0, st, blocks, nblk, pay, crc,   \
+                       bitmap, fb, xc, dt);                                                                          \
+  }
+  const char *only = std::getenv("KF3_SET");  // "xl": the LDS-shared placement study only
+  if (only && std::string(only) == "xl") {
+    vs.push_back({"PROD k_frame (persistent, LDS tables)", 0, true, prod_frame, {}});
+    vs.push_back({"hybrid frame interior K=4 W=4 ld,hash,st", 0, true, XI(4, 4, 1, 2), {}});
+    vs.push_back({"LDS-cols frame K=1 W=4", 0, true, XL(1, 4), {}});
+    vs.push_back({"LDS-cols frame K=1 W=4 st,ld,hash", 0, true, XL(1, 4, 0), {}});
+    vs.push_back({"edges only (2 blocks, 1 WG)", 0, false, [&](hipStream_t st) {
+                    hipLaunchKernelGGL(xb::k_frame_edges_xh, dim3(1), dim3(128), 0, st, src, npay, framed, nblk, crc, xc, dt);
+                  }, {}});
+    vs.push_back({"NULL np frame K=1 (memory pattern)", 0, false, XBN(1), {}});
+    vs.push_back({"PROD k_frame (again)", 0, true, prod_frame, {}});
+    vs.push_back({"PROD k_unframe", 1, true, prod_unframe, {}});
+    vs.push_back({"LDS-cols unframe K=1 W=4", 1, true, XLU(1, 4), {}});
+    vs.push_back({"LDS-cols unframe K=1 W=4 stores first", 1, true, XLU(1, 4, true), {}});
+    vs.push_back({"LDS-cols unframe K=1 W=8 stores first", 1, true, XLU(1, 8, true), {}});
+    vs.push_back({"LDS-cols unframe K=4 W=4", 1, true, XLU(4, 4), {}});
+    vs.push_back({"PROD k_unframe (again)", 1, true, prod_unframe, {}});
+  } else {
   vs.push_back({"PROD k_frame (persistent, LDS tables)", 0, true, prod_frame, {}});
   vs.push_back({"hybrid frame interior K=4 W=4 st,ld,hash", 0, true, XI(4, 4), {}});
   vs.push_back({"hybrid frame interior K=4 W=4 ld,st,hash", 0, true, XI(4, 4, 1, 1), {}});
@@ -673,6 +934,7 @@ int main(int argc, char **argv) {
   vs.push_back({"hybrid unframe K=4 W=8", 1, true, XHU(4, 8), {}});
   vs.push_back({"PROD k_frame (again)", 0, true, prod_frame, {}});
   vs.push_back({"PROD k_unframe (round 3, again)", 1, true, prod_unframe, {}});
+  }
 
   // reference outputs: production frame, production unframe (words, bytes, bitmap, first bad)
   std::vector<uint32_t> cref_f(N), cref_u(N), got(N), bm_ref((N + 31) / 32), bm(bm_ref.size());
