@@ -1,0 +1,110 @@
+"""BASELINE.json configs[4] (config 5) at its full size: 10M WAL records of
+64 B - 64 KiB (log-uniform), framed into 4 KiB blocks exactly as
+lsm/wal/wal.go:177-283 (tools/walgen.c, byte-identical to the oracle's
+framing: tests/test_walgen.py).  That is 26.3M blocks, 100 GiB in host memory,
+the blocks starting where the WAL segment files put them.
+
+- Every block's CRC word through the host-resident entry (hc_crc32_blocks:
+  pageable image, staged over PCIe) against the oracle's restatement of
+  crc_util.go's arithmetic on all 26.3M blocks, and against the word the
+  writer stamped.
+- The batched CheckBlockIntegrity (hc_verify_blocks, recoverMemtable's
+  per-block check, wal.go:383) over the whole image: clean, then with one
+  corrupted block found at its index with the reference's error text.
+- The per-record variant on the device: GetCRC of all 10M records packed back
+  to back in HBM (the packed-record stream), against the oracle on a sample and
+  word for word against k_crc_any.
+
+Host memory: ~108 GB (one image); the box allows ~270 GiB per command."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NREC = 10_000_000
+SEED = 0x57414C
+
+
+def _walgen():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import walgen
+    return walgen
+
+
+def test_config5_wal_blocks_full_size(cuda, hc, oracle):
+    walgen = _walgen()
+    plan = walgen.WalPlan(SEED, nrec=NREC)
+    nb = plan.nblocks
+    assert nb > 26_000_000
+    host = np.empty(nb * 4096, dtype=np.uint8)
+    step = 1 << 18
+    for b0 in range(0, nb, step):
+        b1 = min(nb, b0 + step)
+        plan.render(b0, b1, out=host[b0 * 4096:b1 * 4096], threads=16)
+    try:
+        got = hc.crc32_blocks(host, stride=4096, ulen=4096, nblocks=nb)
+        want = oracle.crc32_blocks(host, stride=4096, ulen=4096, nblocks=nb, threads=16)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, bad[:8]
+        stamped = host.reshape(nb, 4096)[:, :4].copy().view("<u4").reshape(-1)
+        assert np.array_equal(stamped, want), "the writer's stamped words differ from the oracle's"
+        err, bm, fb = hc.verify_blocks(host, stride=4096, ulen=4096, nblocks=nb)
+        assert err is None and fb == -1 and not bm.any()
+        victim = (2 * nb) // 3 + 1
+        host[victim * 4096 + 2000] ^= 0x10
+        err, bm, fb = hc.verify_blocks(host, stride=4096, ulen=4096, nblocks=nb)
+        host[victim * 4096 + 2000] ^= 0x10
+        assert str(err) == "CRC mismatch in block" and fb == victim
+        assert int(np.unpackbits(bm.view(np.uint8)).sum()) == 1 and (bm[victim >> 5] >> (victim & 31)) & 1
+    finally:
+        del host
+
+
+def test_config5_records_full_size_on_device(cuda, hc, oracle):
+    torch = cuda
+    walgen = _walgen()
+    sizes = np.zeros(NREC, dtype=np.uint32)
+    walgen.lib().wg_record_sizes(SEED, NREC, 64, 65536, sizes.ctypes.data)
+    off = np.zeros(NREC, dtype=np.uint64)
+    off[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    off += np.uint64(3)  # back to back from an odd address
+    total = (int(off[-1]) + int(sizes[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
+    assert total > 90e9
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    hc.dev_fill_range(buf, 0x5C, 0, total >> 20, stride=1 << 20, ulen=1 << 20)  # every byte, in 1 MiB blocks
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(sizes.view(np.int32)).cuda()
+    out = torch.empty(NREC, dtype=torch.int32, device="cuda")
+    hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=NREC, flags=hc.HC_F_MESSAGES)
+    torch.cuda.synchronize()
+    assert hc.seg_taken(), "10M packed records should take the packed-record stream"
+    got = out.cpu().numpy().view(np.uint32).copy()
+    # the oracle on 20k records of the first 1 GB (every one of the first 300) and on the last 300
+    rng = np.random.default_rng(5)
+    head = int(np.searchsorted(off, 1 << 30))
+    pick = np.unique(np.r_[np.arange(300), rng.choice(head, 20_000, replace=False)])
+    hi = int((off[pick] + sizes[pick]).max())
+    want = oracle.crc32_messages(buf[:hi].cpu().numpy(), off[pick], sizes[pick], threads=16)
+    assert np.array_equal(got[pick], want)
+    tail = np.arange(NREC - 300, NREC)
+    lo = int(off[tail[0]])
+    seg = buf[lo:int(off[-1]) + int(sizes[-1])].cpu().numpy()
+    want = oracle.crc32_messages(seg, off[tail] - np.uint64(lo), sizes[tail], threads=16)
+    assert np.array_equal(got[tail], want)
+    # every word against k_crc_any: the last record moved one byte up is a gap,
+    # so the batch is not packed and the device flag sends it to k_crc_any
+    g = off.copy()
+    g[-1] += 1
+    l2 = sizes.copy()
+    l2[-1] -= 1
+    doff.copy_(torch.from_numpy(g.view(np.int64)))
+    dlen.copy_(torch.from_numpy(l2.view(np.int32)))
+    hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=NREC, flags=hc.HC_F_MESSAGES)
+    torch.cuda.synchronize()
+    assert not hc.seg_taken()
+    got2 = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got2[:-1], got[:-1])

@@ -172,9 +172,9 @@ def test_seg_config5b_size(cuda, hc, oracle):
     rng = np.random.default_rng(55)
     lens = (64.0 * np.exp(rng.random(n) * np.log(1024.0))).astype(np.uint64)
     off = packed(lens, 1)
-    total = int(off[-1] + lens[-1]) + 64
+    total = (int(off[-1] + lens[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
     buf = torch.empty(total, dtype=torch.uint8, device="cuda")
-    hc.dev_fill_range(buf, 0x5B, 0, 1, stride=total, ulen=total)
+    hc.dev_fill_range(buf, 0x5B, 0, total >> 20, stride=1 << 20, ulen=1 << 20)  # every byte, in 1 MiB blocks
     got, was = run(torch, hc, buf, off, lens)
     assert was
     # oracle on 20k records of the first 512 MB (all of the first 200)
