@@ -957,24 +957,6 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
 }
 
 // ---------------------------------------------------------------------------
-// Fused AddCRCsToData (/root/reference/utils/crc/crc_util.go:41-64): frame the
-// n-byte payload src into ceil(n/4092) zero-padded 4096-byte blocks at dst and
-// stamp each block's CRC -- one read of src, one write of dst.  One wave per
-// output block (4 rows of 1 KiB): lane l of row r owns output bytes
-// 1024r+16l..+15 = payload bytes b*4092 - 4 + (1024r+16l) ..; they are
-// funnel-shifted out of two aligned source chunks (the block's source
-// misalignment is the same for its 4 rows), masked to the block's payload,
-// stored with one coalesced 16-B store per lane and hashed exactly like a
-// block of the streaming kernel (W0 in place of bytes 0..3).  Lane 0 keeps
-// its row-0 chunk and stores it last, with the CRC in bytes 0..3.
-// Interior blocks are handed out like k_crc_grp's: workgroup g owns the chunks
-// of 2^lg_chunk consecutive blocks c*G + g and its waves take them one at a
-// time from an LDS counter (tools/kcopy2: a persistent read+write stream went
-// from 5.0-5.5 TB/s with static deals to 5.9 TB/s this way).
-// Two interior blocks per wave: one prefetched while one is framed (a third
-// in flight, other chunk sizes, XCD-contiguous chunk slots, other store orders
-// and the timing-only build measured the same or slower: DESIGN.md 4.4a,
-// tools/kframe with tools/ab_hc_kernels.hip).
 // Edge blocks of AddCRCsToData framing (the first, whose row 0 would start 4
 // bytes before src, and the last, whose payload may end mid-row): aligned
 // loads predicated on the payload range + funnel shift + byte masks -- never
