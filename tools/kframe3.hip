@@ -903,7 +903,12 @@ int main(int argc, char **argv) {
                        bitmap, fb, xc, dt);                                                                          \
   }
   const char *only = std::getenv("KF3_SET");  // "xl": the LDS-shared placement study only
-  if (only && std::string(only) == "xl") {
+  if (only && std::string(only) == "u") {  // unframe geometry only: production against round 3's first build
+    for (int k = 0; k < 2; k++) {
+      vs.push_back({"PROD k_unframe (K=1, LDS cols)", 1, true, prod_unframe, {}});
+      vs.push_back({"per-lane cols unframe K=4 W=4 (r3 first)", 1, true, XHU(4, 4), {}});
+    }
+  } else if (only && std::string(only) == "xl") {
     vs.push_back({"PROD k_frame (persistent, LDS tables)", 0, true, prod_frame, {}});
     vs.push_back({"hybrid frame interior K=4 W=4 ld,hash,st", 0, true, XI(4, 4, 1, 2), {}});
     vs.push_back({"LDS-cols frame K=1 W=4", 0, true, XL(1, 4), {}});
@@ -914,10 +919,11 @@ int main(int argc, char **argv) {
     vs.push_back({"NULL np frame K=1 (memory pattern)", 0, false, XBN(1), {}});
     vs.push_back({"PROD k_frame (again)", 0, true, prod_frame, {}});
     vs.push_back({"PROD k_unframe", 1, true, prod_unframe, {}});
+    vs.push_back({"per-lane cols unframe K=4 W=4 (r3 first)", 1, true, XHU(4, 4), {}});
     vs.push_back({"LDS-cols unframe K=1 W=4", 1, true, XLU(1, 4), {}});
-    vs.push_back({"LDS-cols unframe K=1 W=4 stores first", 1, true, XLU(1, 4, true), {}});
-    vs.push_back({"LDS-cols unframe K=1 W=8 stores first", 1, true, XLU(1, 8, true), {}});
+    vs.push_back({"LDS-cols unframe K=2 W=4", 1, true, XLU(2, 4), {}});
     vs.push_back({"LDS-cols unframe K=4 W=4", 1, true, XLU(4, 4), {}});
+    vs.push_back({"per-lane cols unframe K=4 W=4 (again)", 1, true, XHU(4, 4), {}});
     vs.push_back({"PROD k_unframe (again)", 1, true, prod_unframe, {}});
   } else {
   vs.push_back({"PROD k_frame (persistent, LDS tables)", 0, true, prod_frame, {}});
