@@ -1335,19 +1335,20 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 //   k_seg_combine  per record: H(a) and H(b) plus the raw CRCs of the whole
 //                  units between them, advanced to re_b, then one inverse
 //                  shift by re_b - b (SegTables: 6 table multiplies a record).
-constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups
+constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups (the kernels take it as kU)
 constexpr uint32_t kSegMaxRecord = 1u << 24;  // longest record the stream takes (16 MiB)
 constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's grid cap: one "bad" slot per workgroup
 
 struct SegGeo {
   uint64_t a0, pend, units;
 };
+template <uint32_t kU = kSegUnitLg>
 __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *offs, const uint32_t *lens,
                                           uint64_t n) {
   SegGeo g;
   g.a0 = ((uint64_t)base + offs[0]) & ~1023ull;
   g.pend = (uint64_t)base + offs[n - 1] + lens[n - 1];
-  g.units = ((g.pend - g.a0) >> kSegUnitLg) + 1;
+  g.units = ((g.pend - g.a0) >> kU) + 1;
   return g;
 }
 
@@ -1358,10 +1359,11 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 // in one 4 KiB group (records under ~64 B: k_crc_any), else 0.  Every slot is
 // written, so the dispatch needs no memset: k_seg_stream's workgroups OR the
 // slots and its workgroup 0 stores the flag the later kernels read.
+template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
                                                   uint32_t *__restrict__ plan_bad, uint32_t *__restrict__ first_ev) {
-  const SegGeo g = seg_geo(base, offs, lens, n);
+  const SegGeo g = seg_geo<kU>(base, offs, lens, n);
   bool bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0;
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= n && !bad; j += step) {
@@ -1371,10 +1373,10 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
       const uint64_t pp = (uint64_t)base + offs[j - 1];
       if ((j < n && offs[j] != offs[j - 1] + lens[j - 1]) || pj < pp) bad = true;
       if (lens[j - 1] > kSegMaxRecord) bad = true;  // k_seg_combine's unit chain stays <= 1025 units
-      ulo = ((pp - g.a0) >> kSegUnitLg) + 1;
+      ulo = ((pp - g.a0) >> kU) + 1;
     }
     if (j >= 64 && ((pj - g.a0) >> 12) == (((uint64_t)base + offs[j - 64] - g.a0) >> 12)) bad = true;
-    const uint64_t uj = (pj - g.a0) >> kSegUnitLg;
+    const uint64_t uj = (pj - g.a0) >> kU;
     if (uj >= g.units || pj < g.a0) bad = true;
     if (bad) break;
     for (uint64_t u = ulo; u <= uj; u++) first_ev[u] = (uint32_t)j;
@@ -1387,6 +1389,7 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
 
 // (its timing-only builds -- rows XOR-folded, or no event work at all -- are in
 // tools/ab_hc_kernels.hip)
+template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
                                                             uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
@@ -1438,7 +1441,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   auto slot_st = [&](uint32_t l, uint32_t v) {
     __hip_atomic_store(&lds[slot + l], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   };
-  const SegGeo geo = seg_geo(base, offs, lens, n);
+  const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint64_t M = geo.units;
   const uint64_t rhi = (geo.pend + 15) & ~15ull;  // loads past the span's last chunk return zeros
   const uint64_t G = gridDim.x;
@@ -1450,9 +1453,9 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     return (((uint64_t)(k >> lg_chunk) * G + blockIdx.x) << lg_chunk) | (k & cmask);
   };
   auto unit_rsrc = [&](uint64_t u) {
-    const uint64_t U = geo.a0 + (u << kSegUnitLg);
+    const uint64_t U = geo.a0 + (u << kU);
     const uint64_t avail = u < M && rhi > U ? rhi - U : 0;
-    return buf_range(reinterpret_cast<const void *>(U), (uint32_t)(avail < (1u << kSegUnitLg) ? avail : (1u << kSegUnitLg)));
+    return buf_range(reinterpret_cast<const void *>(U), (uint32_t)(avail < (1u << kU) ? avail : (1u << kU)));
   };
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   // window: the positions of events f .. f+63, one per lane (a group holds at most 64)
@@ -1550,9 +1553,9 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   };
 
   for (;;) {
-    const uint64_t gs = geo.a0 + (u << kSegUnitLg) + ((uint64_t)g << 12);
+    const uint64_t gs = geo.a0 + (u << kU) + ((uint64_t)g << 12);
     const uint64_t wpos = win_pos(wraw, wfirst);
-    const bool lastg = g == 3;
+    const bool lastg = g == (1u << (kU - 12)) - 1u;  // the unit's last 4 KiB group
     // the next group: this unit's, or unit un's first; its events' window
     const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M]
                               : wfirst + (uint64_t)__popcll(__ballot(wpos < gs + 4096u));
@@ -1605,6 +1608,7 @@ __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) 
 // sub-passes of 64 events (H per lane) and 63 records (the end event's values
 // from the next lane by a shuffle), every sub-pass's loads issued before the
 // first is used.
+template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ lens, uint64_t n,
                                                       const uint32_t *__restrict__ flag,
@@ -1612,7 +1616,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken) {
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
-  constexpr uint32_t kUnitRows = 1u << (kSegUnitLg - 10);
+  constexpr uint32_t kUnitRows = 1u << (kU - 10);
   __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024];
   {  // rs and iv are contiguous in SegTables: every load issued before the first store
     static_assert(offsetof(SegTables, iv) == offsetof(SegTables, rs) + sizeof(SegTables::rs), "rs, iv adjacent");
@@ -1633,7 +1637,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
   __syncthreads();
   if (*flag) return;
-  const SegGeo geo = seg_geo(base, offs, lens, n);
+  const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -1657,7 +1661,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
       const uint64_t xb = __shfl_down((unsigned long long)x[p], 1);
       if (lane < 63 && j < n) {
         const uint32_t da = (uint32_t)(((uint64_t)re << 10) - x[p]), db = (uint32_t)(((uint64_t)rb << 10) - xb);
-        const uint64_t ua = x[p] >> kSegUnitLg, ub = xb >> kSegUnitLg;
+        const uint64_t ua = x[p] >> kU, ub = xb >> kU;
         const uint32_t X = eh[p] ^ st->ones[da - 1];
         const uint32_t ue = (uint32_t)(ua + 1) * kUnitRows;  // a's unit end, in rows
         uint32_t v = rsh(X, ua < ub ? ue - re : rb - re);
@@ -1808,11 +1812,11 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
            *ev_h = unit_raw + max_units;
   const uint64_t pg = (n + 256) / 256;
   const uint32_t plan_wgs = (uint32_t)(pg < kSegPlanMaxWgs ? pg : kSegPlanMaxWgs);
-  hipLaunchKernelGGL(k_seg_plan, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
+  hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
                      first_ev);
-  hipLaunchKernelGGL(k_seg_stream, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
+  hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
                      plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
-  hipLaunchKernelGGL(k_seg_combine, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
+  hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
                      b.crc_out, st, taken);
   return hipGetLastError();
 }

@@ -9,6 +9,8 @@
 //   r3j       launch_seg's kernels with round 3's first combine (22 multiplies)
 //   combine   the combine kernel alone, production's and r3j's, re-run over
 //             the workspace the previous variant's stream left
+//   units     plan + stream + combine with 8 KiB and 4 KiB units (production:
+//             16 KiB), several chunk sizes
 // Each variant runs `launches` calls back to back between two events (the
 // mean includes the gaps between calls, as bench.py's bracket mode); rounds
 // interleave the variants.  Every variant's CRC words are compared with PROD's.
@@ -240,6 +242,28 @@ int main(int argc, char **argv) {
                 }, {}});
   vs.push_back({"combine alone (prod, 6 mul)", new_combine, {}});
   vs.push_back({"combine alone (r3j, 22 mul)", old_combine, {}});
+  // the unit size: 8 KiB and 4 KiB units (k_crc_grp's piece sizes) against production's 16 KiB
+  const uint64_t span_b = (reinterpret_cast<uintptr_t>(buf) + total) - (reinterpret_cast<uintptr_t>(buf) & ~uint64_t(1023));
+  const uint64_t mu13 = (span_b >> 13) + 2, mu12 = (span_b >> 12) + 2;
+  uint32_t *ws13, *ws12;
+  CK(hipMalloc(&ws13, hc::seg_workspace_bytes(n, mu13)));
+  CK(hipMalloc(&ws12, hc::seg_workspace_bytes(n, mu12)));
+#define SEGU(KU, WS, MU, LGC)                                                                                           \
+  [&, WS, MU](hipStream_t st) {                                                                                        \
+    uint32_t *f_ = WS, *pb_ = WS + 64, *fe_ = pb_ + hc::kSegPlanMaxWgs, *ur_ = fe_ + (MU) + 1, *eh_ = ur_ + (MU);        \
+    hipLaunchKernelGGL(hc::k_seg_plan<KU>, dim3(plan_wgs), dim3(256), 0, st, b.base, b.off, b.len, n, (uint64_t)(MU),   \
+                       pb_, fe_);                                                                                      \
+    hipLaunchKernelGGL(hc::k_seg_stream<KU>, dim3(cus), dim3(hc::kFastThreads), 0, st, b.base, b.off, b.len, n,          \
+                       (uint32_t)(LGC), pb_, plan_wgs, f_, fe_, ur_, eh_, dt);                                          \
+    hipLaunchKernelGGL(hc::k_seg_combine<KU>, dim3(cus), dim3(1024), 0, st, b.base, b.off, b.len, n, f_, ur_, eh_, crc, \
+                       dst, nullptr);                                                                                  \
+  }
+  vs.push_back({"seg only, 8 KiB units, chunk 128", SEGU(13, ws13, mu13, 7), {}});
+  vs.push_back({"seg only, 8 KiB units, chunk 256", SEGU(13, ws13, mu13, 8), {}});
+  vs.push_back({"seg only, 4 KiB units, chunk 256", SEGU(12, ws12, mu12, 8), {}});
+  vs.push_back({"seg only, 4 KiB units, chunk 512", SEGU(12, ws12, mu12, 9), {}});
+  vs.push_back({"seg only (cached, again)", [&](hipStream_t st) { CK(hc::launch_seg(b, dst, ws_cached, mu, cus, st, nullptr)); },
+                {}});
 
   std::vector<uint32_t> ref(n), got(n);
   vs[0].run(s);
