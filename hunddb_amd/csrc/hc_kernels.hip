@@ -1094,9 +1094,9 @@ __device__ __forceinline__ uint32_t place_lq(const uint32_t *lq, uint32_t lane, 
 //                  funnel shift and byte masks, one wave each -- no byte
 //                  outside src is touched.
 //   k_frame        interior blocks 1 .. nblk-2: every row window lies inside
-//                  src, so each lane reads its 16 output bytes with ONE
-//                  unaligned 16-byte load (gfx950 runs in unaligned-access
-//                  mode).  One block per wave, 4-wave workgroups that exit:
+//                  src, so each lane's 16 output bytes come from two aligned
+//                  16-B chunks (its own and its neighbour's, by DPP) without
+//                  masks.  One block per wave, 4-wave workgroups that exit:
 //                  row steps and the stream combine through XTab (no LDS
 //                  tables to fill), the lane placement against the
 //                  workgroup's LDS copy of its columns.  The row stores go out
@@ -1128,28 +1128,56 @@ __global__ __launch_bounds__(128) void k_frame_edges(const uint8_t *__restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+__global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, uint64_t n, uint8_t *__restrict__ dst,
                                                uint64_t nblk, uint32_t *__restrict__ crc_out,
                                                const DeviceTables *__restrict__ tables) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef u32x4 u32x4_u __attribute__((aligned(1)));
   constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // interior block
   const bool mine = b + 1 < nblk;
-  u32x4 v[4];
+  // Aligned source loads: lane l's 16 output bytes of row r are bytes m .. m+15
+  // of its aligned chunk C_l and the next one, C_{l+1}, which the right
+  // neighbour loaded (a whole-wave DPP shift, wave_shl:1) -- lane 63 loads its
+  // second chunk itself through a buffer range in which every other lane's
+  // offset is out of range (no memory access, no branch around the load).
+  // m = (S mod 16) is the block's misalignment, uniform over its rows.  +3.5-4 %
+  // over one unaligned 16-B load per lane (tools/kframe3 KF3_SET=a).
+  const uintptr_t S = (uintptr_t)src + b * kPay - 4;  // source of output byte 0
+  const uint32_t m = (uint32_t)(S & 15u), qs = m >> 2, rs = m & 3u;
+  const uintptr_t Sa = S - m;
+  // [Sa, Sa + 4112) clipped to the aligned chunk holding src's last byte: the
+  // buffer range check is per load, so the range ends on a 16-B boundary (as
+  // k_crc_any's edge rows: no byte outside src's own aligned chunks is read)
+  const uintptr_t end16 = ((uintptr_t)src + n + 15) & ~(uintptr_t)15;
+  const __amdgpu_buffer_rsrc_t r63 =
+      buf_range(reinterpret_cast<const void *>(Sa), mine ? (uint32_t)(end16 - Sa < 4112u ? end16 - Sa : 4112u) : 0u);
+  u32x4 C[4];
+  uint4 X[4];
   if (mine) {  // the block's rows first: the table work below overlaps their latency
-    const uint8_t *S = src + b * kPay - 4 + 16u * lane;
 #pragma unroll
-    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(S + r * kRowBytes));
+    for (int r = 0; r < 4; r++)
+      C[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Sa + r * kRowBytes + 16u * lane));
   }
+#pragma unroll
+  for (int r = 0; r < 4; r++) X[r] = buf_load16(r63, lane == 63 ? (uint32_t)((r + 1) * kRowBytes) : 0xFFFFFFFFu);
   fill_lane_q(lq, tables);
   const XTab TM = make_xtab(tables->tg, lane);
   const XTab TS = make_xtab(tables->s4, lane);
   const uint32_t w0 = tables->w0;
   __syncthreads();
   if (!mine) return;
+  auto wave_shl1 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false); };
+  u32x4 v[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint4 a = make_uint4(C[r].x, C[r].y, C[r].z, C[r].w);
+    uint4 nb = make_uint4(wave_shl1(a.x), wave_shl1(a.y), wave_shl1(a.z), wave_shl1(a.w));
+    if (lane == 63) nb = X[r];
+    const uint4 f = funnel16(a, nb, qs, rs);
+    v[r] = u32x4{f.x, f.y, f.z, f.w};
+  }
   uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
 #pragma unroll
   for (int r = 0; r < 4; r++) {  // lane 0 writes zeros to bytes 0..3 and the CRC over them below
@@ -1765,7 +1793,7 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
   if (nblk > 2) {
     const uint64_t wgs = (nblk - 2 + 3) / 4;  // one interior block per wave
     if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, dst, nblk, crc_out, tables);
+    hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, n, dst, nblk, crc_out, tables);
   }
   return hipGetLastError();
 }

@@ -386,6 +386,135 @@ __global__ __launch_bounds__(kW * 64) void k_frame_xl(const uint8_t *__restrict_
   }
 }
 
+// k_frame_xl (K = 1) with 16-B ALIGNED source loads: each lane loads the
+// aligned chunk at its window's start, takes its right neighbour's chunk by a
+// whole-wave DPP shift (wave_shl:1, a VALU op, no LDS crossbar) and funnel-
+// shifts the pair by the block's misalignment (uniform); lane 63 loads its
+// second chunk itself through a buffer range (the other lanes' offsets are out
+// of range: no memory access, no branch around the load).  kcopy2 (DESIGN.md
+// 4.4a): aligned 4 KiB-per-wave copies 6.0 TB/s, the frame geometry's
+// unaligned ones 5.6.
+template <int kW>
+__global__ __launch_bounds__(kW * 64) void k_frame_xa(const uint8_t *__restrict__ src, uint64_t n,
+                                                      uint8_t *__restrict__ dst, uint64_t nblk,
+                                                      uint32_t *__restrict__ crc_out, const XbCols *__restrict__ xc,
+                                                      const hc::DeviceTables *__restrict__ tables) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr uint64_t kPay = 4092;
+  __shared__ __attribute__((aligned(16))) uint32_t lc[8 * 64 * 4];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b = 1 + (uint64_t)blockIdx.x * kW + (threadIdx.x >> 6);
+  const bool mine = b + 1 < nblk;
+  const uintptr_t S = (uintptr_t)src + b * kPay - 4;  // source of output byte 0
+  const uint32_t m = (uint32_t)(S & 15u), q = m >> 2, rb = m & 3u;
+  const uintptr_t Sa = S - m;
+  const uintptr_t end = ((uintptr_t)src + n + 15) & ~(uintptr_t)15;  // the range check is per 16-B load
+  const uint32_t span = mine ? (uint32_t)(end - Sa < 4112u ? end - Sa : 4112u) : 0u;
+  const __amdgpu_buffer_rsrc_t rr = hc::buf_range(reinterpret_cast<const void *>(Sa), span);
+  uint4 C[4], X[4];
+  if (mine) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Sa + r * hc::kRowBytes + 16u * lane));
+      C[r] = make_uint4(t.x, t.y, t.z, t.w);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) X[r] = hc::buf_load16(rr, lane == 63 ? (uint32_t)((r + 1) * hc::kRowBytes) : 0xFFFFFFFFu);
+  {
+    const uint4 *g = reinterpret_cast<const uint4 *>(&xc->lq[0][0][0]);
+    uint4 t[512 / (kW * 64)];
+#pragma unroll
+    for (int k = 0; k < 512 / (kW * 64); k++) t[k] = g[threadIdx.x + k * kW * 64];
+#pragma unroll
+    for (int k = 0; k < 512 / (kW * 64); k++) reinterpret_cast<uint4 *>(lc)[threadIdx.x + k * kW * 64] = t[k];
+  }
+  uint32_t msk[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) msk[i] = 0u - ((lane >> i) & 1u);
+  const Tab5 TM = make_tab5(xc->col[0], msk);
+  const Tab5 TS = make_tab5(xc->col[1], msk);
+  const uint32_t w0 = tables->w0;
+  __syncthreads();
+  if (!mine) return;
+  auto shl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false); };
+  u32x4 v[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    uint4 nb = make_uint4(shl(C[r].x), shl(C[r].y), shl(C[r].z), shl(C[r].w));
+    if (lane == 63) nb = X[r];
+    const uint4 f = hc::funnel16(C[r], nb, q, rb);
+    v[r] = u32x4{f.x, f.y, f.z, f.w};
+  }
+  uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    u32x4 t = v[r];
+    if (r == 0) t.x = lane == 0 ? 0u : t.x;
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x4 *>(ob + r * hc::kRowBytes));
+  }
+  uint32_t c[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    u32x4 t = v[r];
+    if (r == 0) t.x = lane == 0 ? w0 : t.x;
+    const uint32_t wd[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = r == 0 ? wd[k] : apply5(TM, c[k], wd[k]);
+  }
+  const uint32_t d = apply5(TS, apply5(TS, apply5(TS, c[0], c[1]), c[2]), c[3]);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int qq = 0; qq < 8; qq++) {
+    const uint4 c4 = reinterpret_cast<const uint4 *>(lc)[qq * 64 + lane];
+    const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t mm = (uint32_t)((int32_t)(d << (31 - (4 * qq + r))) >> 31);
+      acc = __builtin_amdgcn_bitop3_b32(mm, cq[r], acc, 0x6A);
+    }
+  }
+  const uint32_t crc = hc::wave_xor(acc) ^ 0xFFFFFFFFu;
+  hc::lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crc);
+  if (crc_out) hc::lane0_store_u32(crc_out + b, crc);
+}
+
+// Timing-only twin of k_frame_xa (aligned loads + DPP funnel, XOR fold).
+__global__ __launch_bounds__(256) void k_frame_xa_null(const uint8_t *__restrict__ src, uint64_t n,
+                                                       uint8_t *__restrict__ dst, uint64_t nblk,
+                                                       uint32_t *__restrict__ crc_out) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr uint64_t kPay = 4092;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b + 1 >= nblk) return;
+  const uintptr_t S = (uintptr_t)src + b * kPay - 4;
+  const uint32_t m = (uint32_t)(S & 15u), q = m >> 2, rb = m & 3u;
+  const uintptr_t Sa = S - m;
+  const uintptr_t end = ((uintptr_t)src + n + 15) & ~(uintptr_t)15;
+  const __amdgpu_buffer_rsrc_t rr = hc::buf_range(reinterpret_cast<const void *>(Sa), (uint32_t)(end - Sa < 4112u ? end - Sa : 4112u));
+  uint4 C[4], X[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Sa + r * hc::kRowBytes + 16u * lane));
+    C[r] = make_uint4(t.x, t.y, t.z, t.w);
+    X[r] = hc::buf_load16(rr, lane == 63 ? (uint32_t)((r + 1) * hc::kRowBytes) : 0xFFFFFFFFu);
+  }
+  auto shl = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false); };
+  uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+  uint32_t x = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    uint4 nb = make_uint4(shl(C[r].x), shl(C[r].y), shl(C[r].z), shl(C[r].w));
+    if (lane == 63) nb = X[r];
+    const uint4 f = hc::funnel16(C[r], nb, q, rb);
+    __builtin_nontemporal_store(u32x4{f.x, f.y, f.z, f.w}, reinterpret_cast<u32x4 *>(ob + r * hc::kRowBytes));
+    x ^= f.x ^ f.y ^ f.z ^ f.w;
+  }
+  x = hc::wave_xor(x);
+  if (crc_out) hc::lane0_store_u32(crc_out + b, x);
+}
+
 // The production k_unframe (4 KiB blocks) with the lane placement's columns
 // shared by the workgroup in LDS (as k_frame_xl) and K blocks per wave.
 template <int K, int kW, bool kStoreFirst = false>
@@ -903,7 +1032,25 @@ int main(int argc, char **argv) {
                        bitmap, fb, xc, dt);                                                                          \
   }
   const char *only = std::getenv("KF3_SET");  // "xl": the LDS-shared placement study only
-  if (only && std::string(only) == "u") {  // unframe geometry only: production against round 3's first build
+#define XA(W)                                                                                                     \
+  [&](hipStream_t st) {                                                                                             \
+    hipLaunchKernelGGL(xb::k_frame_edges_xh, dim3(1), dim3(128), 0, st, src, npay, framed, nblk, crc, xc, dt);        \
+    const uint64_t g_ = (nblk - 2 + (W)-1) / (W);                                                                   \
+    hipLaunchKernelGGL((xb::k_frame_xa<W>), dim3((unsigned)g_), dim3((W) * 64), 0, st, src, npay, framed, nblk, crc, \
+                       xc, dt);                                                                                     \
+  }
+  if (only && std::string(only) == "a") {  // aligned source loads for k_frame
+    for (int k = 0; k < 2; k++) {
+      vs.push_back({"PROD k_frame (unaligned loads)", 0, true, prod_frame, {}});
+      vs.push_back({"aligned loads + DPP funnel, W=4", 0, true, XA(4), {}});
+      vs.push_back({"NULL np frame K=1 (unaligned)", 0, false, XBN(1), {}});
+      vs.push_back({"NULL aligned + DPP funnel", 0, false, [&](hipStream_t st) {
+                      const uint64_t g_ = (nblk - 2 + 3) / 4;
+                      hipLaunchKernelGGL(xb::k_frame_xa_null, dim3((unsigned)g_), dim3(256), 0, st, src, npay, framed,
+                                         nblk, crc);
+                    }, {}});
+    }
+  } else if (only && std::string(only) == "u") {  // unframe geometry only: production against round 3's first build
     for (int k = 0; k < 2; k++) {
       vs.push_back({"PROD k_unframe (K=1, LDS cols)", 1, true, prod_unframe, {}});
       vs.push_back({"per-lane cols unframe K=4 W=4 (r3 first)", 1, true, XHU(4, 4), {}});
