@@ -609,6 +609,27 @@ def test_dev_add_crcs_fused(cuda, hc, oracle, shift):
         assert (u32(crcs) == want.view(np.uint32)[::1024]).all()
 
 
+def test_dev_add_crcs_tiny_last_block(cuda, hc, oracle):
+    """k_frame's interior blocks load aligned 16-B chunks, the last lane's second
+    chunk through a buffer range that ends on the 16-B boundary after src's last
+    byte: every source misalignment with a last block of 1-16 payload bytes, so
+    the interior block before it reads right up to that boundary."""
+    torch = cuda
+    rng = np.random.default_rng(77)
+    for shift in range(16):
+        for tail in range(1, 17):
+            n = 4092 * 3 + tail
+            host = rng.integers(0, 256, n + shift, dtype=np.uint8)
+            dsrc = torch.from_numpy(host).to("cuda")[shift:]
+            out_n = hc.lib().hc_add_crcs_size(n)
+            dst = torch.full((out_n,), 0xA5, dtype=torch.uint8, device="cuda")
+            hc.dev_add_crcs(dsrc, dst, n=n)
+            torch.cuda.synchronize()
+            want = np.zeros(out_n, dtype=np.uint8)
+            assert oracle.lib().oc_add_crcs_to_data(host[shift:].tobytes(), n, want.ctypes.data) == out_n
+            assert dst.cpu().numpy().tobytes() == want.tobytes(), (shift, tail)
+
+
 def test_dev_add_crcs_large_properties(cuda, hc, oracle):
     """256 MiB payload: the framed output's blocks verify clean, the payload
     round-trips (SizeWithoutCRCs direction), and the CRC words match the
