@@ -49,6 +49,16 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_a
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// 16-B load from an address computed as an integer, as a GLOBAL load.  Through
+// a generic pointer hipcc emits flat_load, which also counts on lgkmcnt: every
+// later LDS or scalar-load wait then waits for the load too, and a prefetch
+// issued before LDS table lookups stops being one.
+typedef unsigned int gu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(uintptr_t a) {
+  const gu32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) gu32x4 *>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // 32x32 GF(2) mat-vec: XOR of col[i] over the set bits i of d.
 __device__ __forceinline__ uint32_t matvec32(const uint32_t (&col)[32], uint32_t d) {
   uint32_t e = 0;
@@ -678,7 +688,7 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       const bool in = act && L > 0 && X + 16u > P && X < P + L;
       // plain (cached) load: records packed back to back share lines that the
       // next chunks of the neighbouring lanes read again
-      return *reinterpret_cast<const uint4 *>(in ? X : safe);
+      return gload16(in ? X : safe);
     };
     auto sel = [&](uint32_t a, uint32_t b, uint32_t c2, uint32_t d) { return qw == 0 ? a : qw == 1 ? b : qw == 2 ? c2 : d; };
     // 16 bytes at byte mq of the 32-byte pair (a, b), mq per lane
@@ -1107,7 +1117,7 @@ __global__ __launch_bounds__(128) void k_frame_edges(const uint8_t *__restrict__
                                                      uint8_t *__restrict__ dst, uint64_t nblk,
                                                      uint32_t *__restrict__ crc_out,
                                                      const DeviceTables *__restrict__ tables) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   if (wv == 1 && nblk < 2) return;
   const uint64_t b = wv == 0 ? 0 : nblk - 1;
   uint32_t col[32];
@@ -1135,16 +1145,22 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
   constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // interior block
+  const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6);  // interior block
   const bool mine = b + 1 < nblk;
+  // A wave past the last interior block loads block 1's rows (interior
+  // whenever this kernel runs) and exits after the barrier: no branch around
+  // the row loads, so the waitcnt pass sees them on one path.
+  const uint64_t bl = mine ? b : 1;
   // Aligned source loads: lane l's 16 output bytes of row r are bytes m .. m+15
   // of its aligned chunk C_l and the next one, C_{l+1}, which the right
-  // neighbour loaded (a whole-wave DPP shift, wave_shl:1) -- lane 63 loads its
-  // second chunk itself through a buffer range in which every other lane's
-  // offset is out of range (no memory access, no branch around the load).
-  // m = (S mod 16) is the block's misalignment, uniform over its rows.  +3.5-4 %
-  // over one unaligned 16-B load per lane (tools/kframe3 KF3_SET=a).
-  const uintptr_t S = (uintptr_t)src + b * kPay - 4;  // source of output byte 0
+  // neighbour loaded (a whole-wave DPP shift, wave_shl:1).  Lane 63's C_{l+1}
+  // is lane 0's chunk of the next row (v_readlane, no memory access); only row
+  // 3's, the chunk after the block, is loaded, through a buffer range in which
+  // every other lane's offset is out of range (no branch around the load).
+  // m = (S mod 16) is the block's misalignment, uniform over its rows.  Aligned
+  // loads ran +3.5-4 % over one unaligned 16-B load per lane (tools/kframe3
+  // KF3_SET=a); the one tail load instead of four, +2.6-3.1 % (tools/kframe4).
+  const uintptr_t S = (uintptr_t)src + bl * kPay - 4;  // source of output byte 0
   const uint32_t m = (uint32_t)(S & 15u), qs = m >> 2, rs = m & 3u;
   const uintptr_t Sa = S - m;
   // [Sa, Sa + 4112) clipped to the aligned chunk holding src's last byte: the
@@ -1152,29 +1168,40 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
   // k_crc_any's edge rows: no byte outside src's own aligned chunks is read)
   const uintptr_t end16 = ((uintptr_t)src + n + 15) & ~(uintptr_t)15;
   const __amdgpu_buffer_rsrc_t r63 =
-      buf_range(reinterpret_cast<const void *>(Sa), mine ? (uint32_t)(end16 - Sa < 4112u ? end16 - Sa : 4112u) : 0u);
+      buf_range(reinterpret_cast<const void *>(Sa), (uint32_t)(end16 - Sa < 4112u ? end16 - Sa : 4112u));
+  // The workgroup's placement columns (L2 hits) are loaded first, then the rows
+  // (+0.6 % over the other order, tools/kframe4).  The row addresses are
+  // integers, so the row loads are flat loads: global ones (src's provenance)
+  // ran 1.5 % slower here.
+  static_assert(kLaneQWords / 4 / 256 == 2, "two uint4s of columns per thread");
+  const uint4 *lqg = reinterpret_cast<const uint4 *>(&tables->lane_q[0][0][0]);
+  const uint4 lq0 = lqg[threadIdx.x], lq1 = lqg[threadIdx.x + 256u];  // named: an array was promoted to LDS
+  __builtin_amdgcn_sched_barrier(0);
   u32x4 C[4];
-  uint4 X[4];
-  if (mine) {  // the block's rows first: the table work below overlaps their latency
 #pragma unroll
-    for (int r = 0; r < 4; r++)
-      C[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Sa + r * kRowBytes + 16u * lane));
-  }
-#pragma unroll
-  for (int r = 0; r < 4; r++) X[r] = buf_load16(r63, lane == 63 ? (uint32_t)((r + 1) * kRowBytes) : 0xFFFFFFFFu);
-  fill_lane_q(lq, tables);
+  for (int r = 0; r < 4; r++)
+    C[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Sa + r * kRowBytes + 16u * lane));
+  const uint4 X3 = buf_load16(r63, lane == 63 ? 4096u : 0xFFFFFFFFu);
+  __builtin_amdgcn_sched_barrier(0);
+  reinterpret_cast<uint4 *>(lq)[threadIdx.x] = lq0;
+  reinterpret_cast<uint4 *>(lq)[threadIdx.x + 256u] = lq1;
   const XTab TM = make_xtab(tables->tg, lane);
   const XTab TS = make_xtab(tables->s4, lane);
   const uint32_t w0 = tables->w0;
   __syncthreads();
   if (!mine) return;
   auto wave_shl1 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false); };
+  auto lane0_of = [](const u32x4 x) {  // lane 0's chunk, wave-uniform
+    return make_uint4(__builtin_amdgcn_readlane(x.x, 0), __builtin_amdgcn_readlane(x.y, 0),
+                      __builtin_amdgcn_readlane(x.z, 0), __builtin_amdgcn_readlane(x.w, 0));
+  };
   u32x4 v[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const uint4 a = make_uint4(C[r].x, C[r].y, C[r].z, C[r].w);
     uint4 nb = make_uint4(wave_shl1(a.x), wave_shl1(a.y), wave_shl1(a.z), wave_shl1(a.w));
-    if (lane == 63) nb = X[r];
+    const uint4 t = r < 3 ? lane0_of(C[r < 3 ? r + 1 : 3]) : X3;
+    if (lane == 63) nb = t;
     const uint4 f = funnel16(a, nb, qs, rs);
     v[r] = u32x4{f.x, f.y, f.z, f.w};
   }
@@ -1224,7 +1251,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
 //   * first_bad: a wave lowers it at most once, and only after reading it
 //     (a batch of all-bad blocks would otherwise put ~nblk/4 atomics on one word).
 template <uint32_t lg_groups>
-__global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blocks, uint64_t nblk,
+__global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t nblk,  // (not restrict: below)
                                                  uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
                                                  uint32_t *__restrict__ bad_bitmap,
                                                  unsigned long long *__restrict__ first_bad,
@@ -1236,7 +1263,61 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *__restrict__ blo
   constexpr uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * K;
+  if constexpr (lg_groups == 0 && K == 1) {
+    // 4 KiB blocks, one a wave: straight-line code with a wave-uniform block
+    // index.  The group loop below, with the index taken from threadIdx as a
+    // VGPR (exec-masked branches), ran 6.5 % slower (tools/kframe4: 5490 vs
+    // 5830-5850 GB/s).  `blocks` is not __restrict__: with it, hipcc may sink
+    // the row loads past the barrier into the block that uses them.
+    const uint64_t b = (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6);
+    const bool mine = b < nblk;
+    const uint32_t w0 = tables->w0;
+    u32x4 v[4];
+    if (mine) {  // the rows before the table work
+      const uint8_t *S = blocks + b * HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
+    }
+    fill_lane_q(lq, tables);
+    const XTab TM = make_xtab(tables->tg, lane);
+    const XTab TS = make_xtab(tables->s4, lane);
+    __syncthreads();
+    if (!mine) return;
+    uint32_t c[4] = {0, 0, 0, 0};
+    uint32_t stored = 0;
+    uint8_t *ob = out + b * Bp + 16u * lane - 4;
+    u32x4 sv[4];
+    uint8_t *sa[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      u32x4 t = v[r];
+      if (r == 0) {
+        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, t.x, 0x101, 0xF, 0xF, false);  // lane+1's x
+        stored = __builtin_amdgcn_readfirstlane(t.x);                                         // LE32(block[0:4])
+        const u32x4 first = {t.y, t.z, t.w, nx};
+        sv[r] = lane == 0 ? first : t;
+        sa[r] = ob + (lane == 0 ? 4 : 0);
+        t.x = lane == 0 ? w0 : t.x;  // Go's init in place of the CRC field
+      } else {
+        sv[r] = t;
+        sa[r] = ob + r * kRowBytes;
+      }
+      const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : xapply(TM, c[k], w[k]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
+    const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
+    const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
+    if (crc_out) lane0_store_u32(crc_out + b, crcv);
+    if (first_bad && crcv != stored) {  // wave-uniform; one block a wave: at most one lowering
+      if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+      if (b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) lane0_atomic_umin64(first_bad, b);
+    }
+    return;
+  }
+  const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6)) * K;
   const uint64_t p_end = (b0 + K < nblk ? b0 + K : nblk) << lg_groups;  // this wave's groups [p0, p_end)
   uint64_t p = b0 << lg_groups;
   const uint32_t w0 = tables->w0;
@@ -1667,7 +1748,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   if (*flag) return;
   const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni(threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
   auto rsh = [&](uint32_t v, uint32_t rows) {  // rows in [0, 16]
     return rows ? seg_lds_tmul(tl + (rows - 1u) * 1024u, v) : v;
