@@ -61,6 +61,10 @@ WORKLOADS = {
     # f1: batched ReadFromDisk (k_unframe): verify 1M x 4 KiB blocks and strip
     # the CRC words (4096 MB read, 4092 MB payload written)
     "unframe": (1_000_000, "unframe", "weak"),
+    # the same at HundDB's other block sizes (config.go:137, README.md:191,255):
+    # 0.5M x 8 KiB and 0.25M x 16 KiB (4 GB each way)
+    "unframe8k": (500_000, "unframe8k", "weak"),
+    "unframe16k": (250_000, "unframe16k", "weak"),
     # config2's blocks described by off/len arrays (the per-block metadata path)
     "offlen4k": (1_000_000, "offlen4k", "weak"),
     # verify mode (CheckBlockIntegrity over the north-star batch, stamped): read B,
@@ -73,7 +77,9 @@ WORKLOADS = {
     "records": (2_000_000, "records", "weak"),
 }
 # the dominant kernel per workload (PMC passes); frame's k_frame_edges (2 blocks) is left out
-KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "records": "k_seg_stream"}  # else the streaming CRC kernel
+KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
+             "records": "k_seg_stream"}  # else the streaming CRC kernel
+UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
 
 def parse(argv=None):
@@ -335,7 +341,7 @@ def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None, mes
     return res
 
 
-def cpu_baseline_framing(kind, dev_src, threads, budget_s):
+def cpu_baseline_framing(kind, dev_src, threads, budget_s, B=4096):
     """The oracle's restatement of the reference loop over a 256 MB sample of
     the same data (Go runs each AddCRCsToData / ReadFromDisk call on one
     goroutine): 1 thread, and `threads` threads on disjoint slices; bytes
@@ -347,30 +353,31 @@ def cpu_baseline_framing(kind, dev_src, threads, budget_s):
 
     from oracle import oracle as O
     L = O.lib()
-    nblk = (256 << 20) // 4096
+    nblk = (256 << 20) // B
     per_t = nblk // threads
-    if kind == "frame":  # crc_util.go:41-64
-        src = dev_src[: nblk * 4092].cpu().numpy()
-        dst = np.empty(nblk * 4096, dtype=np.uint8)
+    P = B - 4  # payload bytes per block
+    if kind == "frame":  # crc_util.go:41-64 (B = 4096: the function's constant framing)
+        src = dev_src[: nblk * P].cpu().numpy()
+        dst = np.empty(nblk * B, dtype=np.uint8)
 
         def run(a, b):
-            L.oc_add_crcs_to_data(src.ctypes.data + a * 4092, (b - a) * 4092, dst.ctypes.data + a * 4096)
+            L.oc_add_crcs_to_data(src.ctypes.data + a * P, (b - a) * P, dst.ctypes.data + a * B)
         what = f"oc_add_crcs_to_data over {src.size} B of payload (crc_util.go:41-64)"
     else:  # block_manager.go:189-242
-        blocks = dev_src[: nblk * 4096].cpu().numpy()
-        out = np.empty(nblk * 4092, dtype=np.uint8)
+        blocks = dev_src[: nblk * B].cpu().numpy()
+        out = np.empty(nblk * P, dtype=np.uint8)
 
         def run(a, b):
             fo, bad = ctypes.c_uint64(0), ctypes.c_int64(0)
-            L.oc_read_from_disk(blocks.ctypes.data + a * 4096, (b - a) * 4096, 4096, 0, (b - a) * 4092,
-                                out.ctypes.data + a * 4092, ctypes.byref(fo), ctypes.byref(bad))
-        what = f"oc_read_from_disk over {nblk} stamped 4096-B blocks (block_manager.go:189-242)"
-    nbytes = nblk * (4092 + 4096)
+            L.oc_read_from_disk(blocks.ctypes.data + a * B, (b - a) * B, B, 0, (b - a) * P,
+                                out.ctypes.data + a * P, ctypes.byref(fo), ctypes.byref(bad))
+        what = f"oc_read_from_disk over {nblk} stamped {B}-B blocks (block_manager.go:189-242)"
+    nbytes = nblk * (P + B)
     pool = ThreadPoolExecutor(threads)
 
     def par():  # ctypes releases the GIL for the call
         list(pool.map(lambda t: run(t * per_t, (t + 1) * per_t), range(threads)))
-    slices = _slices(par, per_t * threads * (4092 + 4096), budget_s)
+    slices = _slices(par, per_t * threads * (P + B), budget_s)
     one = _rate(lambda: run(0, nblk), nbytes, 0.3 * budget_s)
     pool.shutdown()
     return {"value": round(float(np.median(slices[0])), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
@@ -505,17 +512,18 @@ def main(argv=None):
         block_desc = "GetCRC per record: log-uniform 64 B - 64 KiB records back to back (off/len arrays)"
         k = int(np.searchsorted(off_h, 512 << 20))
         sample = (slice(0, int(off_h[k - 1]) + int(lens_h[k - 1])), off_h[:k].copy(), lens_h[:k].copy())
-    elif bsize == "unframe":
-        buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
-        crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
-        crc.dev_crc32_blocks(buf, None, stride=4096, ulen=4096, nblocks=my, flags=crc.HC_F_STAMP)
-        dst = torch.empty(my * 4092, dtype=torch.uint8, device=dev)
+    elif bsize in UNFRAME_B:
+        UB = UNFRAME_B[bsize]
+        buf = torch.empty(my * UB, dtype=torch.uint8, device=dev)
+        crc.dev_fill_range(buf, SEED, lo, my, stride=UB, ulen=UB)
+        crc.dev_crc32_blocks(buf, None, stride=UB, ulen=UB, nblocks=my, flags=crc.HC_F_STAMP)
+        dst = torch.empty(my * (UB - 4), dtype=torch.uint8, device=dev)
         bitmap = torch.empty((my + 31) // 32, dtype=torch.int32, device=dev)
         first_bad = torch.empty(1, dtype=torch.int64, device=dev)
         crc.dev_verify_prepare(bitmap, first_bad, my)
         kw = "unframe"
-        step_bytes = my * 4096 + my * 4092  # one read of the blocks + one write of the payload
-        block_desc = "ReadFromDisk: verify 4096-B blocks + strip CRCs"
+        step_bytes = my * UB + my * (UB - 4)  # one read of the blocks + one write of the payload
+        block_desc = f"ReadFromDisk: verify {UB}-B blocks + strip CRCs"
     else:
         if scatter_in:
             # the batch starts on rank 0's GPU: its shards go out by RCCL send/recv
@@ -546,7 +554,7 @@ def main(argv=None):
             if kw_ is None:
                 crc.dev_add_crcs(b, dst, crc_out=o, stream=stream)
             elif kw_ == "unframe":
-                crc.dev_read_blocks(b, 4096, out=dst, crc_out=o, bad_bitmap=bitmap, first_bad=first_bad,
+                crc.dev_read_blocks(b, UB, out=dst, crc_out=o, bad_bitmap=bitmap, first_bad=first_bad,
                                     stream=stream)
             else:
                 crc.dev_crc32_blocks(b, o, stream=stream, **kw_)
@@ -679,8 +687,9 @@ def main(argv=None):
         if not args.cpu_threads:
             args.cpu_threads = cores_available()
         if world == 1 and args.cpu_seconds > 0:
-            if bsize in ("frame", "unframe"):
-                cpu = cpu_baseline_framing(bsize, buf, args.cpu_threads, args.cpu_seconds)
+            if bsize == "frame" or bsize in UNFRAME_B:
+                cpu = cpu_baseline_framing("frame" if bsize == "frame" else "unframe", buf, args.cpu_threads,
+                                           args.cpu_seconds, B=UNFRAME_B.get(bsize, 4096))
             elif sample is not None:
                 sl, soff, slen = sample
                 host = buf[sl].cpu().numpy()

@@ -1261,9 +1261,8 @@ int hc_dev_read_blocks(int device, const void *blocks, uint64_t nblocks, uint32_
   if (st != HC_OK) return st;
   DeviceGuard g(device);
   DeviceState &d = g_dev[device];
-  const uint64_t per_wg = 4ull * std::max<uint32_t>(1u, kUnframeWaveGroups >> lg);
   hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4),
-                      (uint32_t)std::min<uint64_t>((nblocks + per_wg - 1) / per_wg, 0xFFFFFFFFull), 256, kLaneQWords * 4};
+                      (uint32_t)std::min<uint64_t>(unframe_grid(nblocks, lg), 0xFFFFFFFFull), 256, kLaneQWords * 4};
   t_last = info;
   return launch_unframe(static_cast<const uint8_t *>(blocks), nblocks, lg, static_cast<uint8_t *>(payload_out),
                         crc_out, bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), d.dtab,

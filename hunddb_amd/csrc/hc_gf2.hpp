@@ -78,6 +78,7 @@ struct DeviceTables {
   uint32_t w0;
   uint32_t pad[63];
   uint32_t lane_q[8][kLanes][4];
+  uint32_t sh4k[4][32];  // columns of shift(., 4096 (j+1) bytes), j = 0..2 (k_unframe's group combine); [3] unused
 };
 static_assert(sizeof(DeviceTables) % 256 == 0, "keep the image 256-B multiple");
 
@@ -95,6 +96,8 @@ inline void build_device_tables(DeviceTables &d) {
   for (int q = 0; q < 8; q++)
     for (uint32_t l = 0; l < kLanes; l++)
       for (int r = 0; r < 4; r++) d.lane_q[q][l][r] = d.lane[l][4 * q + r];
+  for (int j = 0; j < 4; j++)
+    for (int i = 0; i < 32; i++) d.sh4k[j][i] = j < 3 ? g.shift_bytes(1u << i, 4096ull * (j + 1)) : 0u;
 }
 
 // 32x32 GF(2) matrix by columns: c[i] = M e_i (host side only).

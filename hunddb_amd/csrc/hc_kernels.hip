@@ -1233,10 +1233,9 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
 // crc_util.go:88-100) and strip the CRC words, writing the payloads back to
 // back (block b's block[4:B] at out + b*(B-4)) -- the inverse of k_frame, one
 // read of the blocks and one write of the payload.  B = 4096 << lg_groups.
-//   * 4-wave workgroups, each wave one block (kUnframeWaveGroups = 1 in
-//     hc_kernels.hpp: 1, 2 or 4 groups of 4 KiB) in order, the next group's
-//     rows in flight while the current one is hashed and stored, then exit.
-//     The persistent 16-wave version with 144 KiB of LDS tables ran 5.0-5.2
+//   * 4-wave workgroups, each wave one 4 KiB block, or one 4 KiB group of an
+//     8/16 KiB block (the block's groups combined through LDS, below), then
+//     exit.  The persistent 16-wave version with 144 KiB of LDS tables ran 5.0-5.2
 //     TB/s; four blocks per wave with the placement columns loaded per lane
 //     5.45-5.62; one block per wave with them shared in LDS 6.04
 //     (tools/kframe3, profiles/r3/framing/, profiles/r3/framing_lq/).
@@ -1259,11 +1258,10 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef u32x4 u32x4_u __attribute__((aligned(1)));
   constexpr uint32_t kGroups = 1u << lg_groups, gmask = kGroups - 1u;
-  constexpr uint32_t K = kUnframeWaveGroups >> lg_groups > 0 ? kUnframeWaveGroups >> lg_groups : 1u;  // blocks per wave
   constexpr uint64_t B = (uint64_t)HC_FRAME_BLOCK << lg_groups, Bp = B - 4;
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
-  if constexpr (lg_groups == 0 && K == 1) {
+  if constexpr (lg_groups == 0) {
     // 4 KiB blocks, one a wave: straight-line code with a wave-uniform block
     // index.  The group loop below, with the index taken from threadIdx as a
     // VGPR (exec-masked branches), ran 6.5 % slower (tools/kframe4: 5490 vs
@@ -1315,64 +1313,72 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
       if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
       if (b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) lane0_atomic_umin64(first_bad, b);
     }
-    return;
-  }
-  const uint64_t b0 = ((uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6)) * K;
-  const uint64_t p_end = (b0 + K < nblk ? b0 + K : nblk) << lg_groups;  // this wave's groups [p0, p_end)
-  uint64_t p = b0 << lg_groups;
-  const uint32_t w0 = tables->w0;
-  u32x4 v[4];
-  auto load4 = [&](uint64_t q) {
-    const uint8_t *S = blocks + q * HC_FRAME_BLOCK + 16u * lane;
+  } else {
+    // 8/16 KiB blocks: one 4 KiB group per wave, a block's 2 or 4 groups in
+    // one workgroup.  Each wave hashes and stores its group exactly as a 4 KiB
+    // block (the group's raw CRC register r_g, zero init unless g = 0), shifts
+    // r_g past the groups after it (4096 * (G-1-g) bytes: a 32x32 mat-vec on a
+    // wave-uniform value, one column per lane, DeviceTables::sh4k), and the
+    // last group's wave XORs the block's r_g from LDS and reports.  One wave
+    // per block with the groups in turn (each group's rows prefetched during
+    // the previous one) ran 5.17-5.34 TB/s; every wave with one group's rows
+    // in flight is the 4 KiB kernel's pattern.
+    __shared__ uint32_t reg[4], st_word[4];
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const uint64_t q = (uint64_t)blockIdx.x * 4 + wave;  // global group index
+    const uint64_t b = q >> lg_groups;
+    const uint32_t g = (uint32_t)q & gmask;
+    const bool mine = b < nblk;
+    const uint32_t w0 = tables->w0;
+    u32x4 v[4];
+    if (mine) {
+      const uint8_t *S = blocks + b * B + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane;
 #pragma unroll
-    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
-  };
-  if (p < p_end) load4(p);  // the first group's rows before the table work
-  fill_lane_q(lq, tables);
-  const XTab TM = make_xtab(tables->tg, lane);
-  const XTab TS = make_xtab(tables->s4, lane);
-  __syncthreads();
-  uint32_t c[4] = {0, 0, 0, 0};
-  uint32_t stored = 0;
-  bool reported = false;  // wave-uniform: this wave already lowered first_bad
-  for (; p < p_end; p++) {
-    const uint64_t b = p >> lg_groups;
-    const uint32_t g = (uint32_t)p & gmask;
-    u32x4 cur[4] = {v[0], v[1], v[2], v[3]};
-    if ((K << lg_groups) > 1 && p + 1 < p_end) load4(p + 1);  // the next group in flight (none: one group a wave)
+      for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
+    }
+    fill_lane_q(lq, tables);
+    const XTab TM = make_xtab(tables->tg, lane);
+    const XTab TS = make_xtab(tables->s4, lane);
+    const uint32_t shcol = g < gmask ? tables->sh4k[gmask - 1u - g][lane & 31u] : 0u;
+    __syncthreads();
+    if (!mine) return;  // (ended waves do not hold up the barrier below)
+    uint32_t c[4] = {0, 0, 0, 0};
     uint8_t *ob = out + b * Bp + (uint64_t)g * HC_FRAME_BLOCK + 16u * lane - 4;
+    const bool head = g == 0 && lane == 0;  // the block's first 16 bytes: CRC field + 12 payload bytes
     u32x4 sv[4];
-    uint8_t *sa[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      u32x4 t = cur[r];
-      if (r == 0 && g == 0) {
+      u32x4 t = v[r];
+      sv[r] = t;
+      if (r == 0) {  // (selects, not branches: one store address form, a global store)
         const uint32_t nx = __builtin_amdgcn_update_dpp(0u, t.x, 0x101, 0xF, 0xF, false);  // lane+1's x
-        stored = __builtin_amdgcn_readfirstlane(t.x);                                         // LE32(block[0:4])
+        if (head) st_word[wave >> lg_groups] = t.x;                                           // LE32(block[0:4])
         const u32x4 first = {t.y, t.z, t.w, nx};
-        sv[r] = lane == 0 ? first : t;
-        sa[r] = ob + (lane == 0 ? 4 : 0);
-        t.x = lane == 0 ? w0 : t.x;  // Go's init in place of the CRC field
-      } else {
-        sv[r] = t;
-        sa[r] = ob + r * kRowBytes;
+        sv[r] = head ? first : t;
+        t.x = head ? w0 : t.x;  // Go's init in place of the CRC field
       }
       const uint32_t w[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-      for (int k = 0; k < 4; k++) c[k] = (r == 0 && g == 0) ? w[k] : xapply(TM, c[k], w[k]);
+      for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : xapply(TM, c[k], w[k]);
     }
 #pragma unroll
-    for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
-    if (g == gmask) {
-      const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
-      const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
-      if (crc_out) lane0_store_u32(crc_out + b, crcv);
-      if (first_bad && crcv != stored) {  // wave-uniform
-        if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
-        if (!reported && b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-          lane0_atomic_umin64(first_bad, b);
-        reported = true;  // a wave's blocks come in increasing order
-      }
+    for (int r = 0; r < 4; r++)
+      __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(ob + r * kRowBytes + (r == 0 && head ? 4 : 0)));
+    const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
+    uint32_t rg = wave_xor(place_lq(lq, lane, d));
+    if (g < gmask) rg = wave_xor(lane < 32 && ((rg >> lane) & 1u) ? shcol : 0u);  // shift(r_g, 4096 (G-1-g))
+    if (lane == 0) reg[wave] = rg;
+    __syncthreads();
+    if (g != gmask) return;
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kGroups; k++) tot ^= reg[wave - gmask + k];
+    const uint32_t crcv = tot ^ 0xFFFFFFFFu;
+    const uint32_t stored = st_word[wave >> lg_groups];
+    if (crc_out) lane0_store_u32(crc_out + b, crcv);
+    if (first_bad && crcv != stored) {  // one block a wave: at most one lowering
+      if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+      if (b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) lane0_atomic_umin64(first_bad, b);
     }
   }
 }
@@ -1884,8 +1890,7 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
                           const DeviceTables *tables, hipStream_t s) {
   if (nblk == 0) return hipSuccess;
   if (!blocks || !out || lg_groups > 2) return hipErrorInvalidValue;
-  const uint64_t per_wg = 4ull * (kUnframeWaveGroups >> lg_groups ? kUnframeWaveGroups >> lg_groups : 1u);  // blocks
-  const uint64_t grid = (nblk + per_wg - 1) / per_wg;
+  const uint64_t grid = unframe_grid(nblk, lg_groups);  // one 4 KiB group per wave, 4 waves per workgroup
   if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #define HC_UNFRAME(L)                                                                                      \
   hipLaunchKernelGGL((k_unframe<L>), dim3((unsigned)grid), dim3(256), 0, s, blocks, nblk, out, crc_out, bad_bitmap, \

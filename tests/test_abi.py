@@ -178,8 +178,11 @@ def test_debug_tables_consistent(hc):
     lane, w0 = t[2048:4096].reshape(64, 32), int(t[4096])
     # the placement columns regrouped for the workgroup-shared LDS copy (k_frame, k_unframe)
     lane_q = t[4160:4160 + 2048].reshape(8, 64, 4)
-    assert t.size == 4160 + 2048
+    # columns of shift(., 4096 (j+1) bytes), k_unframe's combine of an 8/16 KiB block's 4 KiB groups
+    sh4k = t[6208:6208 + 128].reshape(4, 32)
+    assert t.size == 4160 + 2048 + 128
     assert (lane_q.transpose(1, 0, 2).reshape(64, 32) == lane).all()
+    assert (sh4k[3] == 0).all()
 
     def tab(T, c):
         return T[0][c & 255] ^ T[1][(c >> 8) & 255] ^ T[2][(c >> 16) & 255] ^ T[3][c >> 24]
@@ -197,6 +200,29 @@ def test_debug_tables_consistent(hc):
         for i in range(32):
             e ^= np.where((d >> i) & 1, lane[:, i], 0).astype(np.uint32)
         assert (int(np.bitwise_xor.reduce(e)) ^ 0xFFFFFFFF) == zlib.crc32(blk[4:])
+
+    def mv(cols, v):
+        return int(np.bitwise_xor.reduce(np.where((v >> np.arange(32)) & 1, cols, 0).astype(np.uint32)))
+
+    # k_unframe at 8/16 KiB: each 4 KiB group hashed alone (W0 init in group 0,
+    # zero init after), placed, shifted past the groups after it, XORed
+    for B in (8192, 16384):
+        blk = rng.integers(0, 256, B, dtype=np.uint8).tobytes()
+        G = B // 4096
+        tot = 0
+        for g in range(G):
+            w = np.frombuffer(blk[4096 * g:4096 * (g + 1)], dtype="<u4").reshape(4, 64, 4).copy()
+            if g == 0:
+                w[0, 0, 0] = w0
+            c = w[0].copy()
+            for r in range(1, 4):
+                c = tab(tg, c) ^ w[r]
+            d = tab(s4, tab(s4, tab(s4, c[:, 0]) ^ c[:, 1]) ^ c[:, 2]) ^ c[:, 3]
+            rg = 0
+            for ln in range(64):
+                rg ^= mv(lane[ln], int(d[ln]))
+            tot ^= mv(sh4k[G - 2 - g], rg) if g < G - 1 else rg
+        assert tot ^ 0xFFFFFFFF == zlib.crc32(blk[4:]), B
 
 
 def test_batch_entries_fail_loudly_without_gpu(hc):
