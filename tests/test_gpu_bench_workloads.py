@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {
     "northstar": (4096, "k_crc_grp", 4096 * 8192),
     "verify": (4096, "k_crc_grp", 4096 * (8192 + 4)),
-    "config3": (4096, "k_crc_grp", None),
+    "config3": (4096, "k_crc_grp+k_crc_any", None),
     "frame": (4096, "k_frame", (4096 * 4092 - 1000) + 4096 * 4096),
     "unframe": (4096, "k_unframe", 4096 * (4096 + 4092)),
     "unframe8k": (2048, "k_unframe", 2048 * (8192 + 8188)),

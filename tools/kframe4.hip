@@ -263,6 +263,76 @@ __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64
     if (b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) lane0_atomic_umin64(first_bad, b);
   }
 }
+
+// 4 KiB k_unframe with the payload stores shifted by one word: lane l of row r
+// stores block bytes 1024r + 16l + 4 .. +19 at out_b + 1024r + 16l, i.e. its
+// own words y, z, w and lane l+1's x (DPP wave_shl:1; lane 63 takes lane 0's
+// x of the next row by v_readlane), so no two lanes' stores overlap (the
+// production head: lane 0 stores bytes 4..19, overlapping lane 1) and blocks'
+// output ranges meet without sharing bytes.  Row 3's lane 63 stores 12 bytes.
+__global__ __launch_bounds__(256) void k_unframe_nh(const uint8_t *blocks, uint64_t nblk,
+                                                    uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
+                                                    uint32_t *__restrict__ bad_bitmap,
+                                                    unsigned long long *__restrict__ first_bad,
+                                                    const DeviceTables *__restrict__ tables) {
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+  typedef u32x3 u32x3_u __attribute__((aligned(1)));
+  constexpr uint64_t Bp = HC_FRAME_BLOCK - 4;
+  __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool mine = b < nblk;
+  const uint32_t w0 = tables->w0;
+  u32x4 v[4];
+  if (mine) {
+    const uint8_t *S = blocks + b * HC_FRAME_BLOCK + 16u * lane;
+#pragma unroll
+    for (int r = 0; r < 4; r++) v[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(S + r * kRowBytes));
+  }
+  fill_lane_q(lq, tables);
+  const XTab TM = make_xtab(tables->tg, lane);
+  const XTab TS = make_xtab(tables->s4, lane);
+  __syncthreads();
+  if (!mine) return;
+  auto wave_shl1 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false); };
+  const uint32_t stored = __builtin_amdgcn_readfirstlane(v[0].x);
+  uint8_t *ob = out + b * Bp + 16u * lane;
+  u32x4 sv[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    uint32_t nx = wave_shl1(v[r].x);
+    if (r < 3) {
+      const uint32_t n0 = __builtin_amdgcn_readlane(v[r < 3 ? r + 1 : 3].x, 0);
+      nx = lane == 63 ? n0 : nx;
+    }
+    sv[r] = u32x4{v[r].y, v[r].z, v[r].w, nx};
+  }
+  uint32_t c[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    u32x4 t = v[r];
+    if (r == 0) t.x = lane == 0 ? w0 : t.x;
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : xapply(TM, c[k], w[k]);
+  }
+#pragma unroll
+  for (int r = 0; r < 3; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(ob + r * kRowBytes));
+  if (lane != 63) {
+    __builtin_nontemporal_store(sv[3], reinterpret_cast<u32x4_u *>(ob + 3 * kRowBytes));
+  } else {
+    const u32x3 t3 = {sv[3].x, sv[3].y, sv[3].z};
+    __builtin_nontemporal_store(t3, reinterpret_cast<u32x3_u *>(ob + 3 * kRowBytes));
+  }
+  const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
+  const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
+  if (crc_out) lane0_store_u32(crc_out + b, crcv);
+  if (first_bad && crcv != stored) {
+    if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+    if (b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) lane0_atomic_umin64(first_bad, b);
+  }
+}
 }  // namespace k4
 
 namespace {
@@ -355,6 +425,22 @@ int main(int argc, char **argv) {
       vs.push_back({"NULL unaligned loads", 0, false, [&](hipStream_t st) {
                       hipLaunchKernelGGL(k4::k_frame_unaligned_null, dim3(wgs), dim3(256), 0, st, src, npay, framed,
                                          nblk, crc);
+                    }, {}});
+    }
+    if (set == "u4") {  // what separates 4 KiB unframe from the 8/16 KiB form: the per-block epilogue?
+      vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
+      vs.push_back({"unframe, stores shifted one word (no overlap)", 1, true, [&](hipStream_t st) {
+                      hipLaunchKernelGGL(k4::k_unframe_nh, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, blocks,
+                                         N, pay, crc, bitmap, fb, dt);
+                    }, {}});
+      vs.push_back({"PROD k_unframe, no crc_out", 1, false, [&](hipStream_t st) {
+                      CK(hc::launch_unframe(blocks, N, 0, pay, nullptr, bitmap, fb, dt, st));
+                    }, {}});
+      vs.push_back({"PROD k_unframe, no crc_out, no verify", 1, false, [&](hipStream_t st) {
+                      CK(hc::launch_unframe(blocks, N, 0, pay, nullptr, nullptr, nullptr, dt, st));
+                    }, {}});
+      vs.push_back({"PROD k_unframe, crc_out, no verify", 1, false, [&](hipStream_t st) {
+                      CK(hc::launch_unframe(blocks, N, 0, pay, crc, nullptr, nullptr, dt, st));
                     }, {}});
     }
     if (set == "unframe" || set == "all") {
