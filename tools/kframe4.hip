@@ -86,7 +86,13 @@ __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src
     lq1 = g[threadIdx.x + 256u];
     __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the rows
   }
-  if (mine || kGlobal || kFillFirst) {
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  if constexpr (kTail == 3) {  // one unaligned 16-B load per lane: no tail, no funnel
+    const uint8_t *SP = kGlobal ? src + (bl * kPay - 4) : reinterpret_cast<const uint8_t *>(S);
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      C[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(SP + r * kRowBytes + 16u * lane));
+  } else if (mine || kGlobal || kFillFirst) {
 #pragma unroll
     for (int r = 0; r < 4; r++)
       C[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(SaP + r * kRowBytes + 16u * lane));
@@ -96,6 +102,7 @@ __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src
     for (int r = 0; r < 4; r++) X[r] = buf_load16(r63, lane == 63 ? (uint32_t)((r + 1) * kRowBytes) : 0xFFFFFFFFu);
   } else if constexpr (kTail == 1) {
     X[3] = buf_load16(r63, lane == 63 ? 4096u : 0xFFFFFFFFu);
+  } else if constexpr (kTail == 3) {
   } else {
     // the 16-B chunk after the block's 4096 bytes holds at least one byte of
     // src (b <= nblk-2 and the last block is non-empty), so it lies in src's
@@ -125,6 +132,10 @@ __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src
   u32x4 v[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
+    if constexpr (kTail == 3) {
+      v[r] = C[r];
+      continue;
+    }
     const uint4 a = make_uint4(C[r].x, C[r].y, C[r].z, C[r].w);
     uint4 nb = make_uint4(wave_shl1(a.x), wave_shl1(a.y), wave_shl1(a.z), wave_shl1(a.w));
     if constexpr (kTail == 0) {
@@ -426,6 +437,17 @@ int main(int argc, char **argv) {
                       hipLaunchKernelGGL(k4::k_frame_unaligned_null, dim3(wgs), dim3(256), 0, st, src, npay, framed,
                                          nblk, crc);
                     }, {}});
+    }
+    if (set == "ua") {  // k_frame with unaligned row loads in the late-round-3 structure
+      vs.push_back({"PROD k_frame", 0, true, prod, {}});
+      vs.push_back({"unaligned loads, flat, columns first", 0, true, KT(3, false, false, true), {}});
+      vs.push_back({"unaligned loads, global, columns first", 0, true, KT(3, false, true, true), {}});
+      vs.push_back({"unaligned loads, global", 0, true, KT(3, false, true), {}});
+      vs.push_back({"NULL unaligned loads (round 3 copy)", 0, false, [&](hipStream_t st) {
+                      hipLaunchKernelGGL(k4::k_frame_unaligned_null, dim3(wgs), dim3(256), 0, st, src, npay, framed,
+                                         nblk, crc);
+                    }, {}});
+      vs.push_back({"NULL tail 1 flat columns first", 0, false, KT(1, true, false, true), {}});
     }
     if (set == "u4") {  // what separates 4 KiB unframe from the 8/16 KiB form: the per-block epilogue?
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
