@@ -477,9 +477,10 @@ def main(argv=None):
         sample = (slice(0, k * 4096), np.arange(k, dtype=np.uint64) * 4096, np.full(k, 4096, np.uint32))
     elif bsize == "frame":
         npay = my * 4092 - 1000  # ragged last block
-        raw = torch.empty(npay + 1, dtype=torch.uint8, device=dev)
-        crc.dev_fill_range(raw, SEED, lo, 1, stride=npay + 1, ulen=npay + 1)
-        buf = raw[1:]  # payload at an odd address
+        rawn = (npay + 1 + (1 << 20) - 1) >> 20 << 20  # filled as 1 MiB blocks (one block of 4 GB is one wave's work)
+        raw = torch.empty(rawn, dtype=torch.uint8, device=dev)
+        crc.dev_fill_range(raw, SEED, lo << 20, rawn >> 20, stride=1 << 20, ulen=1 << 20)
+        buf = raw[1:npay + 1]  # payload at an odd address
         dst = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
         kw = None
         step_bytes = npay + my * 4096  # one read of the payload + one write of the blocks
