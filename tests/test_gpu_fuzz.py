@@ -303,3 +303,55 @@ def test_random_multi_gpu_plans(cuda, hc, oracle, seed):
     err, bm, fb = hc.multi_verify_blocks(base, [0] * ndev, off=off, lens=lens, stride=stride, ulen=ulen, nblocks=n,
                                          bounds=bounds)
     assert np.array_equal(bm, bm1) and fb == fb1 and str(err) == str(err1)
+
+
+N_UNFRAME = 24
+
+
+@pytest.mark.parametrize("seed", range(N_UNFRAME))
+def test_random_dev_read_blocks(cuda, hc, oracle, seed):
+    """Row f1 on the device at every block size (k_unframe: one wave per 4 KiB
+    block; one wave per 4 KiB group of an 8/16 KiB block, the groups combined
+    through LDS): random block counts (odd ones leave part of the last
+    workgroup idle), random corruption (none, one, several, the first, the
+    last, every block), against the oracle's CRCs: payload bytes, CRC words,
+    the verify bitmap and first_bad."""
+    torch = cuda
+    rng = np.random.default_rng(9000 + seed)
+    B = [4096, 8192, 16384][seed % 3]
+    n = int(rng.choice([1, 2, 3, 5, int(rng.integers(1, 64)), int(rng.integers(64, 3000))]))
+    raw = rng.integers(0, 256, n * B, dtype=np.uint8)
+    raw.view(np.uint32).reshape(n, B // 4)[:, 0] = oracle.crc32_blocks(raw, stride=B, ulen=B)
+    mode = seed % 6
+    if mode == 1:
+        bad = [int(rng.integers(0, n))]
+    elif mode == 2:
+        bad = sorted(set(rng.integers(0, n, 1 + n // 50).tolist()))
+    elif mode == 3:
+        bad = [0]
+    elif mode == 4:
+        bad = [n - 1]
+    elif mode == 5:
+        bad = list(range(n))
+    else:
+        bad = []
+    for i in bad:  # a flipped bit anywhere in the block: payload or the stored word
+        raw[i * B + int(rng.integers(0, B))] ^= 1 << int(rng.integers(0, 8))
+    want = oracle.crc32_blocks(raw, stride=B, ulen=B)
+    stored = raw.view(np.uint32).reshape(n, B // 4)[:, 0]
+    want_bad = np.nonzero(stored != want)[0]
+    d = torch.from_numpy(raw).cuda()
+    bm = torch.empty((n + 31) // 32, dtype=torch.int32, device="cuda")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda")
+    crcs = torch.empty(n, dtype=torch.int32, device="cuda")
+    hc.dev_verify_prepare(bm, fb, n)
+    out = torch.full((n * (B - 4) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    hc.dev_read_blocks(d, B, out=out, crc_out=crcs, bad_bitmap=bm, first_bad=fb)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert got[: n * (B - 4)].tobytes() == raw.reshape(n, B)[:, 4:].tobytes()
+    assert (got[n * (B - 4):] == 0xA5).all()
+    assert (crcs.cpu().numpy().view(np.uint32) == want).all()
+    bits = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    assert np.nonzero(bits)[0].tolist() == want_bad.tolist()
+    assert int(fb.item()) == (int(want_bad[0]) if len(want_bad) else 2**63 - 1)
