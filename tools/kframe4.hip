@@ -449,6 +449,17 @@ int main(int argc, char **argv) {
                     }, {}});
       vs.push_back({"NULL tail 1 flat columns first", 0, false, KT(1, true, false, true), {}});
     }
+    if (set == "occ") {  // 4 KiB unframe at capped occupancy: dynamic LDS padding limits workgroups per CU
+      vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
+      for (uint32_t pad : {0u, 24u, 32u, 40u, 56u}) {
+        char nm[96];
+        std::snprintf(nm, sizeof nm, "unframe copy + %u KiB LDS pad (%u WGs/CU by LDS)", pad, 160u / (8u + pad));
+        vs.push_back({nm, 1, pad == 0, [&, pad](hipStream_t st) {
+                        hipLaunchKernelGGL(k4::k_unframe_t<false>, dim3((unsigned)((N + 3) / 4)), dim3(256), pad << 10,
+                                           st, blocks, N, pay, crc, bitmap, fb, dt);
+                      }, {}});
+      }
+    }
     if (set == "u4") {  // what separates 4 KiB unframe from the 8/16 KiB form: the per-block epilogue?
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
       vs.push_back({"unframe, stores shifted one word (no overlap)", 1, true, [&](hipStream_t st) {
