@@ -76,7 +76,7 @@ WORKLOADS = {
     # bytes read + 4-B words written
     "records": (2_000_000, "records", "weak"),
 }
-# the dominant kernel per workload (PMC passes); frame's k_frame_edges (2 blocks) is left out
+# the dominant kernel per workload (PMC passes)
 KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
              "records": "k_seg_stream"}  # else the streaming CRC kernel
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes

@@ -1098,12 +1098,12 @@ __device__ __forceinline__ uint32_t place_lq(const uint32_t *lq, uint32_t lane, 
 // ---------------------------------------------------------------------------
 // Fused AddCRCsToData (utils/crc/crc_util.go:41-64, row f2): payload slices of
 // 4092 B -> 4096-B blocks with the CRC in front, one read of the payload and
-// one write of the blocks.  Two launches (launch_frame):
-//   k_frame_edges  the first block (row 0 would start 4 bytes before src) and
+// one write of the blocks.  One launch of k_frame (launch_frame):
+//   workgroup 0    the first block (row 0 would start 4 bytes before src) and
 //                  the last (ragged payload): aligned, range-predicated loads,
 //                  funnel shift and byte masks, one wave each -- no byte
-//                  outside src is touched.
-//   k_frame        interior blocks 1 .. nblk-2: every row window lies inside
+//                  outside src is touched (frame_edges_wave).
+//   the others     interior blocks 1 .. nblk-2: every row window lies inside
 //                  src, so each lane's 16 output bytes come from two aligned
 //                  16-B chunks (its own and its neighbour's, by DPP) without
 //                  masks.  One block per wave, 4-wave workgroups that exit:
@@ -1113,24 +1113,24 @@ __device__ __forceinline__ uint32_t place_lq(const uint32_t *lq, uint32_t lane, 
 //                  before the hash (the other orders within +-0.5 %).
 // Round 2's kernel (persistent 16-wave workgroups, 144 KiB of LDS tables)
 // ran 5.10-5.24 TB/s; this one 5.26-5.48 on the same boxes (tools/kframe3).
-__global__ __launch_bounds__(128) void k_frame_edges(const uint8_t *__restrict__ src, uint64_t n,
-                                                     uint8_t *__restrict__ dst, uint64_t nblk,
-                                                     uint32_t *__restrict__ crc_out,
-                                                     const DeviceTables *__restrict__ tables) {
-  const uint32_t lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
-  if (wv == 1 && nblk < 2) return;
+// The first block (row 0 would start 4 bytes before src) and the last (ragged
+// payload), by waves 0 and 1 of k_frame's workgroup 0 (the workgroup's columns
+// in LDS already; waves 2 and 3 only help fill them).  Aligned,
+// range-predicated loads, funnel shift and byte masks: no byte outside src is
+// touched.  Until late round 3 this was its own launch (k_frame_edges, ~5 us
+// plus the gap between the two kernels, ~0.4 % of a 1M-block call).
+__device__ __forceinline__ void frame_edges_wave(const uint8_t *__restrict__ src, uint64_t n,
+                                                 uint8_t *__restrict__ dst, uint64_t nblk,
+                                                 uint32_t *__restrict__ crc_out, const uint32_t *lq,
+                                                 const XTab &TM, const XTab &TS, uint32_t w0, uint32_t lane,
+                                                 uint32_t wv) {
   const uint64_t b = wv == 0 ? 0 : nblk - 1;
-  uint32_t col[32];
-#pragma unroll
-  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  const XTab TM = make_xtab(tables->tg, lane);
-  const XTab TS = make_xtab(tables->s4, lane);
   auto row_step = [&](uint32_t c, uint32_t w) -> uint32_t { return xapply(TM, c, w); };
   uint32_t c[4];
   uint4 keep;
-  frame_edge_rows(b, src, n, dst, lane, tables->w0, row_step, c, keep);
+  frame_edge_rows(b, src, n, dst, lane, w0, row_step, c, keep);
   const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
-  const uint32_t crcv = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
+  const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
   if (lane == 0) {
     keep.x = crcv;  // binary.LittleEndian.PutUint32(block[:4], crc)
     *reinterpret_cast<uint4 *>(dst + b * (uint64_t)HC_FRAME_BLOCK) = keep;
@@ -1145,7 +1145,16 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
   constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6);  // interior block
+  if (blockIdx.x == 0) {  // the edge blocks first (dispatched early, overlapped with the interior)
+    fill_lane_q(lq, tables);
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const XTab TM = make_xtab(tables->tg, lane);
+    const XTab TS = make_xtab(tables->s4, lane);
+    __syncthreads();
+    if (wv == 0 || (wv == 1 && nblk >= 2)) frame_edges_wave(src, n, dst, nblk, crc_out, lq, TM, TS, tables->w0, lane, wv);
+    return;
+  }
+  const uint64_t b = 1 + (uint64_t)(blockIdx.x - 1) * 4 + uni(threadIdx.x >> 6);  // interior block
   const bool mine = b + 1 < nblk;
   // A wave past the last interior block loads block 1's rows (interior
   // whenever this kernel runs) and exits after the barrier: no branch around
@@ -1876,12 +1885,10 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
                         const DeviceTables *tables, int grid, hipStream_t s) {
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_frame_edges, dim3(1), dim3(128), 0, s, src, n, dst, nblk, crc_out, tables);
-  if (nblk > 2) {
-    const uint64_t wgs = (nblk - 2 + 3) / 4;  // one interior block per wave
-    if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, n, dst, nblk, crc_out, tables);
-  }
+  // workgroup 0: the two edge blocks; then one interior block per wave
+  const uint64_t wgs = 1 + (nblk > 2 ? (nblk - 2 + 3) / 4 : 0);
+  if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, n, dst, nblk, crc_out, tables);
   return hipGetLastError();
 }
 

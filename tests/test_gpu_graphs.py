@@ -7,7 +7,7 @@ graph is replayed after the inputs change and checked against the oracle:
 uniform blocks (k_crc_grp), unaligned messages (k_crc_any), packed records
 (the k_seg_* dispatch: its workspace comes from the stream-ordered allocator
 inside the graph), verify mode with its bitmap reset (k_verify_prepare), and
-the framing pair (k_frame_edges + k_frame, k_unframe)."""
+the framing pair (k_frame, k_unframe)."""
 import numpy as np
 import pytest
 
