@@ -476,6 +476,19 @@ int main(int argc, char **argv) {
                     }, {}});
       vs.push_back({"NULL tail 1 flat columns first", 0, false, KT(1, true, false, true), {}});
     }
+    if (set == "occf") {  // k_frame at capped occupancy (dynamic LDS padding), edges in their own launch
+      vs.push_back({"PROD k_frame (edges in workgroup 0, 68 VGPRs)", 0, true, prod, {}});
+      for (uint32_t pad : {0u, 12u, 16u, 24u, 32u}) {
+        char nm[96];
+        std::snprintf(nm, sizeof nm, "tail 1 flat FF + %u KiB LDS pad (%u WGs/CU by LDS)", pad, 160u / (8u + pad));
+        vs.push_back({nm, 0, pad == 0, [&, pad](hipStream_t st) {
+                        hipLaunchKernelGGL(k4::k_frame_edges_old, dim3(1), dim3(128), 0, st, src, npay, framed, nblk,
+                                           crc, dt);
+                        hipLaunchKernelGGL((k4::k_frame_t<1, false, false, true>), dim3(wgs), dim3(256), pad << 10, st,
+                                           src, npay, framed, nblk, crc, dt);
+                      }, {}});
+      }
+    }
     if (set == "occ") {  // 4 KiB unframe at capped occupancy: dynamic LDS padding limits workgroups per CU
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
       for (uint32_t pad : {0u, 24u, 32u, 40u, 56u}) {
