@@ -1095,6 +1095,18 @@ __device__ __forceinline__ uint32_t place_lq(const uint32_t *lq, uint32_t lane, 
   return acc;
 }
 
+// XCD-contiguous workgroup order for the short-lived framing kernels:
+// workgroup i is dispatched to XCD i % 8, so it takes logical workgroup
+// (i % 8) * (G8 / 8) + i / 8 (G8 = G rounded down to a multiple of 8; the last
+// G % 8 keep their index).  Each XCD's L2 then sees one contiguous stretch of
+// blocks, and the 128-B lines that neighbouring blocks share (4092-B payload
+// strides) meet in one L2 instead of two: +4.6-5 % for k_frame and k_unframe
+// (tools/kframe4 KF4_SET=xcd, profiles/r3/kframe4/).
+__device__ __forceinline__ uint32_t xcd_wg(uint32_t i, uint32_t G) {
+  const uint32_t G8 = G & ~7u;
+  return i < G8 ? (i & 7u) * (G8 >> 3) + (i >> 3) : i;
+}
+
 // ---------------------------------------------------------------------------
 // Fused AddCRCsToData (utils/crc/crc_util.go:41-64, row f2): payload slices of
 // 4092 B -> 4096-B blocks with the CRC in front, one read of the payload and
@@ -1145,7 +1157,8 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
   constexpr uint64_t kPay = 4092;  // BLOCK_SIZE - CRC_SIZE (crc_util.go:43)
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
-  if (blockIdx.x == 0) {  // the edge blocks first (dispatched early, overlapped with the interior)
+  const uint32_t wg = xcd_wg(blockIdx.x, gridDim.x);  // logical workgroup (workgroup 0 stays 0)
+  if (wg == 0) {  // the edge blocks first (dispatched early, overlapped with the interior)
     fill_lane_q(lq, tables);
     const uint32_t wv = uni(threadIdx.x >> 6);
     const XTab TM = make_xtab(tables->tg, lane);
@@ -1154,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
     if (wv == 0 || (wv == 1 && nblk >= 2)) frame_edges_wave(src, n, dst, nblk, crc_out, lq, TM, TS, tables->w0, lane, wv);
     return;
   }
-  const uint64_t b = 1 + (uint64_t)(blockIdx.x - 1) * 4 + uni(threadIdx.x >> 6);  // interior block
+  const uint64_t b = 1 + (uint64_t)(wg - 1) * 4 + uni(threadIdx.x >> 6);  // interior block
   const bool mine = b + 1 < nblk;
   // A wave past the last interior block loads block 1's rows (interior
   // whenever this kernel runs) and exits after the barrier: no branch around
@@ -1276,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
     // VGPR (exec-masked branches), ran 6.5 % slower (tools/kframe4: 5490 vs
     // 5830-5850 GB/s).  `blocks` is not __restrict__: with it, hipcc may sink
     // the row loads past the barrier into the block that uses them.
-    const uint64_t b = (uint64_t)blockIdx.x * 4 + uni(threadIdx.x >> 6);
+    const uint64_t b = (uint64_t)xcd_wg(blockIdx.x, gridDim.x) * 4 + uni(threadIdx.x >> 6);
     const bool mine = b < nblk;
     const uint32_t w0 = tables->w0;
     u32x4 v[4];
@@ -1334,7 +1347,7 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
     // in flight is the 4 KiB kernel's pattern.
     __shared__ uint32_t reg[4], st_word[4];
     const uint32_t wave = uni(threadIdx.x >> 6);
-    const uint64_t q = (uint64_t)blockIdx.x * 4 + wave;  // global group index
+    const uint64_t q = (uint64_t)xcd_wg(blockIdx.x, gridDim.x) * 4 + wave;  // global group index
     const uint64_t b = q >> lg_groups;
     const uint32_t g = (uint32_t)q & gmask;
     const bool mine = b < nblk;

@@ -49,7 +49,16 @@ __device__ __forceinline__ uint4 rl0(const u32x4 v) {  // lane 0's chunk, wave-u
                     __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
 }
 
-template <int kTail, bool kNull, bool kGlobal = true, bool kFillFirst = false>
+
+// XCD-contiguous workgroup order (A/B): workgroup i runs on XCD i % 8; map it to
+// logical workgroup (i % 8) * (G / 8) + i / 8 so each XCD's L2 sees one
+// contiguous stretch of blocks (the shared boundary lines of neighbouring
+// blocks then meet in one L2).  The last G % 8 workgroups keep their index.
+__device__ __forceinline__ uint32_t xcd_wg(uint32_t i, uint32_t G) {
+  const uint32_t G8 = G & ~7u;
+  return i < G8 ? (i & 7u) * (G8 >> 3) + (i >> 3) : i;
+}
+template <int kTail, bool kNull, bool kGlobal = true, bool kFillFirst = false, bool kXcd = false>
 __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src, uint64_t n,
                                                  uint8_t *__restrict__ dst, uint64_t nblk,
                                                  uint32_t *__restrict__ crc_out,
@@ -58,7 +67,8 @@ __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src
   __shared__ __attribute__((aligned(16))) uint32_t lq[kNull ? 4 : kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t b = 1 + (uint64_t)blockIdx.x * 4 + wv;  // interior block
+  const uint32_t wg = kXcd ? xcd_wg(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t b = 1 + (uint64_t)wg * 4 + wv;  // interior block
   const bool mine = b + 1 < nblk;
   // kGlobal: a wave past the last interior block loads block 1's rows (always
   // interior when this kernel runs) instead of branching around its loads, so
@@ -203,7 +213,7 @@ __global__ __launch_bounds__(256) void k_frame_unaligned_null(const uint8_t *__r
 // load is unconditional (a wave past the end reads block 0 and exits), so the
 // LDS writes and the barrier wait only for the columns (L2 hits), not for
 // every wave's rows (production: vmcnt(0) before the LDS writes).
-template <bool kFillFirst>
+template <bool kFillFirst, bool kXcd = false>
 __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64_t nblk,  // not restrict: loads stay before the barrier's fence
                                                    uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
                                                    uint32_t *__restrict__ bad_bitmap,
@@ -213,7 +223,8 @@ __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64
   constexpr uint64_t Bp = HC_FRAME_BLOCK - 4;
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t b = (uint64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wg = kXcd ? xcd_wg(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t b = (uint64_t)wg * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool mine = b < nblk;
   const uint32_t w0 = tables->w0;
   u32x4 v[4];
@@ -475,6 +486,17 @@ int main(int argc, char **argv) {
                                          nblk, crc);
                     }, {}});
       vs.push_back({"NULL tail 1 flat columns first", 0, false, KT(1, true, false, true), {}});
+    }
+    if (set == "xcd") {  // XCD-contiguous workgroup order for the short-lived framing kernels
+      vs.push_back({"PROD k_frame", 0, true, prod, {}});
+      vs.push_back({"frame tail 1 flat FF (2 launches)", 0, true, KT(1, false, false, true), {}});
+      vs.push_back({"frame tail 1 flat FF, XCD-contiguous WGs", 0, true, KT(1, false, false, true, true), {}});
+      vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
+      vs.push_back({"unframe copy", 1, true, KU(false), {}});
+      vs.push_back({"unframe copy, XCD-contiguous WGs", 1, true, [&](hipStream_t st) {
+                      hipLaunchKernelGGL((k4::k_unframe_t<false, true>), dim3((unsigned)((N + 3) / 4)), dim3(256), 0,
+                                         st, blocks, N, pay, crc, bitmap, fb, dt);
+                    }, {}});
     }
     if (set == "occf") {  // k_frame at capped occupancy (dynamic LDS padding), edges in their own launch
       vs.push_back({"PROD k_frame (edges in workgroup 0, 68 VGPRs)", 0, true, prod, {}});
