@@ -1586,8 +1586,10 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   // for short spans: every workgroup gets at least 4 chunks
   while (lg_chunk > 0 && (M >> lg_chunk) < G * 4) lg_chunk--;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
+  // each XCD's workgroups own neighbouring chunk slots (as k_crc_grp's kXcd)
+  const uint64_t wgx = (G & 7u) == 0 ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   auto unit_of = [&](uint32_t k) -> uint64_t {
-    return (((uint64_t)(k >> lg_chunk) * G + blockIdx.x) << lg_chunk) | (k & cmask);
+    return (((uint64_t)(k >> lg_chunk) * G + wgx) << lg_chunk) | (k & cmask);
   };
   auto unit_rsrc = [&](uint64_t u) {
     const uint64_t U = geo.a0 + (u << kU);
