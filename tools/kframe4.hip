@@ -491,6 +491,8 @@ int main(int argc, char **argv) {
       vs.push_back({"PROD k_frame", 0, true, prod, {}});
       vs.push_back({"frame tail 1 flat FF (2 launches)", 0, true, KT(1, false, false, true), {}});
       vs.push_back({"frame tail 1 flat FF, XCD-contiguous WGs", 0, true, KT(1, false, false, true, true), {}});
+      vs.push_back({"NULL frame tail 1 flat FF, XCD-contiguous WGs", 0, false, KT(1, true, false, true, true), {}});
+      vs.push_back({"NULL frame tail 1 flat FF", 0, false, KT(1, true, false, true), {}});
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
       vs.push_back({"unframe copy", 1, true, KU(false), {}});
       vs.push_back({"unframe copy, XCD-contiguous WGs", 1, true, [&](hipStream_t st) {
