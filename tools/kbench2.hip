@@ -238,6 +238,8 @@ int main(int argc, char **argv) {
       add("grp pinned C=128", true, GRP(false, true, false, 7, true));
       add("grp XCD-contiguous C=16", true, GRP(false, true, false, 4, true, false, true));
       add("grp XCD-contiguous C=32", true, GRP(false, true, false, 5, true, false, true));
+      add("grp XCD-contiguous C=64", true, GRP(false, true, false, 6, true, false, true));
+      add("grp XCD-contiguous C=128", true, GRP(false, true, false, 7, true, false, true));
       add("PROD launch_grp (again)", true, [&](hipStream_t st) { launch_grp(b, cus, st); });
       add("grp pinned C=128 (round-2 r1 production at 8/16 KiB)", true, GRP(false, true, false, 7, true));
     }
