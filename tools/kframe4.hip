@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_frame_unaligned_null(const uint8_t *__r
 // load is unconditional (a wave past the end reads block 0 and exits), so the
 // LDS writes and the barrier wait only for the columns (L2 hits), not for
 // every wave's rows (production: vmcnt(0) before the LDS writes).
-template <bool kFillFirst, bool kXcd = false>
+template <bool kFillFirst, bool kXcd = false, bool kEndBar = false>
 __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64_t nblk,  // not restrict: loads stay before the barrier's fence
                                                    uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
                                                    uint32_t *__restrict__ bad_bitmap,
@@ -251,7 +251,11 @@ __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64
   const XTab TM = make_xtab(tables->tg, lane);
   const XTab TS = make_xtab(tables->s4, lane);
   __syncthreads();
-  if (!mine) return;
+  if (!kEndBar && !mine) return;
+  if (kEndBar && !mine) {
+    __syncthreads();
+    return;
+  }
   uint32_t c[4] = {0, 0, 0, 0};
   uint32_t stored = 0;
   uint8_t *ob = out + b * Bp + 16u * lane - 4;
@@ -284,6 +288,7 @@ __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64
     if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
     if (b < __hip_atomic_load(first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) lane0_atomic_umin64(first_bad, b);
   }
+  if constexpr (kEndBar) __syncthreads();  // the workgroup's waves exit together
 }
 
 // 4 KiB k_unframe with the payload stores shifted by one word: lane l of row r
@@ -495,6 +500,10 @@ int main(int argc, char **argv) {
       vs.push_back({"NULL frame tail 1 flat FF", 0, false, KT(1, true, false, true), {}});
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
       vs.push_back({"unframe copy", 1, true, KU(false), {}});
+      vs.push_back({"unframe copy, XCD, waves exit together", 1, true, [&](hipStream_t st) {
+                      hipLaunchKernelGGL((k4::k_unframe_t<false, true, true>), dim3((unsigned)((N + 3) / 4)), dim3(256), 0,
+                                         st, blocks, N, pay, crc, bitmap, fb, dt);
+                    }, {}});
       vs.push_back({"unframe copy, XCD-contiguous WGs", 1, true, [&](hipStream_t st) {
                       hipLaunchKernelGGL((k4::k_unframe_t<false, true>), dim3((unsigned)((N + 3) / 4)), dim3(256), 0,
                                          st, blocks, N, pay, crc, bitmap, fb, dt);
