@@ -1289,7 +1289,13 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
     // VGPR (exec-masked branches), ran 6.5 % slower (tools/kframe4: 5490 vs
     // 5830-5850 GB/s).  `blocks` is not __restrict__: with it, hipcc may sink
     // the row loads past the barrier into the block that uses them.
-    const uint64_t b = (uint64_t)xcd_wg(blockIdx.x, gridDim.x) * 4 + uni(threadIdx.x >> 6);
+    // Logical workgroup L (XCD-contiguous) takes blocks 16 (L / 4) + 4 w + L % 4:
+    // b mod 4 fixes the output's misalignment (4092 b mod 16), so the four
+    // waves of a workgroup store with one alignment (+1.1 % over four
+    // consecutive blocks, tools/kframe4 KF4_SET=xcd); the grid is a multiple
+    // of 4 workgroups (unframe_grid) so every group of 16 blocks is covered.
+    const uint32_t L = xcd_wg(blockIdx.x, gridDim.x);
+    const uint64_t b = 16ull * (L >> 2) + 4u * uni(threadIdx.x >> 6) + (L & 3u);
     const bool mine = b < nblk;
     const uint32_t w0 = tables->w0;
     u32x4 v[4];

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_frame_unaligned_null(const uint8_t *__r
 // load is unconditional (a wave past the end reads block 0 and exits), so the
 // LDS writes and the barrier wait only for the columns (L2 hits), not for
 // every wave's rows (production: vmcnt(0) before the LDS writes).
-template <bool kFillFirst, bool kXcd = false, bool kEndBar = false>
+template <bool kFillFirst, bool kXcd = false, bool kEndBar = false, bool kMis = false>
 __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64_t nblk,  // not restrict: loads stay before the barrier's fence
                                                    uint8_t *__restrict__ out, uint32_t *__restrict__ crc_out,
                                                    uint32_t *__restrict__ bad_bitmap,
@@ -224,7 +224,10 @@ __global__ __launch_bounds__(256) void k_unframe_t(const uint8_t *blocks, uint64
   __shared__ __attribute__((aligned(16))) uint32_t lq[kLaneQWords];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wg = kXcd ? xcd_wg(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint64_t b = (uint64_t)wg * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // kMis: workgroup L of a group of four takes blocks 16(L/4) + 4w + L%4, so its
+  // four waves' outputs share one misalignment (b mod 4 fixes 4092 b mod 16)
+  const uint32_t wvi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t b = kMis ? 16ull * (wg >> 2) + 4u * wvi + (wg & 3u) : (uint64_t)wg * 4 + wvi;
   const bool mine = b < nblk;
   const uint32_t w0 = tables->w0;
   u32x4 v[4];
@@ -500,6 +503,10 @@ int main(int argc, char **argv) {
       vs.push_back({"NULL frame tail 1 flat FF", 0, false, KT(1, true, false, true), {}});
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
       vs.push_back({"unframe copy", 1, true, KU(false), {}});
+      vs.push_back({"unframe copy, XCD, one misalignment per WG", 1, true, [&](hipStream_t st) {
+                      hipLaunchKernelGGL((k4::k_unframe_t<false, true, false, true>), dim3((unsigned)(4 * ((N + 15) / 16))),
+                                         dim3(256), 0, st, blocks, N, pay, crc, bitmap, fb, dt);
+                    }, {}});
       vs.push_back({"unframe copy, XCD, waves exit together", 1, true, [&](hipStream_t st) {
                       hipLaunchKernelGGL((k4::k_unframe_t<false, true, true>), dim3((unsigned)((N + 3) / 4)), dim3(256), 0,
                                          st, blocks, N, pay, crc, bitmap, fb, dt);
