@@ -1167,7 +1167,12 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
     if (wv == 0 || (wv == 1 && nblk >= 2)) frame_edges_wave(src, n, dst, nblk, crc_out, lq, TM, TS, tables->w0, lane, wv);
     return;
   }
-  const uint64_t b = 1 + (uint64_t)(wg - 1) * 4 + uni(threadIdx.x >> 6);  // interior block
+  // interior logical workgroup I = wg - 1 takes interior blocks 16 (I / 4) +
+  // 4 w + I % 4: b mod 4 fixes the source's misalignment (4092 b mod 16), so a
+  // workgroup's four waves share it (+2-4 %, tools/kframe4 KF4_SET=xcd); the
+  // interior grid is a multiple of 4 workgroups (launch_frame)
+  const uint32_t I = wg - 1;
+  const uint64_t b = 1 + 16ull * (I >> 2) + 4u * uni(threadIdx.x >> 6) + (I & 3u);  // interior block
   const bool mine = b + 1 < nblk;
   // A wave past the last interior block loads block 1's rows (interior
   // whenever this kernel runs) and exits after the barrier: no branch around
@@ -1906,8 +1911,9 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
                         const DeviceTables *tables, int grid, hipStream_t s) {
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
-  // workgroup 0: the two edge blocks; then one interior block per wave
-  const uint64_t wgs = 1 + (nblk > 2 ? (nblk - 2 + 3) / 4 : 0);
+  // workgroup 0: the two edge blocks; then one interior block per wave, in
+  // groups of 16 blocks over 4 workgroups
+  const uint64_t wgs = 1 + (nblk > 2 ? 4 * ((nblk - 2 + 15) / 16) : 0);
   if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, n, dst, nblk, crc_out, tables);
   return hipGetLastError();

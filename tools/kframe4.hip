@@ -58,7 +58,7 @@ __device__ __forceinline__ uint32_t xcd_wg(uint32_t i, uint32_t G) {
   const uint32_t G8 = G & ~7u;
   return i < G8 ? (i & 7u) * (G8 >> 3) + (i >> 3) : i;
 }
-template <int kTail, bool kNull, bool kGlobal = true, bool kFillFirst = false, bool kXcd = false>
+template <int kTail, bool kNull, bool kGlobal = true, bool kFillFirst = false, bool kXcd = false, bool kMis = false>
 __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src, uint64_t n,
                                                  uint8_t *__restrict__ dst, uint64_t nblk,
                                                  uint32_t *__restrict__ crc_out,
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void k_frame_t(const uint8_t *__restrict__ src
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wg = kXcd ? xcd_wg(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint64_t b = 1 + (uint64_t)wg * 4 + wv;  // interior block
+  const uint64_t b = 1 + (kMis ? 16ull * (wg >> 2) + 4u * wv + (wg & 3u) : (uint64_t)wg * 4 + wv);  // interior block
   const bool mine = b + 1 < nblk;
   // kGlobal: a wave past the last interior block loads block 1's rows (always
   // interior when this kernel runs) instead of branching around its loads, so
@@ -499,6 +499,12 @@ int main(int argc, char **argv) {
       vs.push_back({"PROD k_frame", 0, true, prod, {}});
       vs.push_back({"frame tail 1 flat FF (2 launches)", 0, true, KT(1, false, false, true), {}});
       vs.push_back({"frame tail 1 flat FF, XCD-contiguous WGs", 0, true, KT(1, false, false, true, true), {}});
+      vs.push_back({"frame tail 1 flat FF, XCD, one misalignment per WG", 0, true, [&](hipStream_t st) {
+                      hipLaunchKernelGGL(k4::k_frame_edges_old, dim3(1), dim3(128), 0, st, src, npay, framed, nblk, crc, dt);
+                      hipLaunchKernelGGL((k4::k_frame_t<1, false, false, true, true, true>),
+                                         dim3((unsigned)(4 * ((nblk - 2 + 15) / 16))), dim3(256), 0, st, src, npay,
+                                         framed, nblk, crc, dt);
+                    }, {}});
       vs.push_back({"NULL frame tail 1 flat FF, XCD-contiguous WGs", 0, false, KT(1, true, false, true, true), {}});
       vs.push_back({"NULL frame tail 1 flat FF", 0, false, KT(1, true, false, true), {}});
       vs.push_back({"PROD k_unframe", 1, true, prod_u, {}});
