@@ -1358,9 +1358,14 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
     // in flight is the 4 KiB kernel's pattern.
     __shared__ uint32_t reg[4], st_word[4];
     const uint32_t wave = uni(threadIdx.x >> 6);
-    const uint64_t q = (uint64_t)xcd_wg(blockIdx.x, gridDim.x) * 4 + wave;  // global group index
-    const uint64_t b = q >> lg_groups;
-    const uint32_t g = (uint32_t)q & gmask;
+    const uint32_t L = xcd_wg(blockIdx.x, gridDim.x);
+    // 16 KiB: one block per workgroup.  8 KiB: workgroup L takes blocks
+    // 8 (L / 4) + L % 4 and that + 4 (waves 0-1 and 2-3), which share b mod 4
+    // and so one output alignment (as the 4 KiB path; unframe_grid covers whole
+    // groups of 8 blocks)
+    const uint64_t b = lg_groups == 1 ? 8ull * (L >> 2) + (L & 3u) + 4u * (wave >> 1)
+                                      : ((uint64_t)L * 4 + wave) >> lg_groups;
+    const uint32_t g = wave & gmask;
     const bool mine = b < nblk;
     const uint32_t w0 = tables->w0;
     u32x4 v[4];
