@@ -1241,7 +1241,7 @@ int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t
   DeviceGuard g(device);
   DeviceState &d = g_dev[device];
   const uint64_t nblk = (n + kPayloadPerBlock - 1) / kPayloadPerBlock;
-  const int grid = (int)std::min<uint64_t>(1 + (nblk > 2 ? 4 * ((nblk - 2 + 15) / 16) : 0), 0x7FFFFFFF);  // k_frame: edges + one interior block per wave
+  const int grid = (int)std::min<uint64_t>(1 + (nblk > 2 ? kFrameSpread * ((nblk - 2 + 4 * kFrameSpread - 1) / (4 * kFrameSpread)) : 0), 0x7FFFFFFF);  // k_frame: edges + one interior block per wave
   hc_launch_info info{"k_frame", nblk, 0, n + nblk * HC_BLOCK_SIZE, (uint32_t)grid, 256, kLaneQWords * 4};
   t_last = info;
   return launch_frame(static_cast<const uint8_t *>(src), n, static_cast<uint8_t *>(dst), crc_out, d.dtab, grid,

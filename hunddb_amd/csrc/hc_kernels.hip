@@ -1167,12 +1167,13 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
     if (wv == 0 || (wv == 1 && nblk >= 2)) frame_edges_wave(src, n, dst, nblk, crc_out, lq, TM, TS, tables->w0, lane, wv);
     return;
   }
-  // interior logical workgroup I = wg - 1 takes interior blocks 16 (I / 4) +
-  // 4 w + I % 4: b mod 4 fixes the source's misalignment (4092 b mod 16), so a
-  // workgroup's four waves share it (+2-4 %, tools/kframe4 KF4_SET=xcd); the
-  // interior grid is a multiple of 4 workgroups (launch_frame)
+  // interior logical workgroup I = wg - 1 takes interior blocks S (4 (I / S) +
+  // w) + I % S (S = kFrameSpread = 8): b mod 4 fixes the source's misalignment
+  // (4092 b mod 16), so a workgroup's four waves share it and read no shared
+  // line (+3.8 % with S = 4, +1.2 % more with S = 8; profiles/r3/kframe4/); the
+  // interior grid is a multiple of S workgroups (launch_frame)
   const uint32_t I = wg - 1;
-  const uint64_t b = 1 + 16ull * (I >> 2) + 4u * uni(threadIdx.x >> 6) + (I & 3u);  // interior block
+  const uint64_t b = 1 + 4ull * kFrameSpread * (I / kFrameSpread) + kFrameSpread * uni(threadIdx.x >> 6) + I % kFrameSpread;
   const bool mine = b + 1 < nblk;
   // A wave past the last interior block loads block 1's rows (interior
   // whenever this kernel runs) and exits after the barrier: no branch around
@@ -1294,13 +1295,14 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
     // VGPR (exec-masked branches), ran 6.5 % slower (tools/kframe4: 5490 vs
     // 5830-5850 GB/s).  `blocks` is not __restrict__: with it, hipcc may sink
     // the row loads past the barrier into the block that uses them.
-    // Logical workgroup L (XCD-contiguous) takes blocks 16 (L / 4) + 4 w + L % 4:
-    // b mod 4 fixes the output's misalignment (4092 b mod 16), so the four
-    // waves of a workgroup store with one alignment (+1.1 % over four
-    // consecutive blocks, tools/kframe4 KF4_SET=xcd); the grid is a multiple
-    // of 4 workgroups (unframe_grid) so every group of 16 blocks is covered.
+    // Logical workgroup L (XCD-contiguous) takes blocks S (4 (L / S) + w) + L % S
+    // (S = kFrameSpread = 8): b mod 4 fixes the output's misalignment (4092 b
+    // mod 16), so the four waves of a workgroup store with one alignment, and
+    // no two of them write a shared line (+3.5 % with S = 4 over four
+    // consecutive blocks, +2.6 % more with S = 8; profiles/r3/kframe4/); the
+    // grid is a multiple of S workgroups (unframe_grid).
     const uint32_t L = xcd_wg(blockIdx.x, gridDim.x);
-    const uint64_t b = 16ull * (L >> 2) + 4u * uni(threadIdx.x >> 6) + (L & 3u);
+    const uint64_t b = 4ull * kFrameSpread * (L / kFrameSpread) + kFrameSpread * uni(threadIdx.x >> 6) + L % kFrameSpread;
     const bool mine = b < nblk;
     const uint32_t w0 = tables->w0;
     u32x4 v[4];
@@ -1917,8 +1919,8 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
   const uint64_t nblk = (n + 4091) / 4092;
   if (nblk == 0) return hipSuccess;
   // workgroup 0: the two edge blocks; then one interior block per wave, in
-  // groups of 16 blocks over 4 workgroups
-  const uint64_t wgs = 1 + (nblk > 2 ? 4 * ((nblk - 2 + 15) / 16) : 0);
+  // runs of 4 x kFrameSpread blocks over kFrameSpread workgroups
+  const uint64_t wgs = 1 + (nblk > 2 ? kFrameSpread * ((nblk - 2 + 4 * kFrameSpread - 1) / (4 * kFrameSpread)) : 0);
   if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, n, dst, nblk, crc_out, tables);
   return hipGetLastError();

@@ -60,10 +60,19 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
                         const DeviceTables *tables, int grid, hipStream_t s);
 constexpr uint32_t kLaneQWords = 8 * kLanes * 4;  // k_frame / k_unframe: LDS copy of DeviceTables::lane_q
 // k_unframe: one 4 KiB group per wave, 4-wave workgroups (a block's groups in one
-// workgroup); 4 and 8 KiB blocks go in groups of 16 / 8 over 4 workgroups (one
-// output alignment per workgroup), so those grids are multiples of 4
+// workgroup); 4 KiB blocks go in runs of 4 x kFrameSpread over kFrameSpread
+// workgroups, 8 KiB blocks in runs of 8 over 4 (one output alignment per
+// workgroup), so those grids are multiples of kFrameSpread / 4
+// k_frame / k_unframe (4 KiB): a workgroup's four waves take blocks kFrameSpread
+// apart, kFrameSpread neighbouring workgroups one contiguous run of 4 x
+// kFrameSpread blocks.  A multiple of 4, so b mod 4 -- the 4092-B stride's
+// misalignment -- is one per workgroup.  Spreads 4 / 8 / 16 / 32 measured
+// (profiles/r3/kframe4/): 8 is the fastest.
+constexpr uint32_t kFrameSpread = 8;
 inline uint64_t unframe_grid(uint64_t nblk, uint32_t lg_groups) {
-  return lg_groups == 0 ? 4 * ((nblk + 15) / 16) : lg_groups == 1 ? 4 * ((nblk + 7) / 8) : nblk;
+  return lg_groups == 0 ? kFrameSpread * ((nblk + 4 * kFrameSpread - 1) / (4 * kFrameSpread))
+         : lg_groups == 1 ? 4 * ((nblk + 7) / 8)
+                          : nblk;
 }
 // Batched ReadFromDisk: verify nblk blocks of 4096 << lg_groups bytes at `blocks`
 // (16-B aligned) and write their payloads back to back at `out`.  Its own grid
