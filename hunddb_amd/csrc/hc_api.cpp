@@ -43,6 +43,10 @@ struct DeviceState {
   DeviceTables *dtab = nullptr;  // device copy of the constant image
   SegTables *dseg = nullptr;     // the packed-record path's tables (k_seg_*)
   uint32_t *seg_last = nullptr;  // 1 when the last packed-record stream took its batch
+  // off/len batches: k_crc_grp's "a block was left to the sweep" word and the
+  // per-call tag it is raised to (Batch::skip_slot)
+  unsigned long long *skip_slot = nullptr;
+  std::atomic<uint64_t> skip_tag{0};
   // the packed-record stream's workspace for calls on the null stream, kept
   // across calls: that stream orders every use after the previous one and is
   // never destroyed.  Calls on other streams (which may be destroyed and their
@@ -125,6 +129,11 @@ int init_device(int dev) {
       return;
     }
     d.seg_last = static_cast<uint32_t *>(p);
+    if (hipMalloc(&p, 8) != hipSuccess || hipMemset(p, 0, 8) != hipSuccess) {
+      d.status = HC_E_NOMEM;
+      return;
+    }
+    d.skip_slot = static_cast<unsigned long long *>(p);
     d.cus = prop.multiProcessorCount;
     d.status = HC_OK;
   });
@@ -260,6 +269,8 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
     }
     // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk
     // size, utils/config/config.go:137); the k_crc_any sweep does the rest
+    b.skip_slot = d.skip_slot;
+    b.skip_tag = d.skip_tag.fetch_add(1, std::memory_order_relaxed) + 1;
     if (e == hipSuccess) e = launch_grp(b, fast_grid, s);
     if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
     if (seg_ws && hipFreeAsync(seg_ws, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;

@@ -123,6 +123,17 @@ __device__ __forceinline__ void lane0_atomic_or(uint32_t *p, uint32_t v) {
       : "v"(p), "v"(v)
       : "memory");
 }
+__device__ __forceinline__ void lane0_atomic_umax64(unsigned long long *p, uint64_t v) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "global_atomic_umax_x2 %1, %2, off\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv)
+      : "v"(p), "v"(v)
+      : "memory");
+}
 __device__ __forceinline__ void lane0_atomic_umin64(unsigned long long *p, uint64_t v) {
   uint64_t sv;
   asm volatile(
@@ -338,7 +349,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
                                                          uint32_t *__restrict__ bad_bitmap,
                                                          unsigned long long *__restrict__ first_bad,
                                                          const DeviceTables *__restrict__ tables,
-                                                         const uint32_t *__restrict__ seg_flag = nullptr) {
+                                                         const uint32_t *__restrict__ seg_flag = nullptr,
+                                                         unsigned long long *__restrict__ skip_slot = nullptr,
+                                                         uint64_t skip_tag = 0) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
   if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
@@ -514,6 +527,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
           if (b < reported) lane0_atomic_umin64(first_bad, b);
           reported = b < reported ? b : reported;
         }
+      } else if (kArrays && skip_slot && skip_tag) {  // left to the k_crc_any sweep: tell it once per wave
+        lane0_atomic_umax64(skip_slot, skip_tag);
+        skip_tag = 0;
       }
       if (!nxt.valid) return;
       cur = nxt;
@@ -599,10 +615,15 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
-    const uint32_t *__restrict__ seg_flag = nullptr) {
+    const uint32_t *__restrict__ seg_flag = nullptr, const unsigned long long *skip_slot = nullptr,
+    uint64_t skip_tag = 0) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;
   if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
+  // the sweep after k_crc_grp: no block was left to it (Batch::skip_slot)
+  if (fast_mask && skip_slot &&
+      __hip_atomic_load(skip_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < skip_tag)
+    return;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = uni(tid >> 6);
   const uint64_t b1 = nblocks;
@@ -1862,10 +1883,12 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
   if (!b.base) return hipErrorInvalidValue;
   if (b.flags & kFlagMessages)
     hipLaunchKernelGGL(k_crc_any<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
+                       b.skip_slot, b.skip_tag);
   else
     hipLaunchKernelGGL(k_crc_any<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
+                       b.skip_slot, b.skip_tag);
   return hipGetLastError();
 }
 
@@ -1904,7 +1927,8 @@ hipError_t launch_grp(const Batch &b, int grid, hipStream_t s) {
   const uint32_t lg = grp_lg_chunk(b.nblocks, grid, (b.off || b.len) ? 0u : b.ulen);
   if (b.off || b.len)
     hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
-                       b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag);
+                       b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
+                       b.skip_slot, b.skip_tag);
   else if (grp_xcd(b.ulen, grid, b.nblocks))  // each XCD's workgroups own neighbouring chunk slots
     hipLaunchKernelGGL((k_crc_grp<false, true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride,
                        b.ulen, b.flags, b.nblocks, lg, b.crc_out, b.bad_bitmap, b.first_bad, b.tables);

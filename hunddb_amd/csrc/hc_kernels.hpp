@@ -29,6 +29,13 @@ struct Batch {
   // optional: the flag of a packed-record stream launched before (launch_seg);
   // k_crc_grp / k_crc_any do nothing when it is 0 (the stream took the batch)
   const uint32_t *seg_flag;
+  // optional (off/len batches): k_crc_grp raises *skip_slot to at least
+  // skip_tag (atomic max) when it leaves a block to k_crc_any, and the k_crc_any
+  // sweep after it exits at once while *skip_slot < skip_tag.  Tags increase
+  // per call, so a slot shared by concurrent calls (or a graph replaying an old
+  // tag) can only make a sweep run without need, never skip one that has work.
+  unsigned long long *skip_slot;
+  uint64_t skip_tag;
 };
 
 // Streaming kernel geometry (one workgroup per CU; see DESIGN.md "Kernel").

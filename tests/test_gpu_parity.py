@@ -1031,3 +1031,80 @@ def test_read_from_disk_verified_mask_gpu_batch(cuda, hc, oracle):
     ta = importlib.import_module("test_abi")
     for B in (4096, 8192, 5000):
         ta._read_mask_case(hc, oracle, 3000, B, B + 1)
+
+
+def test_offlen_sweep_skip_flag(cuda, hc, oracle):
+    """The k_crc_any sweep after an off/len k_crc_grp exits at once when
+    k_crc_grp left it no block (Batch::skip_slot).  Calls that alternate
+    between fully conforming batches and batches with one non-conforming block
+    (first, middle, last, the only block; misaligned or a length that is not a
+    4 KiB multiple) must all be exact; `out` is poisoned before each call, so a
+    sweep that wrongly exits leaves the poison.  Then the same on two streams at
+    once, and a captured graph replayed after its off[] changed under it."""
+    torch = cuda
+    rng = np.random.default_rng(77)
+    n = 3000
+    host = rng.integers(0, 256, n * 16384 + 4096, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    base_off = np.arange(n, dtype=np.uint64) * 16384
+    base_len = (4096 * rng.integers(1, 5, n)).astype(np.uint32)
+
+    def run(off, lens, stream=None, m=n):
+        doff = torch.from_numpy(off[:m].view(np.int64)).cuda()
+        dlen = torch.from_numpy(lens[:m].view(np.int32)).cuda()
+        out = torch.full((m,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=m, stream=stream)
+        return out, (doff, dlen)
+
+    cases = []
+    for pos in (0, n // 2, n - 1):
+        for kind in ("misaligned", "short"):
+            off, lens = base_off.copy(), base_len.copy()
+            if kind == "misaligned":
+                off[pos] += 3
+            else:
+                lens[pos] -= 100
+            cases.append((off, lens, n))
+    single_off, single_len = base_off.copy(), base_len.copy()
+    single_off[0] += 5
+    seq = [(base_off, base_len, n)]
+    for c in cases:
+        seq += [c, (base_off, base_len, n)]
+    seq += [(single_off, single_len, 1), (base_off, base_len, 1)]
+    for off, lens, m in seq:
+        out, _ = run(off, lens, m=m)
+        torch.cuda.synchronize()
+        want = oracle.crc32_blocks(host, off=off[:m], lens=lens[:m], threads=16)
+        assert (u32(out) == want).all(), (m, np.nonzero(u32(out) != want)[0][:5])
+
+    # two streams: one conforming, one with a misaligned block, many rounds
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    off_b, len_b = cases[1][0], cases[1][1]
+    want_a = oracle.crc32_blocks(host, off=base_off, lens=base_len, threads=16)
+    want_b = oracle.crc32_blocks(host, off=off_b, lens=len_b, threads=16)
+    keep = []
+    for _ in range(8):
+        keep.append((run(base_off, base_len, stream=s1), run(off_b, len_b, stream=s2)))
+    torch.cuda.synchronize()
+    for (oa, _), (ob, _) in keep:
+        assert (u32(oa) == want_a).all() and (u32(ob) == want_b).all()
+
+    # a graph captured on a conforming batch, replayed after one offset moved
+    doff = torch.from_numpy(base_off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(base_len.view(np.int32)).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=n, stream=s)  # warm (tables, init)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=n, stream=s)
+    torch.cuda.synchronize()
+    for off in (base_off, off_b, base_off, off_b):
+        doff.copy_(torch.from_numpy(off.view(np.int64)))
+        out.fill_(0x5A5A5A5A)
+        g.replay()
+        torch.cuda.synchronize()
+        want = oracle.crc32_blocks(host, off=off, lens=base_len, threads=16)
+        assert (u32(out) == want).all()
