@@ -16,7 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {
     "northstar": (4096, "k_crc_grp", 4096 * 8192),
     "verify": (4096, "k_crc_grp", 4096 * (8192 + 4)),
+    "config2": (4096, "k_crc_grp", 4096 * 4096),
+    "16k": (1024, "k_crc_grp", 1024 * 16384),
     "config3": (4096, "k_crc_grp+k_crc_any", None),
+    "offlen4k": (4096, "k_crc_grp+k_crc_any", 4096 * 4096),
+    "config4": (4096, "k_crc_grp", 4096 * 8192),
     "frame": (4096, "k_frame", (4096 * 4092 - 1000) + 4096 * 4096),
     "unframe": (4096, "k_unframe", 4096 * (4096 + 4092)),
     "unframe8k": (2048, "k_unframe", 2048 * (8192 + 8188)),
