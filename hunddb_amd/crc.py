@@ -80,6 +80,12 @@ class LaunchInfo(ctypes.Structure):
                 ("lds_bytes", ctypes.c_uint32)]
 
 
+class Stats(ctypes.Structure):  # hc_stats_t (include/hundcrc.h)
+    _fields_ = [("add_crcs_gpu", ctypes.c_uint64), ("add_crcs_host_small", ctypes.c_uint64),
+                ("add_crcs_host_nodev", ctypes.c_uint64), ("add_crcs_gpu_fallback", ctypes.c_uint64),
+                ("last_fallback_error", ctypes.c_int64)]
+
+
 class DevShard(ctypes.Structure):  # hc_dev_shard (include/hundcrc.h)
     _fields_ = [("device", ctypes.c_int), ("base", ctypes.c_void_p), ("off", ctypes.c_void_p),
                 ("len", ctypes.c_void_p), ("stride", ctypes.c_uint64), ("ulen", ctypes.c_uint32),
@@ -135,6 +141,8 @@ def _lib():
             "hc_debug_seg_taken": (I, []),
             "hc_device_count": (I, []),
             "hc_host_pipelines": (I, []),
+            "hc_stats": (I, [ctypes.POINTER(Stats)]),
+            "hc_stats_reset": (None, []),
             "hc_md5": (None, [P, S, P]),
             "hc_md5_messages": (I, [P, P, P, U64, P]),
             "hc_dev_md5_messages": (I, [I, P, P, P, U64, U32, U64, P, P, P]),
@@ -603,6 +611,19 @@ def last_launch() -> dict:
 
 def device_count() -> int:
     return int(_lib().hc_device_count())
+
+
+def stats() -> dict:
+    """hc_stats(): the library's process-wide event counters."""
+    st = Stats()
+    rc = _lib().hc_stats(ctypes.byref(st))
+    if rc != HC_OK:
+        raise HundCRCError(rc, "hc_stats")
+    return {k: int(getattr(st, k)) for k, _ in Stats._fields_}
+
+
+def stats_reset() -> None:
+    _lib().hc_stats_reset()
 
 
 def host_pipelines() -> int:

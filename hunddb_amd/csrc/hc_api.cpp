@@ -33,6 +33,26 @@ using namespace hc;
 namespace {
 
 constexpr size_t kPayloadPerBlock = HC_BLOCK_SIZE - HC_CRC_SIZE;  // 4092 (crc_util.go:43)
+constexpr size_t kAddCrcsGpuMinBlocks = 256;  // placeholder until the crossover is measured
+
+// Process-wide event counters (hc_stats).
+struct Stats {
+  std::atomic<uint64_t> add_crcs_gpu{0}, add_crcs_host_small{0}, add_crcs_host_nodev{0},
+      add_crcs_gpu_fallback{0};
+  std::atomic<int64_t> last_fallback_error{0};
+};
+Stats g_stats;
+
+// HC_INJECT_FAIL=<site>[:nomem] (read per call, tests only): the named GPU step
+// reports HC_E_HIP (or HC_E_NOMEM) without running, so the recovery path can
+// be tested on any host.  Returns 0 when `site` is not named.
+int injected_failure(const char *site) {
+  const char *v = std::getenv("HC_INJECT_FAIL");
+  if (!v || !*v) return 0;
+  const size_t n = std::strlen(site);
+  if (std::strncmp(v, site, n) != 0 || (v[n] != 0 && v[n] != ':')) return 0;
+  return (v[n] == ':' && std::strcmp(v + n + 1, "nomem") == 0) ? HC_E_NOMEM : HC_E_HIP;
+}
 
 // ---------------------------------------------------------------------------
 // Devices
@@ -826,12 +846,14 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
     }
   };
 
-  // CRCs: one GPU batch for multi-block outputs, host for a single block.
-  // AddCRCsToData cannot fail in Go (crc_util.go:41-64), so a host with no
-  // gfx950 (HC_E_NODEV) computes the CRCs on the host path below (hc_cpu.cpp,
-  // product code) instead of failing; any other GPU error is returned, and
-  // HC_FORCE_GPU (test mode) never takes the host path.
-  static const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", 256);
+  // CRCs: one GPU batch for multi-block outputs, host for small ones.
+  // AddCRCsToData cannot fail in Go (crc_util.go:41-64), so a GPU batch that
+  // does not complete -- no gfx950 (HC_E_NODEV), a device or pinned allocation
+  // failure (HC_E_NOMEM), a HIP runtime error (HC_E_HIP) -- is finished on the
+  // host path below (hc_cpu.cpp, product code) from the already framed dst,
+  // and counted in hc_stats.  Only HC_FORCE_GPU (test mode) returns the error.
+  // HC_INJECT_FAIL=add_crcs[:nomem] simulates a failing GPU batch (tests).
+  static const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", (int)kAddCrcsGpuMinBlocks);
   bool on_gpu = false;
   if (nb >= gpu_min || (force_gpu() && nb > 0)) {
     // The CRC of block k is ChecksumIEEE(src[4092k : 4092k+4092]) for every
@@ -850,6 +872,10 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
         return;
       }
       if (!nfull) return;
+      if (const int inj = injected_failure("add_crcs")) {
+        rc = inj;
+        return;
+      }
       if (is_pinned(src)) {  // span DMA wants explicit off/len
         std::vector<uint64_t> o(nfull);
         std::vector<uint32_t> l(nfull, (uint32_t)kPayloadPerBlock);
@@ -871,11 +897,18 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
         std::memcpy(blk, &c, 4);
       }
       on_gpu = true;
-    } else if (rc != HC_E_NODEV || force_gpu()) {
+      g_stats.add_crcs_gpu.fetch_add(1, std::memory_order_relaxed);
+    } else if (force_gpu()) {
       return (size_t)-1;
+    } else if (rc == HC_E_NODEV) {
+      g_stats.add_crcs_host_nodev.fetch_add(1, std::memory_order_relaxed);
+    } else {
+      g_stats.add_crcs_gpu_fallback.fetch_add(1, std::memory_order_relaxed);
+      g_stats.last_fallback_error.store(rc, std::memory_order_relaxed);
     }
   } else {
     frame(0, nb);
+    g_stats.add_crcs_host_small.fetch_add(1, std::memory_order_relaxed);
   }
   if (!on_gpu) {
     for (size_t b = 0; b < nb; b++) {
@@ -1313,6 +1346,24 @@ int hc_dev_fill_blocks(int device, void *base, const uint64_t *off, const uint32
 }
 
 int hc_host_pipelines(void) { return PipePool::get().live(); }
+
+int hc_stats(hc_stats_t *out) {
+  if (!out) return HC_E_ARG;
+  out->add_crcs_gpu = g_stats.add_crcs_gpu.load(std::memory_order_relaxed);
+  out->add_crcs_host_small = g_stats.add_crcs_host_small.load(std::memory_order_relaxed);
+  out->add_crcs_host_nodev = g_stats.add_crcs_host_nodev.load(std::memory_order_relaxed);
+  out->add_crcs_gpu_fallback = g_stats.add_crcs_gpu_fallback.load(std::memory_order_relaxed);
+  out->last_fallback_error = g_stats.last_fallback_error.load(std::memory_order_relaxed);
+  return HC_OK;
+}
+
+void hc_stats_reset(void) {
+  g_stats.add_crcs_gpu.store(0);
+  g_stats.add_crcs_host_small.store(0);
+  g_stats.add_crcs_host_nodev.store(0);
+  g_stats.add_crcs_gpu_fallback.store(0);
+  g_stats.last_fallback_error.store(0);
+}
 
 int hc_last_launch(hc_launch_info *info) {
   if (!info) return HC_E_ARG;

@@ -24,8 +24,11 @@
  *     pointer rule); the library never retains or frees caller memory.
  *   - Host entries (no _dev_) take host pointers, copy through library-owned
  *     pinned staging and are synchronous.  _dev_ entries take device pointers
- *     and a hipStream_t (passed as void*; NULL = the library's per-thread
- *     stream) and are asynchronous on that stream.
+ *     and a hipStream_t (passed as void*; NULL = HIP's legacy default stream
+ *     of the device, one per device and shared by every host thread -- the
+ *     library relies on that ordering for the workspace it keeps across NULL-
+ *     stream calls; it is built without -fgpu-default-stream=per-thread) and
+ *     are asynchronous on that stream.
  *   - Every function is re-entrant and thread-safe.  Shared state: the lazily
  *     initialised per-device constant tables and the bounded pool of host-batch
  *     pipelines (hc_host_pipelines).
@@ -75,9 +78,13 @@ size_t hc_add_crcs_size(size_t n);
 /* AddCRCsToData (crc_util.go:41-64): chunk src into 4092-byte payloads, each
  * in a zeroed 4096-byte block with its CRC in bytes [0:4).  dst is caller
  * memory of >= hc_add_crcs_size(n) bytes (Go: make([]byte, ...)).  Returns the
- * number of bytes written, or (size_t)-1 if dst_cap is too small or a GPU
- * batch fails.  Outputs of >= 256 blocks are CRC'd on the GPU; without a
- * gfx950 device they are CRC'd on the host (the Go function cannot fail). */
+ * number of bytes written, or (size_t)-1 only if dst_cap is too small (or a
+ * pointer is NULL).  Outputs of at least HC_ADD_CRCS_GPU_MIN_BLOCKS blocks
+ * (the measured GPU/host crossover) are CRC'd in one GPU batch;
+ * when that batch cannot run or fails (no gfx950, HC_E_NOMEM, HC_E_HIP) the
+ * CRCs are finished on the host path and the event is counted in hc_stats():
+ * the Go function cannot fail, so neither can this.  Only HC_FORCE_GPU=1 (test
+ * mode) returns (size_t)-1 for a failed GPU batch. */
 size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap);
 /* SizeAfterAddingCRCs (crc_util.go:69-74), float64-ceil semantics. */
 uint64_t hc_size_after_crcs(uint64_t n);
@@ -334,6 +341,21 @@ int hc_device_count(void);
  * + streams).  Host entries lease one per call from a pool of at most
  * HC_MAX_PIPES (default 4) per device; further concurrent callers wait for a free one. */
 int hc_host_pipelines(void);
+
+/* Process-wide event counters (monotonic since load or hc_stats_reset).
+ * AddCRCsToData: calls whose CRCs ran as a GPU batch, on the host because the
+ * output was below the GPU threshold, on the host because no gfx950 device
+ * was usable, and on the host after a GPU batch failed (last_fallback_error =
+ * that batch's HC_E_* code). */
+typedef struct hc_stats_t {
+  uint64_t add_crcs_gpu;
+  uint64_t add_crcs_host_small;
+  uint64_t add_crcs_host_nodev;
+  uint64_t add_crcs_gpu_fallback;
+  int64_t last_fallback_error;
+} hc_stats_t;
+int hc_stats(hc_stats_t *out);
+void hc_stats_reset(void);
 
 #ifdef __cplusplus
 }

@@ -76,10 +76,13 @@ func AddCRCToBlockData(data []byte) []byte {
 }
 
 // AddCRCsToData frames data into BLOCK_SIZE blocks with a CRC each (crc_util.go:41).
-// Multi-hundred-block inputs are CRC'd in one GPU batch; on a host without a
-// gfx950 the library CRCs them on the CPU, so this cannot fail there, as the
-// reference cannot.  Only a HIP runtime error on a GPU host remains, and the
-// signature (no error result) leaves a panic as its report.
+// Inputs above the library's GPU threshold are CRC'd in one GPU batch; when
+// that batch cannot run or fails (no gfx950, a device or pinned allocation
+// failure, a HIP runtime error) the library finishes the CRCs on the host path
+// and counts the event (hc_stats), so this cannot fail, as the reference
+// cannot.  hc_add_crcs returns ^0 only for a dst smaller than
+// hc_add_crcs_size(n), which the make() below rules out, or under the
+// HC_FORCE_GPU test mode; the panic is kept for those.
 func AddCRCsToData(serializedData []byte) []byte {
 	out := make([]byte, int(C.hc_add_crcs_size(C.size_t(len(serializedData)))))
 	if len(out) == 0 {
@@ -87,7 +90,7 @@ func AddCRCsToData(serializedData []byte) []byte {
 	}
 	w := C.hc_add_crcs(ptr(serializedData), C.size_t(len(serializedData)), ptr(out), C.size_t(len(out)))
 	if w == ^C.size_t(0) {
-		panic("hundcrc: AddCRCsToData: GPU batch failed")
+		panic("hundcrc: AddCRCsToData: output buffer too small (or HC_FORCE_GPU batch failed)")
 	}
 	return out
 }

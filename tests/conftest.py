@@ -15,6 +15,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+LAST_PREFIX = "test_gpu_zz_"  # heavy full-size files: collected after every other test
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Run the test_gpu_zz_* files (config 5 at 10M records, ~108 GB of host
+    memory) after everything else, whatever order the paths were given in, so
+    that under -x a failure there cannot hide the parity suite."""
+    last = [it for it in items if os.path.basename(str(it.fspath)).startswith(LAST_PREFIX)]
+    if last:
+        keep = [it for it in items if not os.path.basename(str(it.fspath)).startswith(LAST_PREFIX)]
+        items[:] = keep + last
+
+
 @pytest.fixture(scope="session")
 def golden():
     with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:

@@ -256,6 +256,49 @@ def test_add_crcs_to_data_without_gpu(hc, oracle, monkeypatch):
         hc.AddCRCsToData(src)
 
 
+@pytest.mark.parametrize("inject", ["add_crcs", "add_crcs:nomem"])
+def test_add_crcs_finishes_on_host_after_gpu_failure(hc, oracle, monkeypatch, inject):
+    """AddCRCsToData cannot fail in Go (crc_util.go:41-64),
+    so a GPU batch that fails (HC_E_HIP, HC_E_NOMEM -- here simulated by
+    HC_INJECT_FAIL before any device call) is finished on the host path from the
+    framed output, byte-exact vs the oracle, and counted in hc_stats; under
+    HC_FORCE_GPU the failure is returned instead.  Runs with or without a GPU."""
+    rng = np.random.default_rng(301)
+    src = rng.integers(0, 256, 4092 * 300 + 77, dtype=np.uint8).tobytes()
+    want = np.zeros(hc.hc_add_crcs_size_py(len(src)), dtype=np.uint8)
+    assert oracle.lib().oc_add_crcs_to_data(src, len(src), want.ctypes.data) == len(want)
+    monkeypatch.setenv("HC_INJECT_FAIL", inject)
+    hc.stats_reset()
+    out = hc.AddCRCsToData(src)
+    assert bytes(out) == want.tobytes()
+    st = hc.stats()
+    assert st["add_crcs_gpu_fallback"] == 1 and st["add_crcs_gpu"] == 0 and st["add_crcs_host_nodev"] == 0
+    assert st["last_fallback_error"] == (hc.HC_E_NOMEM if inject.endswith("nomem") else hc.HC_E_HIP)
+    # a different site named: no injection, the call takes its normal path
+    monkeypatch.setenv("HC_INJECT_FAIL", "add_crcsX")
+    hc.stats_reset()
+    assert bytes(hc.AddCRCsToData(src)) == want.tobytes()
+    st = hc.stats()
+    assert st["add_crcs_gpu_fallback"] == 0
+    assert st["add_crcs_gpu"] + st["add_crcs_host_nodev"] == 1
+    assert st["add_crcs_host_nodev"] == (1 if hc.device_count() == 0 else 0)
+    monkeypatch.setenv("HC_INJECT_FAIL", inject)
+    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    with pytest.raises(hc.HundCRCError):
+        hc.AddCRCsToData(src)
+
+
+def test_add_crcs_small_outputs_stay_on_host(hc, oracle):
+    hc.stats_reset()
+    src = bytes(range(256)) * 40  # 3 blocks
+    out = hc.AddCRCsToData(src)
+    want = np.zeros(len(out), dtype=np.uint8)
+    assert oracle.lib().oc_add_crcs_to_data(src, len(src), want.ctypes.data) == len(out)
+    assert bytes(out) == want.tobytes()
+    st = hc.stats()
+    assert st["add_crcs_host_small"] == 1 and st["add_crcs_gpu"] == 0 and st["add_crcs_gpu_fallback"] == 0
+
+
 def test_read_from_disk_host(hc, golden, oracle):
     """hc_read_from_disk (row f1) on the host path: the golden ReadFromDisk cases,
     then random (start, size) over a larger image with corruptions, vs the oracle."""

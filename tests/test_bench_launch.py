@@ -13,8 +13,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_self_launch_strong_scaling_words(world):
+    """world 8 is the size of the driver's scaling run (Next 4): 8
+    ranks spawned, an 8-row device table, one JSON line."""
     code = ("import sys; sys.path.insert(0, %r); import bench; "
             "sys.exit(bench.self_launch(['--blocks', '3001', '--gpus', '%d'], %d, "
             "script=%r))" % (ROOT, world, world, os.path.join(ROOT, "tests", "bench_cpu_rank.py")))

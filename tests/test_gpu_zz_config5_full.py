@@ -15,7 +15,15 @@ the blocks starting where the WAL segment files put them.
   to back in HBM (the packed-record stream), against the oracle on a sample and
   word for word against k_crc_any.
 
-Host memory: ~108 GB (one image); the box allows ~270 GiB per command."""
+Host memory: ~108 GB (one image); the box allows ~270 GiB per command.
+
+The file is named test_gpu_zz_* so that it is collected after every other GPU
+test (tests/conftest.py also moves it last, and
+tests/test_collection_order.py asserts the order): under `pytest -x` a failure
+here can never leave the parity suite unreached.  Before allocating, each test
+compares its need with the cgroup's memory limit and MemAvailable (host) or
+the device's free memory, and FAILS with those numbers when it does not fit --
+no skip, and no OOM kill of the whole pytest process."""
 import os
 import sys
 
@@ -29,6 +37,49 @@ NREC = 10_000_000
 SEED = 0x57414C
 
 
+def host_memory_room():
+    """(bytes this process may still allocate, description): the smaller of
+    /proc/meminfo's MemAvailable and the cgroup limit minus its usage (v2
+    memory.max / memory.current, or v1 memory.limit_in_bytes / usage_in_bytes)."""
+    avail = None
+    with open("/proc/meminfo") as f:
+        for line in f:
+            if line.startswith("MemAvailable:"):
+                avail = int(line.split()[1]) * 1024
+    parts = [f"MemAvailable {avail / 2**30:.1f} GiB"]
+    room = avail
+    for lim_p, use_p in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
+                         ("/sys/fs/cgroup/memory/memory.limit_in_bytes",
+                          "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+        try:
+            with open(lim_p) as f:
+                lim = f.read().strip()
+            with open(use_p) as f:
+                use = int(f.read().strip())
+        except OSError:
+            continue
+        if lim == "max" or int(lim) >= 1 << 60:
+            parts.append(f"cgroup {lim_p}: unlimited")
+        else:
+            free = int(lim) - use
+            parts.append(f"cgroup {lim_p} {int(lim) / 2**30:.1f} GiB, used {use / 2**30:.1f} GiB")
+            room = free if room is None else min(room, free)
+        break
+    return room, "; ".join(parts)
+
+
+def require_host_bytes(need):
+    room, desc = host_memory_room()
+    assert room is None or room >= need, (
+        f"config 5 needs {need / 2**30:.1f} GiB of host memory; this box has {room / 2**30:.1f} GiB ({desc})")
+
+
+def require_device_bytes(torch, need):
+    free, total = torch.cuda.mem_get_info()
+    assert free >= need, (
+        f"config 5 needs {need / 2**30:.1f} GiB on the device; {free / 2**30:.1f} of {total / 2**30:.1f} GiB free")
+
+
 def _walgen():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import walgen
@@ -40,6 +91,7 @@ def test_config5_wal_blocks_full_size(cuda, hc, oracle):
     plan = walgen.WalPlan(SEED, nrec=NREC)
     nb = plan.nblocks
     assert nb > 26_000_000
+    require_host_bytes(nb * 4096 + (4 << 30))  # the image + pipelines, the oracle's words, headroom
     host = np.empty(nb * 4096, dtype=np.uint8)
     step = 1 << 18
     for b0 in range(0, nb, step):
@@ -74,6 +126,8 @@ def test_config5_records_full_size_on_device(cuda, hc, oracle):
     off += np.uint64(3)  # back to back from an odd address
     total = (int(off[-1]) + int(sizes[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
     assert total > 90e9
+    require_device_bytes(torch, total + NREC * 16 + (2 << 30))
+    require_host_bytes((4 << 30))  # the sampled segments copied back for the oracle
     buf = torch.empty(total, dtype=torch.uint8, device="cuda")
     hc.dev_fill_range(buf, 0x5C, 0, total >> 20, stride=1 << 20, ulen=1 << 20)  # every byte, in 1 MiB blocks
     doff = torch.from_numpy(off.view(np.int64)).cuda()

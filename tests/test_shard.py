@@ -80,6 +80,57 @@ def test_sharded_crcs_match_single_process(world, mixed, oracle):
     assert sum(counts) == n
 
 
+def _gather_worker(rank, world, port, n, q):
+    import torch
+    import torch.distributed as dist
+
+    from hunddb_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard.index_range(n, world, rank)
+        counts = [shard.index_range(n, world, r)[1] - shard.index_range(n, world, r)[0] for r in range(world)]
+        # a stand-in word per global block index (the CRC kernel's output on the GPUs)
+        local = _word_of(np.arange(lo, hi, dtype=np.uint64))
+        got = shard.gather_crcs(torch.from_numpy(local.view(np.int32)), counts)
+        wall, kern, tot = shard.job_timing(1.0 + rank, 0.5, float(hi - lo))
+        ids = shard.gather_identities(shard.rank_identity(None, 0.1 * (rank + 1)))
+        proof = shard.device_proof(ids, "gloo")
+        if rank == 0:
+            got = got.numpy().view(np.uint32)
+            want = _word_of(np.arange(n, dtype=np.uint64))
+            q.put((counts, bool(np.array_equal(got, want)), int(got.size), wall, tot,
+                   [i["rank"] for i in proof["ranks"]], proof["comm_world_size"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _word_of(i):
+    return ((i * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(32)).astype(np.uint32)
+
+
+@pytest.mark.parametrize("world", [8, 3])
+def test_gather_configs3_counts(world):
+    """configs[3]'s 16M blocks split by index over 8 ranks (the driver's scaling
+    run) and over 3 (uneven counts): the all-gather path of shard.gather_crcs
+    returns every one of the 16M words in global order, the job clock is the
+    max over ranks, and the device table has one row per rank."""
+    n = 16_000_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, n, q)) for r in range(world)]
+    [p.start() for p in procs]
+    counts, same, size, wall, tot, ranks, cws = q.get(timeout=300)
+    [p.join(timeout=120) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    assert sum(counts) == n and size == n and same
+    assert max(counts) - min(counts) <= 1 and (world != 3 or len(set(counts)) == 2)
+    assert wall == float(world) and tot == float(n)
+    assert ranks == list(range(world)) and cws == world
+
+
 def test_byte_balance():
     from hunddb_amd import shard
     rng = np.random.default_rng(0)

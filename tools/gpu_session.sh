@@ -15,8 +15,6 @@
 #   rocprof    rocprofv3 --kernel-trace --stats of bench.py $BENCH_ARGS (no PMC passes, no CPU leg)
 #   workloads  bench.py --workload W for every W in $WORKLOADS -> bench_W.json
 #   pmc        one rocprofv3 --pmc pass per ';'-separated counter group of $PMC over $PMC_CMD
-#   kb2        tools/kbench2 with each ';'-separated argument list of $KB2 (A/B harness)
-#   kframe     tools/kframe with each ';'-separated argument list of $KFRAME
 #   rehearse   bench.py --gpus 2 over gloo, two ranks sharing the one GPU
 #   extra      bash -c "$EXTRA"
 set -u
@@ -69,22 +67,6 @@ for s in "${LIST[@]}"; do
       k=$((k + 1))
       (cd /tmp && st "pmc$k" 120 rocprofv3 --pmc $g --kernel-include-regex "${PMC_KERNEL:-k_crc_grp}" \
         --output-format csv -d "$OUT/pmc$k" -o run -- ${PMC_CMD:?PMC_CMD=program and args}) || stop $?
-    done ;;
-  kb2)
-    [ -x tools/kbench2 ] || make -s -C tools kbench2 || stop $?
-    IFS=';' read -ra RUNS <<< "${KB2:?KB2=argument lists}"
-    k=0
-    for a in "${RUNS[@]}"; do
-      k=$((k + 1))
-      st "kb2_$k" 300 ./tools/kbench2 $a || stop $?
-    done ;;
-  kframe)
-    [ -x tools/kframe ] || make -s -C tools kframe || stop $?
-    IFS=';' read -ra RUNS <<< "${KFRAME:?KFRAME=argument lists}"
-    k=0
-    for a in "${RUNS[@]}"; do
-      k=$((k + 1))
-      st "kframe_$k" 300 ./tools/kframe $a || stop $?
     done ;;
   rehearse)
     HC_DIST_BACKEND=gloo st rehearse_n2 600 python bench.py --gpus 2 --steps 5 --warmup 2 --blocks 2000000 \
