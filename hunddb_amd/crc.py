@@ -83,7 +83,9 @@ class LaunchInfo(ctypes.Structure):
 class Stats(ctypes.Structure):  # hc_stats_t (include/hundcrc.h)
     _fields_ = [("add_crcs_gpu", ctypes.c_uint64), ("add_crcs_host_small", ctypes.c_uint64),
                 ("add_crcs_host_nodev", ctypes.c_uint64), ("add_crcs_gpu_fallback", ctypes.c_uint64),
-                ("last_fallback_error", ctypes.c_int64)]
+                ("last_fallback_error", ctypes.c_int64), ("read_gpu", ctypes.c_uint64),
+                ("read_gpu_fallback", ctypes.c_uint64), ("wal_gpu", ctypes.c_uint64),
+                ("wal_gpu_fallback", ctypes.c_uint64), ("nodev_host", ctypes.c_uint64)]
 
 
 class DevShard(ctypes.Structure):  # hc_dev_shard (include/hundcrc.h)

@@ -33,26 +33,22 @@ using namespace hc;
 namespace {
 
 constexpr size_t kPayloadPerBlock = HC_BLOCK_SIZE - HC_CRC_SIZE;  // 4092 (crc_util.go:43)
-constexpr size_t kAddCrcsGpuMinBlocks = 256;  // placeholder until the crossover is measured
 
-// Process-wide event counters (hc_stats).
-struct Stats {
-  std::atomic<uint64_t> add_crcs_gpu{0}, add_crcs_host_small{0}, add_crcs_host_nodev{0},
-      add_crcs_gpu_fallback{0};
-  std::atomic<int64_t> last_fallback_error{0};
-};
-Stats g_stats;
+}  // namespace
 
-// HC_INJECT_FAIL=<site>[:nomem] (read per call, tests only): the named GPU step
-// reports HC_E_HIP (or HC_E_NOMEM) without running, so the recovery path can
-// be tested on any host.  Returns 0 when `site` is not named.
-int injected_failure(const char *site) {
-  const char *v = std::getenv("HC_INJECT_FAIL");
-  if (!v || !*v) return 0;
-  const size_t n = std::strlen(site);
-  if (std::strncmp(v, site, n) != 0 || (v[n] != 0 && v[n] != ':')) return 0;
-  return (v[n] == ':' && std::strcmp(v + n + 1, "nomem") == 0) ? HC_E_NOMEM : HC_E_HIP;
+// Process-wide event counters (hc_stats; hc_wal.cpp counts its replays too).
+hc::Stats hc::g_stats;
+
+namespace {
+void count_fallback(std::atomic<uint64_t> &c, int rc) {
+  if (rc == HC_E_NODEV) {
+    g_stats.nodev_host.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
+  c.fetch_add(1, std::memory_order_relaxed);
+  g_stats.last_fallback_error.store(rc, std::memory_order_relaxed);
 }
+
 
 // ---------------------------------------------------------------------------
 // Devices
@@ -853,7 +849,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
   // host path below (hc_cpu.cpp, product code) from the already framed dst,
   // and counted in hc_stats.  Only HC_FORCE_GPU (test mode) returns the error.
   // HC_INJECT_FAIL=add_crcs[:nomem] simulates a failing GPU batch (tests).
-  static const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", (int)kAddCrcsGpuMinBlocks);
+  const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", (int)kAddCrcsGpuMinBlocks);  // per call: tools/crossover.py
   bool on_gpu = false;
   if (nb >= gpu_min || (force_gpu() && nb > 0)) {
     // The CRC of block k is ChecksumIEEE(src[4092k : 4092k+4092]) for every
@@ -903,8 +899,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
     } else if (rc == HC_E_NODEV) {
       g_stats.add_crcs_host_nodev.fetch_add(1, std::memory_order_relaxed);
     } else {
-      g_stats.add_crcs_gpu_fallback.fetch_add(1, std::memory_order_relaxed);
-      g_stats.last_fallback_error.store(rc, std::memory_order_relaxed);
+      count_fallback(g_stats.add_crcs_gpu_fallback, rc);
     }
   } else {
     frame(0, nb);
@@ -1199,8 +1194,8 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
       if (have < take) std::memset(out + produced + have, 0, take - have);
     }
   };
-  bool copied = false;
-  static const uint64_t gpu_min = (uint64_t)env_int("HC_READ_GPU_MIN_BLOCKS", 256);
+  bool copied = false, on_gpu = false;
+  const uint64_t gpu_min = (uint64_t)env_int("HC_READ_GPU_MIN_BLOCKS", (int)kReadGpuMinBlocks);  // per call: tools/crossover.py
   const uint64_t nt = todo.size();
   std::vector<uint8_t> ok(nt, 0);
   if (nt && (nt >= gpu_min || force_gpu()) && B <= 0xFFFFFFFFu) {
@@ -1217,6 +1212,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
         copy_out(k * t / T, k * (t + 1) / T);
         return;
       }
+      if ((rc = injected_failure("read_from_disk")) != HC_OK) return;
       if (nt == nfull) {  // nothing masked: one uniform batch
         rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nt, nullptr, 0, nullptr, &hv);
       } else {
@@ -1227,9 +1223,17 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
       }
     });
     copied = true;
-    if (rc != HC_OK) return rc;
-    for (uint64_t j = 0; j < nt; j++) ok[j] = !((badj[j >> 5] >> (j & 31)) & 1u);
-  } else {
+    if (rc == HC_OK) {
+      for (uint64_t j = 0; j < nt; j++) ok[j] = !((badj[j >> 5] >> (j & 31)) & 1u);
+      on_gpu = true;
+      g_stats.read_gpu.fetch_add(1, std::memory_order_relaxed);
+    } else if (force_gpu()) {
+      return rc;
+    } else {  // ReadFromDisk fails only on I/O or a CRC mismatch: finish on the host path
+      count_fallback(g_stats.read_gpu_fallback, rc);
+    }
+  }
+  if (!on_gpu) {
     for (uint64_t j = 0; j < nt; j++) {
       const uint8_t *blk = blocks + todo[j] * B;
       uint32_t stored;
@@ -1349,19 +1353,25 @@ int hc_host_pipelines(void) { return PipePool::get().live(); }
 
 int hc_stats(hc_stats_t *out) {
   if (!out) return HC_E_ARG;
-  out->add_crcs_gpu = g_stats.add_crcs_gpu.load(std::memory_order_relaxed);
-  out->add_crcs_host_small = g_stats.add_crcs_host_small.load(std::memory_order_relaxed);
-  out->add_crcs_host_nodev = g_stats.add_crcs_host_nodev.load(std::memory_order_relaxed);
-  out->add_crcs_gpu_fallback = g_stats.add_crcs_gpu_fallback.load(std::memory_order_relaxed);
+  auto ld = [](const std::atomic<uint64_t> &a) { return a.load(std::memory_order_relaxed); };
+  out->add_crcs_gpu = ld(g_stats.add_crcs_gpu);
+  out->add_crcs_host_small = ld(g_stats.add_crcs_host_small);
+  out->add_crcs_host_nodev = ld(g_stats.add_crcs_host_nodev);
+  out->add_crcs_gpu_fallback = ld(g_stats.add_crcs_gpu_fallback);
   out->last_fallback_error = g_stats.last_fallback_error.load(std::memory_order_relaxed);
+  out->read_gpu = ld(g_stats.read_gpu);
+  out->read_gpu_fallback = ld(g_stats.read_gpu_fallback);
+  out->wal_gpu = ld(g_stats.wal_gpu);
+  out->wal_gpu_fallback = ld(g_stats.wal_gpu_fallback);
+  out->nodev_host = ld(g_stats.nodev_host);
   return HC_OK;
 }
 
 void hc_stats_reset(void) {
-  g_stats.add_crcs_gpu.store(0);
-  g_stats.add_crcs_host_small.store(0);
-  g_stats.add_crcs_host_nodev.store(0);
-  g_stats.add_crcs_gpu_fallback.store(0);
+  for (auto *a : {&g_stats.add_crcs_gpu, &g_stats.add_crcs_host_small, &g_stats.add_crcs_host_nodev,
+                  &g_stats.add_crcs_gpu_fallback, &g_stats.read_gpu, &g_stats.read_gpu_fallback, &g_stats.wal_gpu,
+                  &g_stats.wal_gpu_fallback, &g_stats.nodev_host})
+    a->store(0);
   g_stats.last_fallback_error.store(0);
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <emmintrin.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -13,6 +14,33 @@ namespace hc {
 inline int env_int(const char *name, int dflt) {
   const char *v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
+}
+
+// Host entries with a host path of their own switch to the GPU batch at these
+// sizes (the measured GPU/host crossover per call, DESIGN.md 5.2,
+// tools/crossover.py); each is overridable per call by its HC_*_GPU_MIN_BLOCKS.
+constexpr uint64_t kAddCrcsGpuMinBlocks = 256;  // hc_add_crcs (output blocks)
+constexpr uint64_t kReadGpuMinBlocks = 256;     // hc_read_from_disk[_v] (blocks to hash)
+constexpr uint64_t kWalGpuMinBlocks = 256;      // hc_wal_replay[_v] (blocks to verify)
+
+// Process-wide event counters behind hc_stats() (defined in hc_api.cpp).
+struct Stats {
+  std::atomic<uint64_t> add_crcs_gpu{0}, add_crcs_host_small{0}, add_crcs_host_nodev{0}, add_crcs_gpu_fallback{0};
+  std::atomic<uint64_t> read_gpu{0}, read_gpu_fallback{0}, wal_gpu{0}, wal_gpu_fallback{0}, nodev_host{0};
+  std::atomic<int64_t> last_fallback_error{0};
+};
+extern Stats g_stats;
+
+// HC_INJECT_FAIL=<site>[:nomem] (read per call, tests only): the named GPU
+// batch ("add_crcs", "read_from_disk", "wal_replay") reports HC_E_HIP (or
+// HC_E_NOMEM) without running, so the host recovery path can be tested on any
+// machine.  Returns 0 when `site` is not named.
+inline int injected_failure(const char *site) {
+  const char *v = std::getenv("HC_INJECT_FAIL");
+  if (!v || !*v) return 0;
+  const size_t n = std::strlen(site);
+  if (std::strncmp(v, site, n) != 0 || (v[n] != 0 && v[n] != ':')) return 0;
+  return (v[n] == ':' && std::strcmp(v + n + 1, "nomem") == 0) ? -4 /*HC_E_NOMEM*/ : -2 /*HC_E_HIP*/;
 }
 
 // HC_FORCE_GPU=1 routes the single-buffer drop-ins through the GPU batch path

@@ -179,7 +179,7 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
   if (start_block >= nblocks) return HC_OK;
   const uint64_t n = nblocks - start_block;
   const uint8_t *base = blocks + start_block * bs;
-  static const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", 256);
+  const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", (int)kWalGpuMinBlocks);  // per call: tools/crossover.py
   static const int threads_cfg = std::max(1, env_int("HC_WAL_THREADS", 16));  // 16: the GPU box's CPU share
   static const int trace = env_int("HC_WAL_TRACE", 0);
   // blocks per range at least HC_WAL_MIN_RANGE (64; read per call so tests can
@@ -199,12 +199,32 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
   double t0 = now_s(), tv = 0, ta = 0, tb = 0, tc = 0;
   parallel_for(2, [&](int role) {
     if (role == 0) {
+      bool on_gpu = false;
       if (n >= gpu_min || force_gpu()) {
-        vrc = hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
-      } else {
+        const int inj = injected_failure("wal_replay");
+        vrc = inj ? inj : hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
+        if (vrc >= 0) {  // HC_OK or the first bad block's reason
+          on_gpu = true;
+          vrc = HC_OK;
+          g_stats.wal_gpu.fetch_add(1, std::memory_order_relaxed);
+        } else if (!force_gpu()) {
+          // recovery fails only on a bad block or a framing error (wal.go:362-455):
+          // a GPU batch that cannot run finishes on the host path
+          if (vrc == HC_E_NODEV) {
+            g_stats.nodev_host.fetch_add(1, std::memory_order_relaxed);
+          } else {
+            g_stats.wal_gpu_fallback.fetch_add(1, std::memory_order_relaxed);
+            g_stats.last_fallback_error.store(vrc, std::memory_order_relaxed);
+          }
+          vrc = HC_OK;
+          first_bad = -1;
+        } else {
+          on_gpu = true;  // HC_FORCE_GPU: the error is returned
+        }
+      }
+      if (!on_gpu)
         for (uint64_t i = 0; i < n && first_bad < 0; i++)
           if (hc_check_block(base + i * bs, bs) != HC_OK) first_bad = (int64_t)i;
-      }
       tv = now_s() - t0;
       return;
     }

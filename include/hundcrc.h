@@ -343,16 +343,28 @@ int hc_device_count(void);
 int hc_host_pipelines(void);
 
 /* Process-wide event counters (monotonic since load or hc_stats_reset).
- * AddCRCsToData: calls whose CRCs ran as a GPU batch, on the host because the
- * output was below the GPU threshold, on the host because no gfx950 device
- * was usable, and on the host after a GPU batch failed (last_fallback_error =
- * that batch's HC_E_* code). */
+ * The three host entries that replace a reference function with a host path
+ * of its own -- AddCRCsToData (hc_add_crcs), ReadFromDisk (hc_read_from_disk*)
+ * and WAL recovery (hc_wal_replay*) -- run a GPU batch above their threshold
+ * and, when that batch cannot run or fails, finish on the host path instead
+ * of failing where the reference cannot (only HC_FORCE_GPU returns the error).
+ *   add_crcs_gpu / read_gpu / wal_gpu: calls whose batch ran on the GPU;
+ *   add_crcs_host_small: AddCRCsToData outputs below the GPU threshold;
+ *   add_crcs_host_nodev / nodev_host: GPU batch skipped, no usable gfx950
+ *     (AddCRCsToData / the other two);
+ *   *_gpu_fallback: GPU batch failed (HC_E_NOMEM, HC_E_HIP), finished on the
+ *     host; last_fallback_error = the last such batch's HC_E_* code. */
 typedef struct hc_stats_t {
   uint64_t add_crcs_gpu;
   uint64_t add_crcs_host_small;
   uint64_t add_crcs_host_nodev;
   uint64_t add_crcs_gpu_fallback;
   int64_t last_fallback_error;
+  uint64_t read_gpu;
+  uint64_t read_gpu_fallback;
+  uint64_t wal_gpu;
+  uint64_t wal_gpu_fallback;
+  uint64_t nodev_host;
 } hc_stats_t;
 int hc_stats(hc_stats_t *out);
 void hc_stats_reset(void);

@@ -299,6 +299,47 @@ def test_add_crcs_small_outputs_stay_on_host(hc, oracle):
     assert st["add_crcs_host_small"] == 1 and st["add_crcs_gpu"] == 0 and st["add_crcs_gpu_fallback"] == 0
 
 
+@pytest.mark.parametrize("inject", ["", "read_from_disk", "read_from_disk:nomem"])
+def test_read_from_disk_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypatch, inject):
+    """ReadFromDisk (block_manager.go:189-242) fails only on I/O or a CRC
+    mismatch: a verify batch above the GPU threshold that cannot run (no gfx950
+    here, or a simulated HC_E_HIP / HC_E_NOMEM) verifies on the host path --
+    payload, final offset and the failing block as the oracle says -- counted
+    in hc_stats.  HC_FORCE_GPU returns the failure instead."""
+    B, nb = 4096, 300
+    img = np.zeros(nb * B, dtype=np.uint8)
+    rng = np.random.default_rng(77)
+    img[:] = rng.integers(0, 256, img.size, dtype=np.uint8)
+    for i in range(nb):
+        hc.AddCRCToBlockData(img[i * B:(i + 1) * B])
+    if inject:
+        monkeypatch.setenv("HC_INJECT_FAIL", inject)
+    monkeypatch.setenv("HC_READ_GPU_MIN_BLOCKS", "256")
+    start, size = 4 + 7, nb * (B - 4) - 100
+    for corrupt in (None, 201):
+        view = img.copy()
+        if corrupt is not None:
+            view[corrupt * B + 9] ^= 4
+        hc.stats_reset()
+        got, fo, err = hc.ReadFromDisk(view.tobytes(), B, start, size)
+        want, wfo, wrc, wbad = oracle.read_from_disk(view.tobytes(), B, start, size)
+        if corrupt is None:
+            assert err is None and bytes(got) == bytes(want) and fo == wfo
+        else:
+            assert str(err) == "CRC mismatch in block" and hc.last_bad_block() == corrupt == wbad
+        st = hc.stats()
+        if inject:
+            assert st["read_gpu_fallback"] == 1 and st["read_gpu"] == 0
+        elif hc.device_count() == 0:
+            assert st["nodev_host"] == 1 and st["read_gpu"] == 0
+        else:
+            assert st["read_gpu"] == 1
+    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    if inject or hc.device_count() == 0:
+        with pytest.raises(hc.HundCRCError):
+            hc.ReadFromDisk(img.tobytes(), B, start, size)
+
+
 def test_read_from_disk_host(hc, golden, oracle):
     """hc_read_from_disk (row f1) on the host path: the golden ReadFromDisk cases,
     then random (start, size) over a larger image with corruptions, vs the oracle."""

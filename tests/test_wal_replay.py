@@ -179,3 +179,39 @@ def test_wal_replay_random_pieces_vs_oracle(hc, oracle, seed, ranges):
         got, err, bad, pos = hc.wal_replay(bytes(view), 4096, sb, 4, mr)
         assert (0 if err is None else err.code) == wrc
         assert got == want and pos == wpos and bad == wbad
+
+
+@pytest.mark.parametrize("inject", ["", "wal_replay", "wal_replay:nomem"])
+def test_wal_replay_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypatch, inject):
+    """A replay above the GPU threshold whose verify batch cannot run (no gfx950
+    here, or a simulated HC_E_HIP / HC_E_NOMEM) verifies on the host path and
+    returns what the oracle's wal.go:362-455 does -- including a corrupt block
+    -- counted in hc_stats; recovery fails only where the reference does."""
+    sizes = [oracle.lib().oc_wal_record_size(7, i, 64, 20000) for i in range(400)]
+    b, _, _ = oracle.wal_frame(7, sizes)
+    img = bytearray(b.tobytes())
+    nb = len(img) // 4096
+    assert nb >= 256
+    monkeypatch.setenv("HC_WAL_GPU_MIN_BLOCKS", "256")
+    if inject:
+        monkeypatch.setenv("HC_INJECT_FAIL", inject)
+    for corrupt in (None, nb // 2):
+        view = bytearray(img)
+        if corrupt is not None:
+            view[corrupt * 4096 + 100] ^= 1
+        hc.stats_reset()
+        want, wrc, wbad, wpos = oracle.wal_replay(bytes(view), 4096, 0, 4, 0)
+        got, err, bad, pos = hc.wal_replay(bytes(view), 4096)
+        assert (0 if err is None else err.code) == wrc and got == want and pos == wpos and bad == wbad
+        st = hc.stats()
+        if inject:
+            assert st["wal_gpu_fallback"] == 1 and st["wal_gpu"] == 0
+            assert st["last_fallback_error"] == (hc.HC_E_NOMEM if "nomem" in inject else hc.HC_E_HIP)
+        elif hc.device_count() == 0:
+            assert st["nodev_host"] == 1 and st["wal_gpu"] == 0 and st["wal_gpu_fallback"] == 0
+        else:
+            assert st["wal_gpu"] == 1 and st["wal_gpu_fallback"] == 0
+    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    if inject or hc.device_count() == 0:
+        with pytest.raises(hc.HundCRCError):
+            hc.wal_replay(bytes(img), 4096)
