@@ -72,6 +72,10 @@ struct DeviceState {
   std::mutex seg_mu;
   uint32_t *seg_ws = nullptr;
   uint64_t seg_ws_bytes = 0;
+  // the packed-record stream's "did not take the batch" word and per-call tag
+  // (Batch::seg_slot)
+  unsigned long long *seg_slot = nullptr;
+  std::atomic<uint64_t> seg_tag{0};
 };
 
 constexpr int kMaxDevices = 64;
@@ -150,6 +154,11 @@ int init_device(int dev) {
       return;
     }
     d.skip_slot = static_cast<unsigned long long *>(p);
+    if (hipMalloc(&p, 8) != hipSuccess || hipMemset(p, 0, 8) != hipSuccess) {
+      d.status = HC_E_NOMEM;
+      return;
+    }
+    d.seg_slot = static_cast<unsigned long long *>(p);
     d.cus = prop.multiProcessorCount;
     d.status = HC_OK;
   });
@@ -201,9 +210,14 @@ uint64_t seg_min_msgs() {
 // The kept workspace (null stream only), grown to `need` bytes on that stream,
 // so the free is ordered after every earlier use.  The lock is held from here
 // until the caller has enqueued the launches that use it.  nullptr: allocate
-// per call.
+// per call.  Only workspaces up to kSegKeepBytes are kept (about 16M records):
+// a larger one would stay pinned in the default mempool for the life of the
+// process, and its per-call allocation is small against the batch.
+// Relies on the legacy null stream's ordering across host threads (hundcrc.h;
+// the library is not built with -fgpu-default-stream=per-thread).
+constexpr uint64_t kSegKeepBytes = 64ull << 20;
 uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::unique_lock<std::mutex> &lk) {
-  if (s != nullptr) return nullptr;
+  if (s != nullptr || need > kSegKeepBytes) return nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   lk = std::unique_lock<std::mutex>(d.seg_mu);
@@ -211,7 +225,7 @@ uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::uniqu
   if (d.seg_ws) (void)hipFreeAsync(d.seg_ws, s);
   d.seg_ws = nullptr;
   d.seg_ws_bytes = 0;
-  const uint64_t bytes = need + need / 4;  // headroom for a slightly larger next batch
+  const uint64_t bytes = std::min(kSegKeepBytes, need + need / 4);  // headroom for a slightly larger next batch
   if (hipMallocAsync(reinterpret_cast<void **>(&d.seg_ws), bytes, s) != hipSuccess) {
     d.seg_ws = nullptr;
     lk.unlock();
@@ -268,6 +282,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
   } else {
     uint32_t *seg_ws = nullptr;           // a per-call workspace (else the kept one, under seg_lock)
     std::unique_lock<std::mutex> seg_lock;  // held while the kept workspace's launches are enqueued
+    bool seg = false;
     // the stream's only output is crc_out (k_seg_combine): a batch without it
     // (verify or stamp only) takes k_crc_grp + k_crc_any
     if (seg_ok && (flags & kFlagMessages) && crc_out && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
@@ -279,19 +294,31 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
         const uint64_t need = seg_workspace_bytes(n, mu);
         uint32_t *ws = seg_cached_ws(d, s, need, seg_lock);
         if (!ws && hipMallocAsync(reinterpret_cast<void **>(&seg_ws), need, s) == hipSuccess) ws = seg_ws;
-        if (ws && (e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last)) == hipSuccess)
-          b.seg_flag = ws;  // word 0: raised when the stream did not take the batch
+        if (ws) {
+          b.seg_slot = d.seg_slot;
+          b.seg_tag = d.seg_tag.fetch_add(1, std::memory_order_relaxed) + 1;
+          e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last);
+          seg = true;
+        }
       }
     }
-    // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk
-    // size, utils/config/config.go:137); the k_crc_any sweep does the rest
-    b.skip_slot = d.skip_slot;
-    b.skip_tag = d.skip_tag.fetch_add(1, std::memory_order_relaxed) + 1;
-    if (e == hipSuccess) e = launch_grp(b, fast_grid, s);
-    if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
+    if (seg) {
+      // the fallback, for a batch the stream did not take: k_crc_any over every
+      // message (it exits at once when the stream took the batch).  One launch
+      // instead of round 3's k_crc_grp + sweep: a batch of messages that is
+      // not packed is rarely made of aligned 4 KiB multiples.
+      if (e == hipSuccess) e = launch_general(b, 0, gen_grid, s);
+    } else {
+      // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk
+      // size, utils/config/config.go:137); the k_crc_any sweep does the rest
+      b.skip_slot = d.skip_slot;
+      b.skip_tag = d.skip_tag.fetch_add(1, std::memory_order_relaxed) + 1;
+      if (e == hipSuccess) e = launch_grp(b, fast_grid, s);
+      if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
+    }
     if (seg_ws && hipFreeAsync(seg_ws, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;
-    info.kernel = b.seg_flag ? "k_seg_stream|k_crc_grp+k_crc_any" : "k_crc_grp+k_crc_any";
-    t_seg_dev = b.seg_flag ? dev : -1;
+    info.kernel = seg ? "k_seg_stream+k_seg_combine|k_crc_any" : "k_crc_grp+k_crc_any";
+    t_seg_dev = seg ? dev : -1;
     info.fast_blocks = n;  // routing is decided on the device per block
   }
   t_last = info;

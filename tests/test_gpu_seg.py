@@ -86,9 +86,10 @@ def test_seg_boundaries_and_shapes(cuda, hc, oracle, seg_all):
 
 
 def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
-    """Batches the stream does not take are hashed by k_crc_grp + k_crc_any
-    (the device flag): a gap, an overlap, unsorted records, and 65 events in
-    one 4 KiB group (records under 64 B)."""
+    """Batches the stream does not take are hashed by k_crc_any (the device
+    slot raised to the call's tag): a gap, an overlap, unsorted records, and 65
+    events in one 4 KiB group (records under 64 B) -- found on the stream's own
+    event windows since round 4 (no k_seg_plan)."""
     torch = cuda
     rng = np.random.default_rng(11)
     total = 8 << 20
@@ -115,7 +116,7 @@ def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
 def test_seg_record_cap(cuda, hc, oracle, seg_all):
     """k_seg_combine chains the raw CRCs of the whole units a record spans, so
     the stream takes records up to 16 MiB (1024 units) and a batch with a
-    longer one falls back to k_crc_grp + k_crc_any on the device."""
+    longer one falls back to k_crc_any on the device."""
     torch = cuda
     rng = np.random.default_rng(17)
     total = 40 << 20
