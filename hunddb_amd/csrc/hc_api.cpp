@@ -1311,12 +1311,15 @@ int hc_dev_add_crcs(int device, const void *src, uint64_t n, void *dst, uint32_t
   if (n == 0) return HC_OK;  // Go returns an empty slice
   if (!src || !dst) return HC_E_ARG;
   if ((reinterpret_cast<uintptr_t>(dst) & 15u) != 0) return HC_E_LAYOUT;
+  const uint64_t nblk = (n + kPayloadPerBlock - 1) / kPayloadPerBlock;
+  // k_frame: edges + one interior block per wave
+  const uint64_t wgs = 1 + (nblk > 2 ? kFrameSpread * ((nblk - 2 + 4 * kFrameSpread - 1) / (4 * kFrameSpread)) : 0);
+  if (wgs > kMaxGridWgs) return HC_E_ARG;  // over 2^32 work-items (~68 TB of payload)
   int st = init_device(device);
   if (st != HC_OK) return st;
   DeviceGuard g(device);
   DeviceState &d = g_dev[device];
-  const uint64_t nblk = (n + kPayloadPerBlock - 1) / kPayloadPerBlock;
-  const int grid = (int)std::min<uint64_t>(1 + (nblk > 2 ? kFrameSpread * ((nblk - 2 + 4 * kFrameSpread - 1) / (4 * kFrameSpread)) : 0), 0x7FFFFFFF);  // k_frame: edges + one interior block per wave
+  const int grid = (int)wgs;
   hc_launch_info info{"k_frame", nblk, 0, n + nblk * HC_BLOCK_SIZE, (uint32_t)grid, 256, kLaneQWords * 4};
   t_last = info;
   return launch_frame(static_cast<const uint8_t *>(src), n, static_cast<uint8_t *>(dst), crc_out, d.dtab, grid,
@@ -1332,12 +1335,13 @@ int hc_dev_read_blocks(int device, const void *blocks, uint64_t nblocks, uint32_
   uint32_t lg = 0;
   while (lg < 3 && (HC_BLOCK_SIZE << lg) != block_size) lg++;
   if (lg == 3 || (reinterpret_cast<uintptr_t>(blocks) & 15u) != 0) return HC_E_LAYOUT;
+  if (unframe_grid(nblocks, lg) > kMaxGridWgs) return HC_E_ARG;  // over 2^32 work-items
   int st = init_device(device);
   if (st != HC_OK) return st;
   DeviceGuard g(device);
   DeviceState &d = g_dev[device];
-  hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4),
-                      (uint32_t)std::min<uint64_t>(unframe_grid(nblocks, lg), 0xFFFFFFFFull), 256, kLaneQWords * 4};
+  hc_launch_info info{"k_unframe", nblocks, 0, nblocks * (2ull * block_size - 4), (uint32_t)unframe_grid(nblocks, lg),
+                      256, kLaneQWords * 4};
   t_last = info;
   return launch_unframe(static_cast<const uint8_t *>(blocks), nblocks, lg, static_cast<uint8_t *>(payload_out),
                         crc_out, bad_bitmap, reinterpret_cast<unsigned long long *>(first_bad), d.dtab,

@@ -64,7 +64,7 @@ struct Gf2 {
   }
 };
 
-// Device constant image (one per device, 20 KiB), uploaded once.
+// Device constant image (one per device, 24.75 KiB), uploaded once.
 //   tg[k][b]   = shift(b << 8k, kRowBytes)        Horner step across a row
 //   s4[k][b]   = shift(b << 8k, 4)                lane stream combine
 //   lane[l][i] = shift(1 << i, kRowBytes - 12 - 16 l)   lane placement

@@ -2024,7 +2024,7 @@ hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *
   // workgroup 0: the two edge blocks; then one interior block per wave, in
   // runs of 4 x kFrameSpread blocks over kFrameSpread workgroups
   const uint64_t wgs = 1 + (nblk > 2 ? kFrameSpread * ((nblk - 2 + 4 * kFrameSpread - 1) / (4 * kFrameSpread)) : 0);
-  if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  if (wgs > kMaxGridWgs) return hipErrorInvalidValue;  // gridDim.x * 256 must stay below 2^32
   hipLaunchKernelGGL(k_frame, dim3((unsigned)wgs), dim3(256), 0, s, src, n, dst, nblk, crc_out, tables);
   return hipGetLastError();
 }
@@ -2035,7 +2035,7 @@ hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_grou
   if (nblk == 0) return hipSuccess;
   if (!blocks || !out || lg_groups > 2) return hipErrorInvalidValue;
   const uint64_t grid = unframe_grid(nblk, lg_groups);  // one 4 KiB group per wave, 4 waves per workgroup
-  if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  if (grid > kMaxGridWgs) return hipErrorInvalidValue;  // gridDim.x * 256 must stay below 2^32
 #define HC_UNFRAME(L)                                                                                      \
   hipLaunchKernelGGL((k_unframe<L>), dim3((unsigned)grid), dim3(256), 0, s, blocks, nblk, out, crc_out, bad_bitmap, \
                      first_bad, tables)

@@ -64,21 +64,26 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
 bool grp_xcd(uint32_t block_bytes, int grid, uint64_t nblocks);
 uint32_t grp_lg_chunk(uint64_t nblocks, int grid, uint32_t block_bytes);
 hipError_t launch_grp(const Batch &b, int grid, hipStream_t s);
+// (launch_frame and launch_unframe refuse grids of more than kMaxGridWgs
+// 256-thread workgroups: HIP's limit is gridDim.x * blockDim.x < 2^32.)
+constexpr uint64_t kMaxGridWgs = 0xFFFFFFFFull / 256;
 // Fused AddCRCsToData: frame n payload bytes into (n+4091)/4092 stamped 4096-B
-// blocks (k_frame_edges + k_frame; `grid` is unused: one interior block per wave).
+// blocks in ONE launch of k_frame (its workgroup 0 does the two edge blocks,
+// every other wave one interior block; `grid` is unused).
 constexpr uint32_t HC_FRAME_BLOCK = 4096;
 hipError_t launch_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *crc_out,
                         const DeviceTables *tables, int grid, hipStream_t s);
 constexpr uint32_t kLaneQWords = 8 * kLanes * 4;  // k_frame / k_unframe: LDS copy of DeviceTables::lane_q
-// k_unframe: one 4 KiB group per wave, 4-wave workgroups (a block's groups in one
-// workgroup); 4 KiB blocks go in runs of 4 x kFrameSpread over kFrameSpread
-// workgroups, 8 KiB blocks in runs of 8 over 4 (one output alignment per
-// workgroup), so those grids are multiples of kFrameSpread / 4
-// k_frame / k_unframe (4 KiB): a workgroup's four waves take blocks kFrameSpread
-// apart, kFrameSpread neighbouring workgroups one contiguous run of 4 x
-// kFrameSpread blocks.  A multiple of 4, so b mod 4 -- the 4092-B stride's
-// misalignment -- is one per workgroup.  Spreads 4 / 8 / 16 / 32 measured
-// (profiles/r3/kframe4/): 8 is the fastest.
+
+// Geometry of the framing kernels (256-thread, 4-wave workgroups):
+//   * k_frame and k_unframe at 4 KiB: a workgroup's four waves take blocks
+//     kFrameSpread apart, kFrameSpread neighbouring workgroups one contiguous
+//     run of 4 x kFrameSpread blocks.  kFrameSpread is a multiple of 4, so b mod
+//     4 -- the 4092-B stride's misalignment -- is one per workgroup.  Spreads 4
+//     / 8 / 16 / 32 measured (profiles/r3/kframe4/): 8 is the fastest.
+//   * k_unframe at 8 / 16 KiB: one 4 KiB group per wave, a block's groups in
+//     one workgroup; 8 KiB blocks in runs of 8 over 4 workgroups (one output
+//     alignment per workgroup), 16 KiB blocks one per workgroup.
 constexpr uint32_t kFrameSpread = 8;
 inline uint64_t unframe_grid(uint64_t nblk, uint32_t lg_groups) {
   return lg_groups == 0 ? kFrameSpread * ((nblk + 4 * kFrameSpread - 1) / (4 * kFrameSpread))
@@ -87,7 +92,8 @@ inline uint64_t unframe_grid(uint64_t nblk, uint32_t lg_groups) {
 }
 // Batched ReadFromDisk: verify nblk blocks of 4096 << lg_groups bytes at `blocks`
 // (16-B aligned) and write their payloads back to back at `out`.  Its own grid
-// (4-wave workgroups, 16 KiB of blocks per wave).
+// (unframe_grid: 4-wave workgroups, one 4 KiB group per wave).  Refused
+// (hipErrorInvalidValue) when the grid's work-items would pass 2^32 - 1.
 hipError_t launch_unframe(const uint8_t *blocks, uint64_t nblk, uint32_t lg_groups, uint8_t *out,
                           uint32_t *crc_out, uint32_t *bad_bitmap, unsigned long long *first_bad,
                           const DeviceTables *tables, hipStream_t s);

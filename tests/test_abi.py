@@ -503,3 +503,19 @@ def test_read_from_disk_zero_size_null_out(hc, oracle):
         assert rc == wrc == 0 and fo.value == wfo and bad.value == -1 and hashed.value == 0, start
         assert hc.read_blocks_touched(B, start, 0) == 0
 
+
+
+def test_framing_grids_refused_past_2_to_32_work_items(hc):
+    """gridDim.x * 256 must stay below 2^32; a device ReadFromDisk
+    or AddCRCsToData whose grid would pass it is refused with HC_E_ARG before
+    any device call (so this runs without a GPU)."""
+    L = hc.lib()
+    fake = 1 << 40  # never dereferenced: the size check comes first
+    rc = L.hc_dev_read_blocks(0, fake, 1 << 40, 16384, fake, None, None, None, None)
+    assert rc == hc.HC_E_ARG
+    rc = L.hc_dev_add_crcs(0, fake, 1 << 62, fake, None, None)
+    assert rc == hc.HC_E_ARG
+    # the largest 16 KiB batch that fits: not refused for its size (NODEV here, or enqueued on a GPU
+    # would need real memory: only the size check is exercised, with a device count of 0)
+    if hc.device_count() == 0:
+        assert L.hc_dev_read_blocks(0, fake, (0xFFFFFFFF // 256), 16384, fake, None, None, None, None) == hc.HC_E_NODEV

@@ -17,6 +17,7 @@
 #   pmc        one rocprofv3 --pmc pass per ';'-separated counter group of $PMC over $PMC_CMD
 #   rehearse   bench.py --gpus 2 over gloo, two ranks sharing the one GPU
 #   extra      bash -c "$EXTRA"
+#   extras     bash -c "$EXTRA1" ... "$EXTRA9", one step each
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
@@ -73,6 +74,14 @@ for s in "${LIST[@]}"; do
       --cpu-seconds 0 --pmc off --json-out "$OUT/rehearse_n2.json" || stop $? ;;
   extra)
     st extra 900 bash -c "${EXTRA:?EXTRA=command}" || stop $? ;;
+  extras)
+    # EXTRA1 .. EXTRA9, each its own step (extra1.log ...); a plain failure
+    # (rc 1) goes on to the next, a fault / abort / time limit ends the session
+    for k in 1 2 3 4 5 6 7 8 9; do
+      v="EXTRA$k"
+      [ -n "${!v:-}" ] || continue
+      st "extra$k" 600 bash -c "${!v}"; rc=$?; ok $rc || stop $rc
+    done ;;
   *)
     echo "[sess] unknown step $s"; exit 2 ;;
   esac
