@@ -13,9 +13,6 @@ k = k.replace("void k_crc_grp(", "void k_crc_grp_perm(")
 old = "unsigned long long *__restrict__ skip_slot = nullptr,"
 assert old in k
 k = k.replace(old, "uint64_t perm, uint64_t nchunks, unsigned long long *__restrict__ skip_slot = nullptr,")
-old = "const uint32_t *__restrict__ seg_flag = nullptr,"
-assert old in k
-k = k.replace(old, "const uint32_t *__restrict__ seg_flag,")
 old = "auto blk_of = [&](uint32_t k) -> uint64_t { return (((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask); };"
 assert old in k
 k = k.replace(old, """auto blk_of = [&](uint32_t k) -> uint64_t {

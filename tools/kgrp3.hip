@@ -85,10 +85,10 @@ int main(int argc, char **argv) {
     return [&, lg, p, q, xcd](hipStream_t st) {
       if (xcd)
         hipLaunchKernelGGL((hc::k_crc_grp_perm<false, true>), dim3(cus), dim3(hc::kFastThreads), 0, st, b.base, nullptr,
-                           nullptr, b.stride, b.ulen, 0u, N, lg, crc, nullptr, nullptr, dt, nullptr, p, q);
+                           nullptr, b.stride, b.ulen, 0u, N, lg, crc, nullptr, nullptr, dt, p, q);
       else
         hipLaunchKernelGGL((hc::k_crc_grp_perm<false, false>), dim3(cus), dim3(hc::kFastThreads), 0, st, b.base,
-                           nullptr, nullptr, b.stride, b.ulen, 0u, N, lg, crc, nullptr, nullptr, dt, nullptr, p, q);
+                           nullptr, nullptr, b.stride, b.ulen, 0u, N, lg, crc, nullptr, nullptr, dt, p, q);
     };
   };
   for (uint32_t lg : {7u, 5u}) {
