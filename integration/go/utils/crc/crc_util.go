@@ -271,3 +271,27 @@ func WalReplay(blocks []byte, blockSize int, startOffset uint64) (WalWindow, err
 	}
 	return w, goErr(rc)
 }
+
+// LibraryStats are the library's process-wide event counters (hc_stats): how
+// many AddCRCsToData / ReadFromDisk / WAL-recovery batches ran on the GPU, and
+// how many finished on the host path because no gfx950 was usable or the GPU
+// batch failed (LastFallbackError: the last failure's library code).  For
+// metrics; the reference has no counterpart.
+type LibraryStats struct {
+	AddCRCsGPU, AddCRCsHostSmall, AddCRCsHostNoDev, AddCRCsGPUFallback uint64
+	LastFallbackError                                                  int64
+	ReadGPU, ReadGPUFallback, WALGPU, WALGPUFallback, NoDevHost        uint64
+}
+
+// Stats reads the counters.
+func Stats() LibraryStats {
+	var out C.hc_stats_t
+	C.hc_stats(&out)
+	return LibraryStats{
+		AddCRCsGPU: uint64(out.add_crcs_gpu), AddCRCsHostSmall: uint64(out.add_crcs_host_small),
+		AddCRCsHostNoDev: uint64(out.add_crcs_host_nodev), AddCRCsGPUFallback: uint64(out.add_crcs_gpu_fallback),
+		LastFallbackError: int64(out.last_fallback_error),
+		ReadGPU: uint64(out.read_gpu), ReadGPUFallback: uint64(out.read_gpu_fallback),
+		WALGPU: uint64(out.wal_gpu), WALGPUFallback: uint64(out.wal_gpu_fallback), NoDevHost: uint64(out.nodev_host),
+	}
+}
