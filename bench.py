@@ -678,8 +678,8 @@ def main(argv=None):
                                   else "HIP events on the launch stream around every timed launch"),
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
-                **({"launch_note": "one dispatch = k_seg_stream + k_seg_combine + k_crc_any (the fallback, "
-                                   "exits at once when the stream took the batch); traffic: k_seg_stream"}
+                **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine + k_crc_any (the "
+                                   "fallback, exits at once when the stream took the batch); traffic: k_seg_stream"}
                    if bsize == "records" else {}),
                 "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"

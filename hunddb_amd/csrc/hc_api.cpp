@@ -72,10 +72,6 @@ struct DeviceState {
   std::mutex seg_mu;
   uint32_t *seg_ws = nullptr;
   uint64_t seg_ws_bytes = 0;
-  // the packed-record stream's "did not take the batch" word and per-call tag
-  // (Batch::seg_slot)
-  unsigned long long *seg_slot = nullptr;
-  std::atomic<uint64_t> seg_tag{0};
 };
 
 constexpr int kMaxDevices = 64;
@@ -154,11 +150,7 @@ int init_device(int dev) {
       return;
     }
     d.skip_slot = static_cast<unsigned long long *>(p);
-    if (hipMalloc(&p, 8) != hipSuccess || hipMemset(p, 0, 8) != hipSuccess) {
-      d.status = HC_E_NOMEM;
-      return;
-    }
-    d.seg_slot = static_cast<unsigned long long *>(p);
+
     d.cus = prop.multiProcessorCount;
     d.status = HC_OK;
   });
@@ -295,9 +287,8 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
         uint32_t *ws = seg_cached_ws(d, s, need, seg_lock);
         if (!ws && hipMallocAsync(reinterpret_cast<void **>(&seg_ws), need, s) == hipSuccess) ws = seg_ws;
         if (ws) {
-          b.seg_slot = d.seg_slot;
-          b.seg_tag = d.seg_tag.fetch_add(1, std::memory_order_relaxed) + 1;
           e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last);
+          b.seg_flag = ws;  // word 0: raised when the stream did not take the batch
           seg = true;
         }
       }
@@ -317,7 +308,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
     }
     if (seg_ws && hipFreeAsync(seg_ws, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;
-    info.kernel = seg ? "k_seg_stream+k_seg_combine|k_crc_any" : "k_crc_grp+k_crc_any";
+    info.kernel = seg ? "k_seg_plan+k_seg_stream+k_seg_combine|k_crc_any" : "k_crc_grp+k_crc_any";
     t_seg_dev = seg ? dev : -1;
     info.fast_blocks = n;  // routing is decided on the device per block
   }
@@ -885,13 +876,15 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
     // HC_COPY_THREADS threads frame dst: the two overlap instead of framing
     // first and reading dst back.  The ragged last block (zero-padded) is
     // hashed on the host after framing.
-    const int T = std::max(1, env_int("HC_COPY_THREADS", 8));
+    // framing tasks: HC_COPY_THREADS (8), one per MiB of output at most
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max(1, env_int("HC_COPY_THREADS", 8)), nb >> 8));
     std::vector<uint32_t> crc(nfull);
     int rc = HC_OK;
     // (plain stores: streamed framing measured 10-35 % slower, profiles/r2/addcrcs/)
+    // task 0 is the GPU batch, so the caller starts it at once
     parallel_for(T + 1, [&](int t) {
-      if (t < T) {
-        frame(nb * t / T, nb * (t + 1) / T);
+      if (t > 0) {
+        frame(nb * (t - 1) / T, nb * t / T);
         return;
       }
       if (!nfull) return;
@@ -910,7 +903,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
       }
     });
     if (rc == HC_OK) {
-      parallel_for(T, [&](int t) {
+      parallel_for(T, [&](int t) {  // the words into the framed blocks
         for (size_t k = nfull * t / T, e = nfull * (t + 1) / T; k < e; k++)
           std::memcpy(dst + k * HC_BLOCK_SIZE, &crc[k], 4);
       });
@@ -1232,11 +1225,14 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
     hv.bitmap = badj.data();
     // the copy-out runs on HC_COPY_THREADS threads while the batch verifies;
     // on a CRC failure `out` is left unspecified (Go returns no data)
-    const int T = std::max(1, env_int("HC_COPY_THREADS", 8));
+    // copy-out tasks: HC_COPY_THREADS (8), one per MiB of blocks at most; task 0
+    // is the GPU batch, so the caller starts it at once
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max(1, env_int("HC_COPY_THREADS", 8)),
+                                                                 k * B >> 20));
     int rc = HC_OK;
     parallel_for(T + 1, [&](int t) {
-      if (t < T) {
-        copy_out(k * t / T, k * (t + 1) / T);
+      if (t > 0) {
+        copy_out(k * (t - 1) / T, k * t / T);
         return;
       }
       if ((rc = injected_failure("read_from_disk")) != HC_OK) return;

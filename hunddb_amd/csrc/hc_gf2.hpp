@@ -64,13 +64,15 @@ struct Gf2 {
   }
 };
 
-// Device constant image (one per device, 24.75 KiB), uploaded once.
+// Device constant image (one per device, 32.75 KiB), uploaded once.
 //   tg[k][b]   = shift(b << 8k, kRowBytes)        Horner step across a row
 //   s4[k][b]   = shift(b << 8k, 4)                lane stream combine
 //   lane[l][i] = shift(1 << i, kRowBytes - 12 - 16 l)   lane placement
 //   w0         = shift^-1(0xFFFFFFFF, 4)           Go's init as a prefix word
 //   lane_q[q][l][r] = lane[l][4q + r]              the placement columns regrouped
 //                    for a workgroup-shared LDS copy read by ds_read_b128
+//   sh512[0][k][b] = shift(b << 8k, 512), sh512[1][k][b] = shift^-1(b << 8k, 512)
+//                    k_crc_grp's paired placement (two blocks, one mat-vec)
 struct DeviceTables {
   uint32_t tg[4][256];
   uint32_t s4[4][256];
@@ -79,9 +81,13 @@ struct DeviceTables {
   uint32_t pad[63];
   uint32_t lane_q[8][kLanes][4];
   uint32_t sh4k[4][32];  // columns of shift(., 4096 (j+1) bytes), j = 0..2 (k_unframe's group combine); [3] unused
+  // k_crc_grp's paired placement: [0][k][b] = shift(b << 8k, 512), [1][k][b] = shift^-1(b << 8k, 512)
+  uint32_t sh512[2][4][256];
 };
 static_assert(sizeof(DeviceTables) % 256 == 0, "keep the image 256-B multiple");
 
+struct Mat32;
+inline void build_sh512(DeviceTables &d);
 inline void build_device_tables(DeviceTables &d) {
   Gf2 g;
   for (int k = 0; k < 4; k++)
@@ -98,6 +104,7 @@ inline void build_device_tables(DeviceTables &d) {
       for (int r = 0; r < 4; r++) d.lane_q[q][l][r] = d.lane[l][4 * q + r];
   for (int j = 0; j < 4; j++)
     for (int i = 0; i < 32; i++) d.sh4k[j][i] = j < 3 ? g.shift_bytes(1u << i, 4096ull * (j + 1)) : 0u;
+  build_sh512(d);
 }
 
 // 32x32 GF(2) matrix by columns: c[i] = M e_i (host side only).
@@ -145,6 +152,16 @@ inline Mat32 shift_mat(const Gf2 &g, uint64_t n) {
   Mat32 m;
   for (int i = 0; i < 32; i++) m.c[i] = g.shift_bytes(1u << i, n);
   return m;
+}
+
+inline void build_sh512(DeviceTables &d) {
+  Gf2 g;
+  const Mat32 f = shift_mat(g, 512), inv = mat_inverse(f);
+  for (int k = 0; k < 4; k++)
+    for (uint32_t b = 0; b < 256; b++) {
+      d.sh512[0][k][b] = mat_apply(f, b << (8 * k));
+      d.sh512[1][k][b] = mat_apply(inv, b << (8 * k));
+    }
 }
 
 // Constant image of the packed-record path (k_seg_*; 164 KiB, global memory):

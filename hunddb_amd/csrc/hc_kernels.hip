@@ -155,7 +155,8 @@ __device__ __forceinline__ void lane0_atomic_umin64(unsigned long long *p, uint6
 // one is hashed.  Round 1 (tools/kbench, profiles/r1/glds/): non-temporal
 // loads +17 %, a ring of 4 best, this block order 0-7 % ahead of contiguous
 // runs per wave.  The LDS-staged ring it was measured against, the timing-only
-// build and the round-1 off/len path live in tools/ab_hc_kernels.hip.
+// build and the round-1 off/len path are in git history (tools/ab_hc_kernels.hip,
+// up to commit 61a2e0e).
 constexpr int kFastRing = 4;
 
 // Row load, 16 B per lane, non-temporal (the blocks are read once).
@@ -339,8 +340,19 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
 //     group, never stored) and is left to k_crc_any (fast_mask 4095).
 //   * kXcd: workgroup g runs on XCD g % 8; the chunk slots are renumbered so
 //     that each XCD's workgroups own neighbouring chunks (grp_xcd decides).
-// The variants measured against this one (static deal, batched refills,
-// nibble finalise tables, timing-only build) are in tools/ab_hc_kernels.hip.
+//   * Paired placement (round 4): a wave finalises its blocks two at a time.
+//     Lane l's placement M_l (shift by 1012 - 16 l bytes) is shift(512) of
+//     lane l+32's, so block A folds lanes l and l+32 into lane l+32 (d_{l+32} ^
+//     shift(d_l, 512)) and block B into lane l (d_l ^ shift(d_{l+32}, -512)):
+//     one 4-lookup shift (lanes 0-31 forward, 32-63 inverse, 8 KiB of LDS), a
+//     v_permlane32_swap, ONE 32x32 mat-vec for both, and the XORs of the lower
+//     and upper halves.  The block waiting for a partner keeps d in a VGPR; the
+//     wave's last odd block is finalised alone.  Against one mat-vec a block:
+//     SQ_INSTS_VALU -11.5 % at 1M x 4 KiB, +0.65 points at 4 KiB and +0.17 at
+//     8 KiB over five and four same-box A/B pairs (profiles/r4/r4a, r4b, r4c).
+// The variants measured against this one before round 4 (static deal, batched
+// refills, nibble finalise tables, timing-only build) are in git history
+// (tools/ab_hc_kernels.hip, up to commit 61a2e0e).
 template <bool kArrays, bool kXcd = false>
 __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ lens, uint64_t stride,
@@ -351,11 +363,12 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
                                                          const DeviceTables *__restrict__ tables,
                                                          unsigned long long *__restrict__ skip_slot = nullptr,
                                                          uint64_t skip_tag = 0) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 2048];
   __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   fill_crc_tables(lds, tables, tid, kFastThreads);
+  for (uint32_t q = tid; q < 2048; q += kFastThreads) lds[kFastLdsBytes / 4 + q] = (&tables->sh512[0][0][0])[q];
   if (tid == 0) s_next = 3 * kFastWaves;  // indices 0 .. 3W-1 are dealt statically below
   uint32_t col[32];
 #pragma unroll
@@ -379,6 +392,16 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
     const uint32_t t2 = lds_u32(lds, S4base + 8192u + (((x >> 16) & 255u) << 4));
     const uint32_t t3 = lds_u32(lds, S4base + 12288u + ((x >> 24) << 4));
     return xor3(xor3(t0, t1, t2), t3, w);
+  };
+
+  // paired placement: lanes 0-31 shift by 512 bytes, lanes 32-63 by -512
+  const uint32_t PHbase = kFastLdsBytes + ((lane >> 5) << 12);
+  auto pshift = [&](uint32_t y) -> uint32_t {
+    const uint32_t t0 = lds_u32(lds, PHbase + ((y & 255u) << 2));
+    const uint32_t t1 = lds_u32(lds, PHbase + 1024u + (((y >> 8) & 255u) << 2));
+    const uint32_t t2 = lds_u32(lds, PHbase + 2048u + (((y >> 16) & 255u) << 2));
+    const uint32_t t3 = lds_u32(lds, PHbase + 3072u + ((y >> 24) << 2));
+    return xor3(t0, t1, t2) ^ t3;
   };
 
   const uint32_t wave = uni(tid >> 6);
@@ -447,6 +470,24 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
   if (lane == 0) k3v = atomicAdd(&s_next, 1u);
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, stored = 0;
   uint64_t reported = ~0ull;  // wave-uniform: lowest block this wave has put into first_bad
+  // a block's outputs: CRC word, stamp, verify bitmap / first_bad
+  auto emit = [&](uint64_t b, const uint8_t *p, uint32_t st, uint32_t crc) {
+    if (crc_out) lane0_store_u32(crc_out + b, crc);
+    if (flags & kFlagStamp) lane0_store_u32(const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(p)), crc);
+    const bool bad = st != crc;
+    if (first_bad && bad) {
+      if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
+      // blocks arrive in increasing order: one atomic per wave (a batch of
+      // all-bad blocks would otherwise serialise every wave on one word)
+      if (b < reported) lane0_atomic_umin64(first_bad, b);
+      reported = b < reported ? b : reported;
+    }
+  };
+  // the finalised block waiting for a partner (its lane-combined streams)
+  bool pend = false;
+  uint32_t pd = 0, pst = 0;
+  uint64_t pi = 0;
+  const uint8_t *pp = nullptr;
   for (;;) {
     const bool last = g + 1 == gc;
     // refills: this block's next group, or the next block's first group (a
@@ -513,23 +554,40 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
     if (last) {  // block cur is complete
       if (!cur.skip) {
         const uint32_t d = shift4(shift4(shift4(c0, c1), c2), c3);
-        const uint32_t crc = wave_xor(matvec32(col, d)) ^ 0xFFFFFFFFu;
-        const uint64_t b = cur.i;
-        if (crc_out) lane0_store_u32(crc_out + b, crc);
-        if (flags & kFlagStamp) lane0_store_u32(const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(cur.p)), crc);
-        const bool bad = uni(stored) != crc;
-        if (first_bad && bad) {
-          if (bad_bitmap) lane0_atomic_or(bad_bitmap + (b >> 5), 1u << (b & 31));
-          // blocks arrive in increasing order: one atomic per wave (a batch of
-          // all-bad blocks would otherwise serialise every wave on one word)
-          if (b < reported) lane0_atomic_umin64(first_bad, b);
-          reported = b < reported ? b : reported;
+        if (!pend) {  // wait for a partner
+          pd = d;
+          pst = uni(stored);
+          pi = cur.i;
+          pp = cur.p;
+          pend = true;
+        } else {
+          // two blocks, one placement: A (pending) is folded into lanes 32-63
+          // (d_j ^ shift(d_{j-32}, 512): lane j's placement covers both), B
+          // (this one) into lanes 0-31 (d_l ^ shift(d_{l+32}, -512)); one
+          // 32x32 mat-vec, then the lower and upper halves' XORs
+          const bool lo = lane < 32;
+          const uint32_t z = pshift(lo ? pd : d);
+          const auto sw = __builtin_amdgcn_permlane32_swap(z, z, false, false);
+          const uint32_t x = (lo ? d : pd) ^ (lo ? sw[1] : sw[0]);
+          uint32_t v = matvec32(col, x);
+          v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+          v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+          v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+          v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+          const uint32_t crc_b = __builtin_amdgcn_readlane(v, 0) ^ __builtin_amdgcn_readlane(v, 16) ^ 0xFFFFFFFFu;
+          const uint32_t crc_a = __builtin_amdgcn_readlane(v, 32) ^ __builtin_amdgcn_readlane(v, 48) ^ 0xFFFFFFFFu;
+          emit(pi, pp, pst, crc_a);
+          emit(cur.i, cur.p, uni(stored), crc_b);
+          pend = false;
         }
       } else if (kArrays && skip_slot && skip_tag) {  // left to the k_crc_any sweep: tell it once per wave
         lane0_atomic_umax64(skip_slot, skip_tag);
         skip_tag = 0;
       }
-      if (!nxt.valid) return;
+      if (!nxt.valid) {
+        if (pend) emit(pi, pp, pst, wave_xor(matvec32(col, pd)) ^ 0xFFFFFFFFu);  // no partner left
+        return;
+      }
       cur = nxt;
       g = 0;
       gc = cur.skip ? 1u : cur.groups;
@@ -605,7 +663,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_range(const void *p, uint3
 // over one static run per wave, profiles/r2/any/).  kSmallLanes (whole-message
 // batches): records of <= 1020 bytes are hashed one per lane (below).  The
 // measured alternatives (static runs, other batch sizes, issue orders, the
-// timing-only build) are in tools/ab_hc_kernels.hip.
+// timing-only build) are in git history (tools/ab_hc_kernels.hip, up to 61a2e0e).
 constexpr int kAnyBatch = 4;
 template <bool kSmallLanes>
 __global__ __launch_bounds__(kFastThreads) void k_crc_any(
@@ -613,13 +671,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
-    const unsigned long long *seg_slot = nullptr, uint64_t seg_tag = 0, const unsigned long long *skip_slot = nullptr,
+    const uint32_t *__restrict__ seg_flag = nullptr, const unsigned long long *skip_slot = nullptr,
     uint64_t skip_tag = 0) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
   __shared__ uint32_t s_next;
-  // after a packed-record stream (k_seg_*): it took the batch unless it raised
-  // the slot to this call's tag
-  if (seg_slot && __hip_atomic_load(seg_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seg_tag) return;
+  if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
   // the sweep after k_crc_grp: no block was left to it (Batch::skip_slot)
   if (fast_mask && skip_slot &&
       __hip_atomic_load(skip_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < skip_tag)
@@ -1498,10 +1554,10 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 // from the span's raw CRCs at a and b relative to any common origin; the stream
 // only has to leave them at the record boundaries ("events"), relative to the
 // 16 KiB unit holding each event.
+//   k_seg_plan     events -> first event of every 16 KiB unit; checks that the
+//                  batch is packed and no record exceeds kSegMaxRecord (else a
+//                  flag, stored by k_seg_stream, sends it to k_crc_grp + k_crc_any)
 //   k_seg_stream   k_crc_grp's rows, groups and hand-out over the span's units;
-//                  each unit's first event by a 64-ary search it runs itself,
-//                  and the packing check on its event windows (below; round 3
-//                  ran both in a separate k_seg_plan launch, 17 us at 2M records);
 //                  per unit its raw CRC, and at every row holding events
 //                  H(x) = shift(raw(unit .. x), re - x) (re = the row's end):
 //                  the row start's value from the Horner streams, the row's
@@ -1513,6 +1569,7 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 //                  shift by re_b - b (SegTables: 6 table multiplies a record).
 constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups (the kernels take it as kU)
 constexpr uint32_t kSegMaxRecord = 1u << 24;  // longest record the stream takes (16 MiB)
+constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's grid cap: one "bad" slot per workgroup
 
 struct SegGeo {
   uint64_t a0, pend, units;
@@ -1528,102 +1585,64 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 }
 
 // Events: position j = base + off[j] (j < n) and the span's end (j = n).
-//
-// k_seg_stream finds the first event of each unit it takes itself (no plan
-// kernel, no first-event table): the first event at or after the unit's start
-// T by a 64-ary search over a FIXED implicit tree on [0, n].  Level k splits
-// the bracket [b, b + 64 s) (s = 64^(L-k)) at the samples b + (l+1) s - 1, one
-// per lane; the ballot of pos(sample) < T counts the pieces wholly before T.
-// Every wave searches the same tree, so the upper levels' samples are shared
-// L2 lines, and the last level's 64 neighbouring entries are the ones the
-// unit's first event window loads next.  The top level's 64 samples are read
-// once into registers; each further level is one 64-lane load, issued one
-// group ahead: the search for the wave's next unit starts when the hand-out
-// gives it (the previous unit's end) and has four loaded levels by the top of
-// the current unit's last group, where its result starts the next window (n up
-// to 64^5 - 1 events without a synchronous level).
-//
-// The packing check is done on the event windows the stream loads anyway
-// (off and len of the group's events): the batch is packed when every event j
-// < n-1 has pos(j+1) = pos(j) + len(j), no record is over kSegMaxRecord and no
-// 4 KiB group holds 64 or more events (records under ~64 B).  Every event lies
-// in a group of the span, so every adjacent pair is seen by one window (a pair
-// split by a window's end would need 64 events in one group).  A wave that finds
-// the batch is not packed raises the per-device word *bad_slot to the call's
-// tag (tags increase per call) and stops; the others poll it once per group
-// and stop too.  The span's geometry (units over max_units, n, an end before
-// the start) is checked by every workgroup before the table fill.  With the
-// slot at the tag k_seg_combine writes nothing and k_crc_any hashes every
-// record; below it k_crc_any exits at once.  Memory stays in bounds without
-// packing: rows through buffer ranges clipped to the span, off/len indices
-// clamped to [0, n), ev_h indices <= n, unit_raw indices < units.
-typedef unsigned int seg_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ seg_u32x2 gload8(const uint64_t *p) {  // (a global load, as gload16)
-  return *reinterpret_cast<const __attribute__((address_space(1))) seg_u32x2 *>(reinterpret_cast<uintptr_t>(p));
+// first_ev[u] = first event in unit u (u = 0 .. units; first_ev[units] = n + 1).
+// Workgroup w writes plan_bad[w] = 1 when its events find the batch not packed,
+// over max_units, with a record over kSegMaxRecord, or with more than 64 events
+// in one 4 KiB group (records under ~64 B: k_crc_any), else 0.  Every slot is
+// written, so the dispatch needs no memset: k_seg_stream's workgroups OR the
+// slots and its workgroup 0 stores the flag the later kernels read.
+template <uint32_t kU = kSegUnitLg>
+__global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                  const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
+                                                  uint32_t *__restrict__ plan_bad, uint32_t *__restrict__ first_ev) {
+  const SegGeo g = seg_geo<kU>(base, offs, lens, n);
+  bool bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= n && !bad; j += step) {
+    const uint64_t pj = j < n ? (uint64_t)base + offs[j] : g.pend;
+    uint64_t ulo = 0;
+    if (j > 0) {
+      const uint64_t pp = (uint64_t)base + offs[j - 1];
+      if ((j < n && offs[j] != offs[j - 1] + lens[j - 1]) || pj < pp) bad = true;
+      if (lens[j - 1] > kSegMaxRecord) bad = true;  // k_seg_combine's unit chain stays <= 1025 units
+      ulo = ((pp - g.a0) >> kU) + 1;
+    }
+    if (j >= 64 && ((pj - g.a0) >> 12) == (((uint64_t)base + offs[j - 64] - g.a0) >> 12)) bad = true;
+    const uint64_t uj = (pj - g.a0) >> kU;
+    if (uj >= g.units || pj < g.a0) bad = true;
+    if (bad) break;
+    for (uint64_t u = ulo; u <= uj; u++) first_ev[u] = (uint32_t)j;
+    if (j == n)
+      for (uint64_t u = uj + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(n + 1);
+  }
+  const int any_bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) plan_bad[blockIdx.x] = any_bad ? 1u : 0u;  // every slot written: no memset
 }
 
+// (its timing-only builds -- rows XOR-folded, or no event work at all -- are in
+// git history: tools/ab_hc_kernels.hip, up to commit 61a2e0e)
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint32_t lg_chunk, uint64_t max_units,
-                                                            unsigned long long *__restrict__ bad_slot, uint64_t tag,
+                                                            uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
+                                                            uint32_t plan_wgs, uint32_t *__restrict__ flag,
+                                                            const uint32_t *__restrict__ first_ev,
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
                                                             const DeviceTables *__restrict__ tables) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
   __shared__ uint32_t s_next;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
-  const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
-  const uint64_t M = geo.units;
-  if (n >= 0x7FFFFFFFull || geo.pend < geo.a0 || M > max_units) {  // the same in every workgroup
-    if (blockIdx.x == 0 && tid < 64) lane0_atomic_umax64(bad_slot, tag);
-    return;
-  }
-  typedef seg_u32x2 u32x2;
-  const uint64_t pend = geo.pend;
-  auto pos_at = [&](uint64_t j, u32x2 v) -> uint64_t {
-    return j < n ? (uint64_t)base + (((uint64_t)v.y << 32) | v.x) : pend;
-  };
-  auto off_load = [&](uint64_t j) -> u32x2 { return gload8(offs + (j < n ? j : n - 1)); };
-  // the fixed tree: top level pieces of 2^top_sh = 64^(L-1) events, 64^L >= n + 1
-  int32_t top_sh = 0;
-  while ((64ull << top_sh) < n + 1) top_sh += 6;
-  const uint64_t top_ix = ((uint64_t)(lane + 1) << top_sh) - 1;
-  const u32x2 top_v = off_load(top_ix);  // (completes during the table fill)
   fill_crc_tables(lds, tables, tid, kFastThreads);
   if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  __syncthreads();
-  const uint64_t top_pos = pos_at(top_ix, top_v);
-
-  // a search: bracket [b, b + 64 * 2^sh) holds the first event at or after T;
-  // sh < 0: resolved, the event is b (n < 2^31)
-  struct Srch {
-    uint64_t T;
-    uint32_t b;
-    int32_t sh;
-  };
-  auto s_start = [&](uint64_t T) -> Srch {  // the top level, from registers
-    const uint32_t c = (uint32_t)__popcll(__ballot(top_pos < T));
-    Srch s;
-    s.T = T;
-    s.b = (c < 63 ? c : 63u) << top_sh;
-    s.sh = top_sh - 6;
-    return s;
-  };
-  // this lane's sample of the next level (n when resolved: a harmless load)
-  auto s_ix = [&](const Srch &s) -> uint64_t {
-    return s.sh >= 0 ? (uint64_t)s.b + ((uint64_t)(lane + 1) << s.sh) - 1 : n;
-  };
-  auto s_step = [&](Srch &s, u32x2 v) {  // v = offs at s_ix(s)
-    if (s.sh < 0) return;
-    const uint32_t c = (uint32_t)__popcll(__ballot(pos_at(s_ix(s), v) < s.T));  // < 64 for a packed batch
-    s.b += (c < 63 ? c : 63u) << s.sh;
-    s.sh -= 6;
-  };
-  auto unit_T = [&](uint64_t u) -> uint64_t { return geo.a0 + (u << kU); };
+  uint32_t bad = 0;
+  for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) bad |= plan_bad[i];
+  if (__syncthreads_or((int)bad)) bad = 1;
+  if (blockIdx.x == 0 && tid == 0) *flag = bad;  // read by k_seg_combine and the fallback kernels
+  if (bad) return;                                // not a packed batch: k_crc_any takes it
 
   const uint32_t r4 = (lane & 31u) << 2;
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
@@ -1654,7 +1673,9 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   auto slot_st = [&](uint32_t l, uint32_t v) {
     __hip_atomic_store(&lds[slot + l], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   };
-  const uint64_t rhi = (pend + 15) & ~15ull;  // loads past the span's last chunk return zeros
+  const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
+  const uint64_t M = geo.units;
+  const uint64_t rhi = (geo.pend + 15) & ~15ull;  // loads past the span's last chunk return zeros
   const uint64_t G = gridDim.x;
   // chunks of 2^lg_chunk units (128 = 2 MiB best, profiles/r2/seg/), fewer
   // for short spans: every workgroup gets at least 4 chunks
@@ -1670,48 +1691,29 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     const uint64_t avail = u < M && rhi > U ? rhi - U : 0;
     return buf_range(reinterpret_cast<const void *>(U), (uint32_t)(avail < (1u << kU) ? avail : (1u << kU)));
   };
-  // window: the positions and lengths of events f .. f+63, one per lane, and
-  // (every lane) the position of event f+64, for the 65-events-a-group check
-  struct Win {
-    u32x2 o, o64;
-    uint32_t l;
-  };
-  auto win_issue = [&](uint64_t f) -> Win {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  // window: the positions of events f .. f+63, one per lane (a group holds at most 64)
+  auto win_issue = [&](uint64_t f) -> u32x2 {
     const uint64_t fc = f < n ? f : n;
     const uint64_t cnt = n - fc;
-    const __amdgpu_buffer_rsrc_t ro = buf_range(offs + fc, (uint32_t)(cnt < 65 ? cnt * 8 : 520));
-    const __amdgpu_buffer_rsrc_t rl = buf_range(lens + fc, (uint32_t)(cnt < 64 ? cnt * 4 : 256));
-    Win w;
-    w.o = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(ro, lane * 8u, 0, 0));
-    w.o64 = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(ro, 512u, 0, 0));
-    w.l = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lane * 4u, 0, 0);
-    return w;
+    const __amdgpu_buffer_rsrc_t r = buf_range(offs + fc, (uint32_t)(cnt < 64 ? cnt * 8 : 512));
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, 0, 0));
   };
   auto win_pos = [&](u32x2 v, uint64_t f) -> uint64_t {
     const uint64_t j = f + lane;
-    return j < n ? (uint64_t)base + (((uint64_t)v.y << 32) | v.x) : j == n ? pend : ~0ull;
+    return j < n ? (uint64_t)base + (((uint64_t)v.y << 32) | v.x) : j == n ? geo.pend : ~0ull;
   };
-  auto raise_bad = [&]() { lane0_atomic_umax64(bad_slot, tag); };
 
   uint64_t u = unit_of(wave);
   if (u >= M) return;
   uint64_t un = unit_of(kFastWaves + wave);
   uint32_t kv = 0;  // VGPR: the LDS hand-out result, read one unit later
   if (lane == 0) kv = atomicAdd(&s_next, 1u);
-  uint64_t wfirst;
-  {  // the first unit's first event: a synchronous search (the prologue's only one)
-    Srch s = s_start(unit_T(u));
-    while (s.sh >= 0) s_step(s, off_load(s_ix(s)));
-    wfirst = s.b;
-  }
-  // the next unit's search (X): started here, one level per group top
-  Srch X = s_start(unit_T(un < M ? un : 0));
-  u32x2 xv = off_load(s_ix(X));
-  Win wraw = win_issue(wfirst);
+  uint64_t wfirst = first_ev[u];
+  u32x2 wraw = win_issue(wfirst);
   __amdgpu_buffer_rsrc_t rc = unit_rsrc(u);
   uint4 q0 = buf_load16(rc, lane * 16u), q1 = buf_load16(rc, 1024u + lane * 16u),
         q2 = buf_load16(rc, 2048u + lane * 16u), q3 = buf_load16(rc, 3072u + lane * 16u);
-  uint64_t polled = 0;  // *bad_slot as read one group earlier
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, g = 0;
 
   // H at the events of the row starting at rs (uniform mask evm of window
@@ -1786,32 +1788,11 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
 
   for (;;) {
     const uint64_t gs = geo.a0 + (u << kU) + ((uint64_t)g << 12);
-    const uint64_t wpos = win_pos(wraw.o, wfirst);
-    const uint32_t wlen = wfirst + lane < n ? wraw.l : 0u;
+    const uint64_t wpos = win_pos(wraw, wfirst);
     const bool lastg = g == (1u << (kU - 12)) - 1u;  // the unit's last 4 KiB group
-    // packing, on this group's window: pos(j+1) = pos(j) + len(j), records up to
-    // kSegMaxRecord, at most 64 events in the group
-    {
-      const uint64_t pnext = __shfl_down((unsigned long long)wpos, 1);
-      const uint64_t j = wfirst + lane;
-      const bool bad = (lane < 63 && j + 1 < n && pnext != wpos + wlen) || wlen > kSegMaxRecord;
-      const uint64_t j64 = wfirst + 64;
-      const uint64_t p64 = j64 < n ? (uint64_t)base + (((uint64_t)wraw.o64.y << 32) | wraw.o64.x)
-                                   : j64 == n ? pend : ~0ull;
-      const bool crowded = __ballot(wpos < gs + 4096u) == ~0ull && p64 < gs + 4096u;
-      if (__ballot(bad) != 0 || crowded || uni((uint32_t)(polled >= tag))) {
-        if (!uni((uint32_t)(polled >= tag))) raise_bad();
-        return;
-      }
-    }
-    // the next unit's search: one level (the load issued one group ago)
-    s_step(X, xv);
-    if (lastg)
-      while (X.sh >= 0) s_step(X, off_load(s_ix(X)));  // (more than 64^5 events only)
-    xv = off_load(s_ix(X));
-    polled = __hip_atomic_load(bad_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the next group: this unit's, or unit un's first; its events' window
-    const uint64_t nf = lastg ? (un < M ? X.b : n + 1) : wfirst + (uint64_t)__popcll(__ballot(wpos < gs + 4096u));
+    const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M]
+                              : wfirst + (uint64_t)__popcll(__ballot(wpos < gs + 4096u));
     const __amdgpu_buffer_rsrc_t rn = lastg ? unit_rsrc(un) : rc;
     const uint32_t no = lastg ? lane * 16u : ((g + 1) << 12) + lane * 16u;
     // each refill pinned right after its row's fold (as k_crc_grp's kPin):
@@ -1832,8 +1813,6 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
       c0 = c1 = c2 = c3 = 0;
       un = unit_of(uni(kv));
       if (lane == 0) kv = atomicAdd(&s_next, 1u);
-      X = s_start(unit_T(un < M ? un : 0));  // the new next unit's search
-      xv = off_load(s_ix(X));
     } else {
       g++;
     }
@@ -1853,7 +1832,7 @@ __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) 
 // chains the raw CRCs of the units it crosses (Horner, 16 rows per step) and
 // shifts the result from U_b to re_b (1 .. 16 rows); no prefix over the whole
 // span is needed (round 2 computed one with three scan kernels, 54 us at 2M
-// records).  k_seg_stream caps records at kSegMaxRecord (1024 units).  Then one
+// records).  k_seg_plan caps records at kSegMaxRecord (1024 units).  Then one
 // inverse shift by re_b - b in [1, 1024] bytes, by the octal digits of
 // re_b - b - 1.  Every row shift is ONE table multiply (SegTables::rs) and the
 // inverse shift four (SegTables::iv): 6 multiplies a record where the binary
@@ -1866,7 +1845,7 @@ __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) 
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ lens, uint64_t n,
-                                                      const unsigned long long *__restrict__ bad_slot, uint64_t tag,
+                                                      const uint32_t *__restrict__ flag,
                                                       const uint32_t *__restrict__ unit_raw,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken) {
@@ -1889,11 +1868,9 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
       if (i < kQ) reinterpret_cast<uint4 *>(tl)[i] = t[k];
     }
   }
-  // the stream did not take the batch when the slot reached this call's tag
-  const bool bad = __hip_atomic_load(bad_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tag;
-  if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = bad ? 0u : 1u;  // (hc_debug_seg_taken)
+  if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
   __syncthreads();
-  if (bad) return;
+  if (*flag) return;
   const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni(threadIdx.x >> 6);
@@ -1962,12 +1939,12 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
   if (!b.base) return hipErrorInvalidValue;
   if (b.flags & kFlagMessages)
     hipLaunchKernelGGL(k_crc_any<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_slot,
-                       b.seg_tag, b.skip_slot, b.skip_tag);
+                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
+                       b.skip_slot, b.skip_tag);
   else
     hipLaunchKernelGGL(k_crc_any<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_slot,
-                       b.seg_tag, b.skip_slot, b.skip_tag);
+                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
+                       b.skip_slot, b.skip_tag);
   return hipGetLastError();
 }
 
@@ -2057,19 +2034,25 @@ hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, 
 
 uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
 
-uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) { return 4 * (max_units + n + 1); }
+uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
+  return 4 * (64 + kSegPlanMaxWgs + (max_units + 1) + max_units + n + 1);
+}
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
                       uint32_t *taken, uint32_t lg_chunk) {
-  if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages) ||
-      !b.seg_slot || !b.seg_tag)
+  if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
     return hipErrorInvalidValue;
   const uint64_t n = b.nblocks;
-  uint32_t *unit_raw = ws, *ev_h = unit_raw + max_units;
-  hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
-                     max_units, b.seg_slot, b.seg_tag, unit_raw, ev_h, b.tables);
-  hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n,
-                     (const unsigned long long *)b.seg_slot, b.seg_tag, unit_raw, ev_h, b.crc_out, st, taken);
+  uint32_t *flag = ws, *plan_bad = ws + 64, *first_ev = plan_bad + kSegPlanMaxWgs, *unit_raw = first_ev + max_units + 1,
+           *ev_h = unit_raw + max_units;
+  const uint64_t pg = (n + 256) / 256;
+  const uint32_t plan_wgs = (uint32_t)(pg < kSegPlanMaxWgs ? pg : kSegPlanMaxWgs);
+  hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
+                     first_ev);
+  hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
+                     plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
+  hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
+                     b.crc_out, st, taken);
   return hipGetLastError();
 }
 

@@ -26,13 +26,9 @@ struct Batch {
   uint32_t *bad_bitmap;           // optional (verify)
   unsigned long long *first_bad;  // optional (verify), INT64_MAX when clean
   const DeviceTables *tables;
-  // packed-record stream (launch_seg): the stream raises *seg_slot to seg_tag
-  // (atomic max) when it does not take the batch; k_crc_any launched after it
-  // with the same pair does nothing while *seg_slot < seg_tag.  Tags increase
-  // per call (as skip_tag below), so a slot shared by concurrent calls can only
-  // make a fallback run without need, never skip one.
-  unsigned long long *seg_slot;
-  uint64_t seg_tag;
+  // optional: the flag of a packed-record stream launched before (launch_seg);
+  // k_crc_any does nothing when it is 0 (the stream took the batch)
+  const uint32_t *seg_flag;
   // optional (off/len batches): k_crc_grp raises *skip_slot to at least
   // skip_tag (atomic max) when it leaves a block to k_crc_any, and the k_crc_any
   // sweep after it exits at once while *skip_slot < skip_tag.  Tags increase
@@ -109,12 +105,11 @@ hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s);
 hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 // Packed whole-message batches (off[i+1] = off[i] + len[i], HC_F_MESSAGES) as
-// one stream over their span (k_seg_stream + k_seg_combine, hc_kernels.hip).
-// max_units bounds the span's 16 KiB units (seg_max_units of a byte bound on
-// the span); ws holds seg_workspace_bytes(n, max_units) bytes.  A batch that is
-// not packed, is larger than the bound, holds records under ~64 B or over 16
-// MiB raises *b.seg_slot to b.seg_tag on the device and writes nothing
-// (k_crc_any with the same slot and tag then takes it).
+// one stream over their span (k_seg_*, hc_kernels.hip).  max_units bounds the
+// span's 16 KiB units (seg_max_units of a byte bound on the span); ws holds
+// seg_workspace_bytes(n, max_units) bytes.  A batch that is not packed, is
+// larger than the bound, holds records under ~64 B or over 16 MiB raises ws[0]
+// on the device and writes nothing (k_crc_any with seg_flag = ws then takes it).
 uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
 // taken (optional, device word): 1 when the stream took the batch, else 0.

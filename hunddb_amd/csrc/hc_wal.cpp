@@ -197,7 +197,7 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
   std::vector<Range> R(T);
   int last_range = T - 1;  // ranges after a stop are not used
   double t0 = now_s(), tv = 0, ta = 0, tb = 0, tc = 0;
-  parallel_for(2, [&](int role) {
+  auto work = [&](int role) {
     if (role == 0) {
       bool on_gpu = false;
       if (n >= gpu_min || force_gpu()) {
@@ -327,7 +327,15 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
       _mm_sfence();  // the streamed stores are visible before the call returns
     });
     tc = now_s() - t0;
-  });
+  };
+  // verify and parse side by side; a replay of a few blocks runs both on the
+  // calling thread (handing a task to a pool thread costs more than it saves)
+  if (n >= 256) {
+    parallel_for(2, work);
+  } else {
+    work(0);
+    work(1);
+  }
   if (trace)
     std::fprintf(stderr, "[hc_wal_replay] %llu blocks, %d ranges: verify %.3f s, scan+merge %.3f s, "
                  "resolve %.3f s, copy-out %.3f s (from the call start)\n",

@@ -117,22 +117,44 @@ func FixLastBlockCRC(data []byte) error {
 
 // ---- batched entries (new; the GPU hot path) ------------------------------
 
-// CheckBlocksIntegrity verifies every blockSize-byte block of data in one GPU
-// batch (the per-block loop of BlockManager.ReadFromDisk,
-// block_manager.go:203-235, and WAL recovery, wal.go:366-403).  It returns
-// the index of the first failing block (-1 if none) and that block's error.
+// gpuBatchMinBlocks is where one GPU batch beats the per-block host loop for
+// a single caller on pageable (Go) memory: 1024 blocks of 4 KiB
+// (tools/crossover.py; DESIGN.md 5.2).  Below it the batched helpers run the
+// reference's own loop on the host path of the library.
+const gpuBatchMinBlocks = 1024
+
+// CheckBlocksIntegrity verifies every blockSize-byte block of data (the
+// per-block loop of BlockManager.ReadFromDisk, block_manager.go:203-235, and
+// WAL recovery, wal.go:366-403): one GPU batch from gpuBatchMinBlocks blocks,
+// CheckBlockIntegrity per block below.  It returns the index of the first
+// failing block (-1 if none) and that block's error.
 func CheckBlocksIntegrity(data []byte, blockSize int) (int, error) {
 	n := len(data) / blockSize
+	if n < gpuBatchMinBlocks {
+		for i := 0; i < n; i++ {
+			if err := CheckBlockIntegrity(data[i*blockSize : (i+1)*blockSize]); err != nil {
+				return i, err
+			}
+		}
+		return -1, nil
+	}
 	var first C.int64_t = -1
 	rc := C.hc_verify_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize),
 		C.uint64_t(n), nil, &first)
 	return int(first), goErr(rc)
 }
 
-// AddCRCToBlocks stamps every blockSize-byte block of data in one GPU batch
-// (flushBlock over a run of WAL blocks, wal.go:260-271).
+// AddCRCToBlocks stamps every blockSize-byte block of data (flushBlock over a
+// run of WAL blocks, wal.go:260-271): one GPU batch from gpuBatchMinBlocks
+// blocks, AddCRCToBlockData per block below.
 func AddCRCToBlocks(data []byte, blockSize int) error {
 	n := len(data) / blockSize
+	if n < gpuBatchMinBlocks {
+		for i := 0; i < n; i++ {
+			AddCRCToBlockData(data[i*blockSize : (i+1)*blockSize])
+		}
+		return nil
+	}
 	return goErr(C.hc_stamp_blocks(ptr(data), nil, nil, C.uint64_t(blockSize), C.uint32_t(blockSize), C.uint64_t(n)))
 }
 

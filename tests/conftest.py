@@ -13,6 +13,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "default_thresholds: run with the library's own GPU/host crossovers")
 
 
 LAST_PREFIX = "test_gpu_zz_"  # heavy full-size files: collected after every other test
@@ -26,6 +27,21 @@ def pytest_collection_modifyitems(session, config, items):
     if last:
         keep = [it for it in items if not os.path.basename(str(it.fspath)).startswith(LAST_PREFIX)]
         items[:] = keep + last
+
+
+# The GPU tests were written for the round-3 crossover (256 blocks) and keep
+# it, so every size they use still runs the GPU batch; the production
+# thresholds (hc_util.hpp) have a test of their own
+# (test_gpu_parity.py::test_default_thresholds_route).
+GPU_TEST_THRESHOLDS = {"HC_ADD_CRCS_GPU_MIN_BLOCKS": "256", "HC_READ_GPU_MIN_BLOCKS": "256",
+                       "HC_WAL_GPU_MIN_BLOCKS": "256"}
+
+
+@pytest.fixture(autouse=True)
+def _gpu_test_thresholds(request, monkeypatch):
+    if request.node.get_closest_marker("gpu") is not None and not request.node.get_closest_marker("default_thresholds"):
+        for k, v in GPU_TEST_THRESHOLDS.items():
+            monkeypatch.setenv(k, v)
 
 
 @pytest.fixture(scope="session")

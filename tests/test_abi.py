@@ -180,7 +180,9 @@ def test_debug_tables_consistent(hc):
     lane_q = t[4160:4160 + 2048].reshape(8, 64, 4)
     # columns of shift(., 4096 (j+1) bytes), k_unframe's combine of an 8/16 KiB block's 4 KiB groups
     sh4k = t[6208:6208 + 128].reshape(4, 32)
-    assert t.size == 4160 + 2048 + 128
+    # k_crc_grp's paired placement: shift by +512 (lanes 0-31) and -512 (lanes 32-63) bytes
+    sh512 = t[6336:6336 + 2048].reshape(2, 4, 256)
+    assert t.size == 4160 + 2048 + 128 + 2048
     assert (lane_q.transpose(1, 0, 2).reshape(64, 32) == lane).all()
     assert (sh4k[3] == 0).all()
 
@@ -203,6 +205,30 @@ def test_debug_tables_consistent(hc):
 
     def mv(cols, v):
         return int(np.bitwise_xor.reduce(np.where((v >> np.arange(32)) & 1, cols, 0).astype(np.uint32)))
+
+    # the paired placement (k_crc_grp, round 4): two blocks A and B of one wave,
+    # A folded into lanes 32-63 (d_j ^ shift(d_{j-32}, 512)), B into lanes 0-31
+    # (d_l ^ shift(d_{l+32}, -512)), ONE mat-vec per lane, then the XOR of each half
+    def lane_d(blk):
+        w = np.frombuffer(blk, dtype="<u4").reshape(len(blk) // 1024, 64, 4).copy()
+        w[0, 0, 0] = w0
+        c = w[0].copy()
+        for r in range(1, len(blk) // 1024):
+            c = tab(tg, c) ^ w[r]
+        return tab(s4, tab(s4, tab(s4, c[:, 0]) ^ c[:, 1]) ^ c[:, 2]) ^ c[:, 3]
+
+    for B in (4096, 8192, 16384):
+        a_blk = rng.integers(0, 256, B, dtype=np.uint8).tobytes()
+        b_blk = rng.integers(0, 256, B, dtype=np.uint8).tobytes()
+        da, db = lane_d(a_blk), lane_d(b_blk)
+        lo = np.arange(64) < 32
+        y = np.where(lo, da, db)
+        z = np.array([int(tab(sh512[0 if ln < 32 else 1], int(y[ln]))) for ln in range(64)], dtype=np.uint32)
+        zs = np.roll(z, 32)  # v_permlane32_swap: lane l gets lane l +- 32
+        x = np.where(lo, db, da) ^ zs
+        e = np.array([mv(lane[ln], int(x[ln])) for ln in range(64)], dtype=np.uint32)
+        assert int(np.bitwise_xor.reduce(e[:32])) ^ 0xFFFFFFFF == zlib.crc32(b_blk[4:]), B
+        assert int(np.bitwise_xor.reduce(e[32:])) ^ 0xFFFFFFFF == zlib.crc32(a_blk[4:]), B
 
     # k_unframe at 8/16 KiB: each 4 KiB group hashed alone (W0 init in group 0,
     # zero init after), placed, shifted past the groups after it, XORed
@@ -245,6 +271,7 @@ def test_add_crcs_to_data_without_gpu(hc, oracle, monkeypatch):
     mode) the missing device is an error instead."""
     if hc.device_count() > 0:
         pytest.skip("a gfx950 device is present")
+    monkeypatch.setenv("HC_ADD_CRCS_GPU_MIN_BLOCKS", "256")  # 301 blocks: a GPU batch
     rng = np.random.default_rng(300)
     src = rng.integers(0, 256, 4092 * 300 + 77, dtype=np.uint8).tobytes()
     out = hc.AddCRCsToData(src)
@@ -264,6 +291,7 @@ def test_add_crcs_finishes_on_host_after_gpu_failure(hc, oracle, monkeypatch, in
     framed output, byte-exact vs the oracle, and counted in hc_stats; under
     HC_FORCE_GPU the failure is returned instead.  Runs with or without a GPU."""
     rng = np.random.default_rng(301)
+    monkeypatch.setenv("HC_ADD_CRCS_GPU_MIN_BLOCKS", "256")  # 301 blocks: a GPU batch
     src = rng.integers(0, 256, 4092 * 300 + 77, dtype=np.uint8).tobytes()
     want = np.zeros(hc.hc_add_crcs_size_py(len(src)), dtype=np.uint8)
     assert oracle.lib().oc_add_crcs_to_data(src, len(src), want.ctypes.data) == len(want)

@@ -58,7 +58,7 @@ def test_seg_log_uniform_records(cuda, hc, oracle, seg_all, start):
     buf = torch.from_numpy(host).cuda()
     assert int(off[-1] + lens[-1]) <= total
     check(torch, hc, oracle, host, buf, off, lens, True)
-    assert hc.last_launch()["kernel"].startswith("k_seg_stream")
+    assert "k_seg_stream" in hc.last_launch()["kernel"]
 
 
 def test_seg_boundaries_and_shapes(cuda, hc, oracle, seg_all):
@@ -87,9 +87,8 @@ def test_seg_boundaries_and_shapes(cuda, hc, oracle, seg_all):
 
 def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
     """Batches the stream does not take are hashed by k_crc_any (the device
-    slot raised to the call's tag): a gap, an overlap, unsorted records, and 65
-    events in one 4 KiB group (records under 64 B) -- found on the stream's own
-    event windows since round 4 (no k_seg_plan)."""
+    flag): a gap, an overlap, unsorted records, and 65 events in one 4 KiB
+    group (records under 64 B)."""
     torch = cuda
     rng = np.random.default_rng(11)
     total = 8 << 20
@@ -111,6 +110,16 @@ def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
     check(torch, hc, oracle, host, buf, packed(small, 0), small, False)
     small[:] = 64  # exactly 64 per group: still the stream
     check(torch, hc, oracle, host, buf, packed(small, 0), small, True)
+    # 63 records and the span's end in the last group (64 events, no 65th): the stream
+    edge = np.full(64 * 10 + 63, 64, dtype=np.uint64)
+    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, True)
+    # 64 records fill the last group exactly; the span's end opens the next one: the stream
+    edge = np.full(64 * 10 + 64, 64, dtype=np.uint64)
+    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, True)
+    # 63 records of 64 B and one of 60 B (64 events), then the span's end in the same group
+    # (the 65th event): the fallback
+    edge = np.r_[np.full(64 * 10 + 63, 64), [60]].astype(np.uint64)
+    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, False)
 
 
 def test_seg_record_cap(cuda, hc, oracle, seg_all):
@@ -218,7 +227,7 @@ def test_seg_workspace_streams(cuda, hc, oracle, seg_all):
             dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
             out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
             hc.dev_crc32_blocks(buf, out, nblocks=n, off=doff, lens=dlen, flags=hc.HC_F_MESSAGES, stream=s)
-        assert hc.last_launch()["kernel"].startswith("k_seg_stream")
+        assert "k_seg_stream" in hc.last_launch()["kernel"]
         jobs.append((host, off, lens, out, buf, doff, dlen))
     torch.cuda.synchronize()
     for host, off, lens, out, *_ in jobs:
