@@ -178,7 +178,7 @@ int hc_dev_multi_crc32_blocks(const hc_dev_shard *shards, int nshards, uint32_t 
  * (row f1): `blocks` holds the blocks from index start_offset/block_size on, as
  * the caller read them (`avail` bytes; past that a block reads as zeros, like
  * readBlockFromDisk's short read).  Every block the loop touches is verified in
- * ONE batch (GPU above HC_READ_GPU_MIN_BLOCKS = 256, host CPU below), the
+ * ONE batch (GPU from HC_READ_GPU_MIN_BLOCKS = 1024, host CPU below), the
  * payload bytes [blockOffset:] of each are copied to out (size bytes; with the
  * GPU batch the copy runs on HC_COPY_THREADS threads while the batch verifies),
  * and *final_offset = SizeAfterAddingCRCs(SizeWithoutCRCs(start_offset) + size).
@@ -205,7 +205,8 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
 /* WAL recovery (lsm/wal/wal.go:362-455 recoverMemtable + processBlockForRecovery,
  * row f3) over nblocks written WAL blocks of block_size bytes (every log's
  * written blocks back to back), starting at (start_block, start_offset).
- * All blocks are verified in ONE batch (GPU from 256 blocks), then parsed:
+ * All blocks are verified in ONE batch (GPU from HC_WAL_GPU_MIN_BLOCKS = 1024
+ * blocks), then parsed:
  * FULL payloads and reassembled FIRST/MIDDLE/LAST fragments are the records
  * (the bytes record.Deserialize receives), copied back to back into rec_buf
  * with rec_off/rec_len.  One call = one memtable: max_records plays
