@@ -2046,7 +2046,9 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   uint32_t *flag = ws, *plan_bad = ws + 64, *first_ev = plan_bad + kSegPlanMaxWgs, *unit_raw = first_ev + max_units + 1,
            *ev_h = unit_raw + max_units;
   const uint64_t pg = (n + 256) / 256;
-  const uint32_t plan_wgs = (uint32_t)(pg < kSegPlanMaxWgs ? pg : kSegPlanMaxWgs);
+  // HC_SEG_PLAN_WGS caps the plan's grid below kSegPlanMaxWgs (tuning sweeps)
+  static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanMaxWgs)));
+  const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
                      first_ev);
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
