@@ -1569,7 +1569,8 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 //                  shift by re_b - b (SegTables: 6 table multiplies a record).
 constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups (the kernels take it as kU)
 constexpr uint32_t kSegMaxRecord = 1u << 24;  // longest record the stream takes (16 MiB)
-constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's grid cap: one "bad" slot per workgroup
+constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's largest grid: one "bad" slot per workgroup
+constexpr uint32_t kSegPlanWgs = 2048;       // its default grid cap (grid-stride beyond; r4e: 13.5 vs 16.8 us at 2M events)
 
 struct SegGeo {
   uint64_t a0, pend, units;
@@ -2046,8 +2047,8 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   uint32_t *flag = ws, *plan_bad = ws + 64, *first_ev = plan_bad + kSegPlanMaxWgs, *unit_raw = first_ev + max_units + 1,
            *ev_h = unit_raw + max_units;
   const uint64_t pg = (n + 256) / 256;
-  // HC_SEG_PLAN_WGS caps the plan's grid below kSegPlanMaxWgs (tuning sweeps)
-  static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanMaxWgs)));
+  // HC_SEG_PLAN_WGS overrides the plan's grid cap, up to kSegPlanMaxWgs (tuning sweeps)
+  static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanWgs)));
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
                      first_ev);

@@ -233,3 +233,37 @@ def test_seg_workspace_streams(cuda, hc, oracle, seg_all):
     for host, off, lens, out, *_ in jobs:
         want = oracle.crc32_messages(host, off, lens.astype(np.uint32), threads=16)
         assert (u32(out) == want).all()
+
+
+@pytest.mark.parametrize("plan_wgs", [1, 3])
+def test_seg_plan_grid_stride(cuda, hc, oracle, plan_wgs):
+    """k_seg_plan grid-strides over the events once they outnumber its grid cap
+    (default 2048 workgroups, 524288 events a stride; config 5b strides 4 times).
+    A child process caps it at 1 or 3 workgroups (HC_SEG_PLAN_WGS, read once per
+    process) so 60k events take 79 or 27 strides: a packed batch is taken and
+    bit-exact, and a gap found in a late stride of one workgroup still sends the
+    batch to k_crc_any."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys; sys.path.insert(0, {root!r}); sys.path.insert(0, {root + '/tests'!r})
+import numpy as np, torch
+from hunddb_amd import crc as hc
+from oracle import oracle as O
+import test_gpu_seg as T
+rng = np.random.default_rng(31)
+n = 60_000
+lens = rng.integers(64, 3000, n).astype(np.uint64)
+off = T.packed(lens, 3)
+host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
+buf = torch.from_numpy(host).cuda()
+T.check(torch, hc, O, host, buf, off, lens, True)
+g = off.copy(); g[n - 700:] += np.uint64(1)  # a gap near the end: the last strides
+T.check(torch, hc, O, host, buf, g, lens, False)
+print("ok")
+"""
+    env = dict(os.environ, HC_SEG_PLAN_WGS=str(plan_wgs), HC_SEG_MIN_MSGS="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
