@@ -650,6 +650,13 @@ __device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t v
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_range(const void *p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
 }
+// Buffer store of one word per lane: lanes whose offset is at or past the
+// range's end store nothing.  A compiler-visible VMEM op issued on every path,
+// so the waitcnt pass counts it exactly (an asm store after a prefetch makes
+// the prefetch's wait also wait for the next one).
+__device__ __forceinline__ void buf_store_u32(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t voff) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+}
 
 // Pipelined per wave over its messages (blocks in block mode): the edge rows
 // of message i+1 (and its stored word) are loaded while message i is
@@ -1715,7 +1722,14 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   __amdgpu_buffer_rsrc_t rc = unit_rsrc(u);
   uint4 q0 = buf_load16(rc, lane * 16u), q1 = buf_load16(rc, 1024u + lane * 16u),
         q2 = buf_load16(rc, 2048u + lane * 16u), q3 = buf_load16(rc, 3072u + lane * 16u);
+  // two empty stores, as the loop issues per group, so the loop's first waits
+  // count the same VMEM ops as its later ones (hipcc takes the fewer)
+  buf_store_u32(buf_range(ev_h, 0), 0u, lane * 4u);
+  buf_store_u32(buf_range(unit_raw, 0), 0u, lane * 4u);
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, g = 0;
+  uint32_t hv = 0;  // lane k: H of the group's event wfirst + k (stored once per group)
+  uint32_t ur_pend = 0, ur_bytes = 0;  // the last unit's raw CRC, stored after the next group
+  uint64_t u_pend = 0;
 
   // H at the events of the row starting at rs (uniform mask evm of window
   // lanes), from the streams c with the row already folded in: H(x) is the
@@ -1737,7 +1751,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
         const int L = (int)(rel >> 4), q = lane == (uint32_t)L ? (int)(rel & 15u) : lane < (uint32_t)L ? 16 : 0;
         const uint32_t h = wave_xor(place(c0 ^ (w.x & ~keep(q, 0)), c1 ^ (w.y & ~keep(q, 1)),
                                           c2 ^ (w.z & ~keep(q, 2)), c3 ^ (w.w & ~keep(q, 3))));
-        lane0_store_u32(ev_h + wfirst + k, h);
+        hv = lane == k ? h : hv;
       }
       return;
     }
@@ -1764,7 +1778,8 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
       const bool has = sv != 0xFFFFFFFFu;
       const int q = has ? (int)(sv >> 8) : 0;
       const uint32_t ep = place(w.x & keep(q, 0), w.y & keep(q, 1), w.z & keep(q, 2), w.w & keep(q, 3));
-      lanes_store_u32(ev_h + wfirst + (sv & 255u), base_h ^ x ^ ep, __ballot(has));
+      const uint32_t hl = __shfl(base_h ^ x ^ ep, (int)L);  // event lane k <- its chunk's lane L
+      hv = (sel >> lane) & 1u ? hl : hv;
       rem &= ~sel;
     }
   };
@@ -1792,8 +1807,8 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     const uint64_t wpos = win_pos(wraw, wfirst);
     const bool lastg = g == (1u << (kU - 12)) - 1u;  // the unit's last 4 KiB group
     // the next group: this unit's, or unit un's first; its events' window
-    const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M]
-                              : wfirst + (uint64_t)__popcll(__ballot(wpos < gs + 4096u));
+    const uint32_t gcnt = (uint32_t)__popcll(__ballot(wpos < gs + 4096u));  // the group's events
+    const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M] : wfirst + gcnt;
     const __amdgpu_buffer_rsrc_t rn = lastg ? unit_rsrc(un) : rc;
     const uint32_t no = lastg ? lane * 16u : ((g + 1) << 12) + lane * 16u;
     // each refill pinned right after its row's fold (as k_crc_grp's kPin):
@@ -1804,10 +1819,21 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     row(q1, gs + 1024u, wpos, rn, no + 1024u);
     row(q2, gs + 2048u, wpos, rn, no + 2048u);
     row(q3, gs + 3072u, wpos, rn, no + 3072u);
+    // the group's event words and the previous unit's raw CRC (if one is
+    // pending): two buffer stores every group, straight-line code (a store
+    // behind a branch makes hipcc's vmcnt waits count the path without it)
+    buf_store_u32(buf_range(ev_h + wfirst, gcnt * 4u), hv, lane * 4u);
+    buf_store_u32(buf_range(unit_raw + u_pend, ur_bytes), ur_pend, lane * 4u);
+    ur_bytes = 0;
     wfirst = nf;
     if (lastg) {
-      lane0_store_u32(unit_raw + u, wave_xor(place(c0, c1, c2, c3)));
-      if (un >= M) return;
+      ur_pend = wave_xor(place(c0, c1, c2, c3));
+      u_pend = u;
+      ur_bytes = 4;
+      if (un >= M) {
+        buf_store_u32(buf_range(unit_raw + u_pend, 4u), ur_pend, lane * 4u);
+        return;
+      }
       u = un;
       rc = rn;
       g = 0;
