@@ -3,9 +3,11 @@ copies hunddb_amd/csrc + Makefile to tools/ab/<name>/, applies exact string
 replacements to one source file and builds tools/ab/<name>/libhundcrc.so
 (tools/ab/ is git-ignored; bench.py loads a variant with HUNDCRC_LIB=...).
 
-  python tools/ab_variant.py <name> <file in csrc> <spec.py>
+  python tools/ab_variant.py <name> <file in csrc> <spec.py> [source file]
 
-spec.py defines SUBS = [(old, new), ...]; every `old` must occur exactly once."""
+spec.py defines SUBS = [(old, new), ...]; every `old` must occur exactly once.
+An optional source file replaces csrc/<file> before the substitutions (a
+variant stacked on an uncommitted one, e.g. a patch applied elsewhere)."""
 import os
 import runpy
 import shutil
@@ -17,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     name, fname, spec = sys.argv[1:4]
+    alt = sys.argv[4] if len(sys.argv) > 4 else None
     dst = os.path.join(ROOT, "tools", "ab", name)
     shutil.rmtree(dst, ignore_errors=True)
     shutil.copytree(os.path.join(ROOT, "hunddb_amd", "csrc"), os.path.join(dst, "csrc"))
@@ -25,6 +28,8 @@ def main():
     os.makedirs(inc, exist_ok=True)
     shutil.copy(os.path.join(ROOT, "include", "hundcrc.h"), inc)
     path = os.path.join(dst, "csrc", fname)
+    if alt:
+        shutil.copy(alt, path)
     src = open(path).read()
     for old, new in runpy.run_path(spec)["SUBS"]:
         k = src.count(old)
