@@ -1783,23 +1783,29 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
       rem &= ~sel;
     }
   };
-  // a row: fold it, issue its register's refill, then its events (from a copy
-  // of the row, so the wave keeps 4 loads in flight through the event work)
+  // a row: fold it, its events, then its register's refill.  (Round 3 issued
+  // the refill before the events, from a copy of the row, to keep 4 loads in
+  // flight through the event work; the copy's 4 v_mov a row cost more than
+  // the wait under sustained launches, where the clock is what the work
+  // leaves: +0.55 points, profiles/r4/r4m/.)  The row as one 128-bit asm
+  // operand where it is folded keeps the loop-carried row in its load's
+  // register tuple: without it small changes elsewhere made hipcc copy the
+  // rows at the loop latch, which waits for the refills.
   auto row = [&](uint4 &q, uint64_t rs, uint64_t wpos, __amdgpu_buffer_rsrc_t rn, uint32_t no) {
-    const uint4 w = q;
+    typedef unsigned int r32x4 __attribute__((ext_vector_type(4)));
+    r32x4 qq = __builtin_bit_cast(r32x4, q);
+    asm volatile("" : "+v"(qq));
+    const uint4 w = __builtin_bit_cast(uint4, qq);
     c0 = row_step(c0, w.x);
     c1 = row_step(c1, w.y);
     c2 = row_step(c2, w.z);
     c3 = row_step(c3, w.w);
     const uint64_t evm = __ballot(wpos >= rs && wpos < rs + 1024u);
-    uint4 we = w;
-    // the folds complete before the refill (else they sink past the event
-    // branch's join and the refill needs a fresh register: see pin below)
-    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(we.x), "+v"(we.y), "+v"(we.z), "+v"(we.w));
+    asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
+    if (evm) events(w, rs, wpos, evm);
     __builtin_amdgcn_sched_barrier(0);
     q = buf_load16(rn, no);
     __builtin_amdgcn_sched_barrier(0);
-    if (evm) events(we, rs, wpos, evm);
   };
 
   for (;;) {
@@ -1811,9 +1817,9 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M] : wfirst + gcnt;
     const __amdgpu_buffer_rsrc_t rn = lastg ? unit_rsrc(un) : rc;
     const uint32_t no = lastg ? lane * 16u : ((g + 1) << 12) + lane * 16u;
-    // each refill pinned right after its row's fold (as k_crc_grp's kPin):
-    // hipcc otherwise hoists it into a fresh register and copies that at the
-    // loop latch, which waits for the load (vmcnt(0))
+    // each refill pinned right after its row's fold and events (sched
+    // barriers, as k_crc_grp's kPin): hipcc otherwise hoists it into a fresh
+    // register and copies that at the loop latch, which waits for the load
     wraw = win_issue(nf);
     row(q0, gs, wpos, rn, no);
     row(q1, gs + 1024u, wpos, rn, no + 1024u);
