@@ -1563,7 +1563,7 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 // 16 KiB unit holding each event.
 //   k_seg_plan     events -> first event of every 16 KiB unit; checks that the
 //                  batch is packed and no record exceeds kSegMaxRecord (else a
-//                  flag, stored by k_seg_stream, sends it to k_crc_grp + k_crc_any)
+//                  flag, stored by k_seg_stream, sends it to k_crc_any)
 //   k_seg_stream   k_crc_grp's rows, groups and hand-out over the span's units;
 //                  per unit its raw CRC, and at every row holding events
 //                  H(x) = shift(raw(unit .. x), re - x) (re = the row's end):
