@@ -184,19 +184,22 @@ namespace {
 
 // ---------------------------------------------------------------------------
 // Device batch dispatch (shared by _dev_ entries and the host pipeline)
-// Whole-message off/len batches of at least HC_SEG_MIN_MSGS messages (default
-// 131072) from a device entry first go to the packed-record stream (k_seg_*,
-// launch_seg): it takes the batch when its messages lie back to back
-// (off[i+1] = off[i] + len[i]) and mostly at least 64 B long, and raises a
-// device flag otherwise, on which k_crc_grp + k_crc_any run as before.  The
-// decision is made on the device (no host sync).  On the null stream the
+// Whole-message off/len batches with crc_out from a device entry (at least
+// HC_SEG_MIN_MSGS messages, default 1: every one) first go to the packed-record
+// stream (k_seg_*, launch_seg): it takes the batch when its messages lie back
+// to back (off[i+1] = off[i] + len[i]) and mostly at least 64 B long, and
+// raises a device flag otherwise, on which k_crc_any runs.  The decision is
+// made on the device (no host sync).  The stream wins at every batch size
+// measured, 16 records up (profiles/r4/r4s/, r4t/: 1.2-8.3x against
+// k_crc_grp + k_crc_any, whose 64-message windows leave most waves idle on
+// small batches); round 3's default was 131072.  On the null stream the
 // workspace is kept across calls (seg_cached_ws: a per-call hipMallocAsync /
 // hipFreeAsync pair cost 4-17 us a call, tools/kseg3.hip); other streams take
 // one from the stream-ordered allocator per call.  The span is bounded by the allocation holding
 // `base` (a batch reaching past it is not packed for the stream).
 uint64_t seg_min_msgs() {
   const char *v = std::getenv("HC_SEG_MIN_MSGS");
-  return v && *v ? std::strtoull(v, nullptr, 10) : (1ull << 17);
+  return v && *v ? std::strtoull(v, nullptr, 10) : 1ull;
 }
 
 // The kept workspace (null stream only), grown to `need` bytes on that stream,

@@ -63,12 +63,12 @@ def test_graph_uniform_blocks_and_verify(cuda, hc, oracle):
 
 @pytest.mark.parametrize("packed", [False, True])
 def test_graph_messages(cuda, hc, oracle, monkeypatch, packed):
-    """Unaligned whole messages (k_crc_any), and packed ones offered to the
-    packed-record stream (HC_SEG_MIN_MSGS=1: the k_seg_* dispatch captured,
-    workspace allocated inside the graph)."""
+    """Whole messages offered to the packed-record stream (the default at any
+    batch size: the k_seg_* dispatch captured, workspace allocated inside the
+    graph): packed ones taken by the stream, ones with gaps by k_crc_any on the
+    device flag."""
     torch = cuda
-    if packed:
-        monkeypatch.setenv("HC_SEG_MIN_MSGS", "1")
+    monkeypatch.delenv("HC_SEG_MIN_MSGS", raising=False)
     rng = np.random.default_rng(2 + packed)
     n = 5000
     lens = rng.integers(64, 9000, n).astype(np.uint64)
@@ -82,7 +82,7 @@ def test_graph_messages(cuda, hc, oracle, monkeypatch, packed):
     dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     g = capture(torch, lambda: hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=n, flags=hc.HC_F_MESSAGES))
-    assert hc.last_launch()["kernel"] == ("k_seg_plan+k_seg_stream+k_seg_combine|k_crc_any" if packed else "k_crc_grp+k_crc_any")
+    assert hc.last_launch()["kernel"] == "k_seg_plan+k_seg_stream+k_seg_combine|k_crc_any"
     for _ in range(3):
         host = rng.integers(0, 256, total, dtype=np.uint8)
         buf.copy_(torch.from_numpy(host))
@@ -90,8 +90,7 @@ def test_graph_messages(cuda, hc, oracle, monkeypatch, packed):
         torch.cuda.synchronize()
         want = oracle.crc32_messages(host, off, lens.astype(np.uint32), threads=8)
         assert np.array_equal(u32(out), want)
-    if packed:
-        assert hc.seg_taken()
+    assert hc.seg_taken() == packed
 
 
 def test_graph_framing_pair(cuda, hc, oracle):

@@ -158,8 +158,9 @@ def test_seg_without_crc_out(cuda, hc, oracle, seg_all):
 
 
 def test_seg_threshold(cuda, hc, oracle, monkeypatch):
-    """Below HC_SEG_MIN_MSGS (default 131072 messages) the batch is not offered
-    to the stream."""
+    """By default every whole-message batch with crc_out is offered to the
+    stream (it beats k_crc_grp + k_crc_any from 16 records up, profiles/r4/r4s,
+    r4t); below HC_SEG_MIN_MSGS the batch is not offered."""
     torch = cuda
     rng = np.random.default_rng(3)
     lens = rng.integers(64, 3000, 5000).astype(np.uint64)
@@ -168,6 +169,11 @@ def test_seg_threshold(cuda, hc, oracle, monkeypatch):
     host = rng.integers(0, 256, total, dtype=np.uint8)
     buf = torch.from_numpy(host).cuda()
     monkeypatch.delenv("HC_SEG_MIN_MSGS", raising=False)
+    check(torch, hc, oracle, host, buf, off, lens, True)
+    assert "k_seg_stream" in hc.last_launch()["kernel"]
+    for n in (1, 2, 17):  # tiny batches at the default
+        check(torch, hc, oracle, host, buf, off[:n], lens[:n], True)
+    monkeypatch.setenv("HC_SEG_MIN_MSGS", "5001")
     check(torch, hc, oracle, host, buf, off, lens, False)
     assert hc.last_launch()["kernel"] == "k_crc_grp+k_crc_any"
 
