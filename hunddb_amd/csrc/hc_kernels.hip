@@ -581,7 +581,12 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
           pend = false;
         }
       } else if (kArrays && skip_slot && skip_tag) {  // left to the k_crc_any sweep: tell it once per wave
-        lane0_atomic_umax64(skip_slot, skip_tag);
+        // a relaxed load first: once one wave has raised the word the others
+        // skip their atomic (a batch whose blocks all go to the sweep put one
+        // same-address atomic per wave on it, serialised at the L2: 45 us at
+        // 4096 blocks, profiles/r4/r4v/)
+        if (__hip_atomic_load(skip_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < skip_tag)
+          lane0_atomic_umax64(skip_slot, skip_tag);
         skip_tag = 0;
       }
       if (!nxt.valid) {
@@ -692,9 +697,15 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
   const uint64_t b1 = nblocks;
   const uint64_t G = gridDim.x, wg = blockIdx.x;
   const uint32_t cmask = (1u << lg_chunk) - 1u;
+  // windows of 64 messages, fewer on small batches so that every wave gets one
+  // (a wave hashes its window's records one after another: 4096 records in
+  // 64-message windows kept 64 of 4096 waves busy, 42-82 us, profiles/r4/r4t/)
+  uint32_t lgw = 6;
+  while (lgw > 0 && (b1 >> lgw) < G * kFastWaves) lgw--;
+  const uint32_t W = 1u << lgw;
   // first message of the workgroup's k-th window (increasing in k)
   auto win_of = [&](uint32_t k) -> uint64_t {
-    return ((((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask)) * 64;
+    return ((((uint64_t)(k >> lg_chunk) * G + wg) << lg_chunk) | (k & cmask)) << lgw;
   };
   if (tid == 0) s_next = kFastWaves;
   // fast_mask != 0 (the sweep after a streaming kernel): look for work before
@@ -707,10 +718,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       const uint64_t g0 = win_of(kk);
       if (g0 >= b1 || any) break;
       const uint64_t j = g0 + lane;
-      const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
-      const uint32_t lj = j < b1 ? (lens ? lens[j] : ulen) : 0;
+      const bool in = lane < W && j < b1;
+      const uint64_t oj = in ? (offs ? offs[j] : j * stride) : 0;
+      const uint32_t lj = in ? (lens ? lens[j] : ulen) : 0;
       const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & fast_mask) == 0 && lj != 0;
-      any = __ballot(j < b1 && !fast) != 0;
+      any = __ballot(in && !fast) != 0;
     }
     if (!__syncthreads_or(any)) return;
   }
@@ -874,8 +886,9 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       uint64_t gv = g;
       asm volatile("" : "+s"(gv));  // window address computed afresh each refill
       const uint64_t j = gv + lane;
-      const uint64_t oj = j < b1 ? (offs ? offs[j] : j * stride) : 0;
-      const uint32_t lj = j < b1 ? (lens ? lens[j] : ulen) : 0;
+      const bool in = lane < W && j < b1;  // the window's messages
+      const uint64_t oj = in ? (offs ? offs[j] : j * stride) : 0;
+      const uint32_t lj = in ? (lens ? lens[j] : ulen) : 0;
       // consume the loads inside the refill branch (their vmcnt(0) stays here)
       wo_lo = (uint32_t)oj;
       wo_hi = (uint32_t)(oj >> 32);
@@ -884,10 +897,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
       // fast_mask != 0: the streaming kernel of this batch took the 16-B aligned
       // blocks whose length is a positive multiple of fast_mask + 1
       const bool fast = (((uintptr_t)base + oj) & 15u) == 0 && (lj & fast_mask) == 0 && lj != 0;
-      todo = __ballot(j < b1 && !(fast_mask && fast));
+      todo = __ballot(in && !(fast_mask && fast));
       if constexpr (kSmallLanes) {
         if (msg) {
-          const uint64_t sm = __ballot(j < b1 && !(fast_mask && fast) && lj <= kSmallMax);
+          const uint64_t sm = __ballot(in && !(fast_mask && fast) && lj <= kSmallMax);
           if (sm) {
             small_lanes(sm, oj, lj, gv);
             todo &= ~sm;
