@@ -1,0 +1,2 @@
+# k_crc_any: windows of at most 2^4 messages on every batch
+SUBS = [("  uint32_t lgw = 6;\n", "  uint32_t lgw = 4;\n")]
