@@ -50,3 +50,17 @@ def test_bench_workload_small(workload):
         assert roof["bytes_per_launch"] == nbytes
     if workload == "verify":
         assert res["config"]["verify_clean"] is True
+
+
+@pytest.mark.gpu
+def test_north_star_meets_its_target():
+    """BASELINE.json's north star: >= 70 % of MI355X HBM peak for device-resident
+    CRC32 over 1M x 8 KiB blocks, at full size (bench.py's HIP-event timing of
+    k_crc_grp; 85-88 % on the boxes of round 4, profiles/r4/)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "northstar", "--steps", "10",
+           "--warmup", "3", "--cpu-seconds", "0", "--pmc", "off"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["config"]["blocks_total"] == 1_000_000 and res["config"]["block_bytes"] == "8192 B"
+    assert res["roofline"]["frac"] >= 0.70, res["roofline"]
