@@ -189,10 +189,12 @@ namespace {
 // stream (k_seg_*, launch_seg): it takes the batch when its messages lie back
 // to back (off[i+1] = off[i] + len[i]) and mostly at least 64 B long, and
 // raises a device flag otherwise, on which k_crc_any runs.  The decision is
-// made on the device (no host sync).  The stream wins at every batch size
-// measured, 16 records up (profiles/r4/r4s/, r4t/: 1.2-8.3x against
-// k_crc_grp + k_crc_any, whose 64-message windows leave most waves idle on
-// small batches); round 3's default was 131072.  On the null stream the
+// made on the device (no host sync).  On config 5's record sizes the stream
+// wins at every batch size measured, 16 records up (profiles/r4/r4x/: 1.5-3.1x
+// against k_crc_grp + k_crc_any); batches of up to ~1024 short records (1 KiB)
+// run faster on k_crc_any (13-27 against 24-28 us: the stream's floor is its
+// four launches), which a caller gets by raising HC_SEG_MIN_MSGS.  Round 3's
+// default was 131072.  On the null stream the
 // workspace is kept across calls (seg_cached_ws: a per-call hipMallocAsync /
 // hipFreeAsync pair cost 4-17 us a call, tools/kseg3.hip); other streams take
 // one from the stream-ordered allocator per call.  The span is bounded by the allocation holding
