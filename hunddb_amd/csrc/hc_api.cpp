@@ -190,7 +190,7 @@ namespace {
 // to back (off[i+1] = off[i] + len[i]) and mostly at least 64 B long, and
 // raises a device flag otherwise, on which k_crc_any runs.  The decision is
 // made on the device (no host sync).  On config 5's record sizes the stream
-// wins at every batch size measured, 16 records up (profiles/r4/r4x/: 1.5-3.1x
+// wins at every batch size measured, 16 records up (profiles/r4/r4x/: 1.5-2.6x
 // against k_crc_grp + k_crc_any); batches of up to ~1024 short records (1 KiB)
 // run faster on k_crc_any (13-27 against 24-28 us: the stream's floor is its
 // four launches), which a caller gets by raising HC_SEG_MIN_MSGS.  Round 3's
