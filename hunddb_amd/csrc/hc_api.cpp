@@ -292,19 +292,14 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
         uint32_t *ws = seg_cached_ws(d, s, need, seg_lock);
         if (!ws && hipMallocAsync(reinterpret_cast<void **>(&seg_ws), need, s) == hipSuccess) ws = seg_ws;
         if (ws) {
+          // word 0 of ws: raised when the stream did not take the batch; then
+          // k_seg_combine runs k_crc_any's work over every message itself
           e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last);
-          b.seg_flag = ws;  // word 0: raised when the stream did not take the batch
           seg = true;
         }
       }
     }
-    if (seg) {
-      // the fallback, for a batch the stream did not take: k_crc_any over every
-      // message (it exits at once when the stream took the batch).  One launch
-      // instead of round 3's k_crc_grp + sweep: a batch of messages that is
-      // not packed is rarely made of aligned 4 KiB multiples.
-      if (e == hipSuccess) e = launch_general(b, 0, gen_grid, s);
-    } else {
+    if (!seg) {
       // k_crc_grp takes the 16-B aligned blocks of 4 KiB multiples (every on-disk
       // size, utils/config/config.go:137); the k_crc_any sweep does the rest
       b.skip_slot = d.skip_slot;
@@ -313,7 +308,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       if (e == hipSuccess) e = launch_general(b, 4095, gen_grid, s);
     }
     if (seg_ws && hipFreeAsync(seg_ws, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;
-    info.kernel = seg ? "k_seg_plan+k_seg_stream+k_seg_combine|k_crc_any" : "k_crc_grp+k_crc_any";
+    info.kernel = seg ? "k_seg_plan+k_seg_stream+k_seg_combine" : "k_crc_grp+k_crc_any";
     t_seg_dev = seg ? dev : -1;
     info.fast_blocks = n;  // routing is decided on the device per block
   }

@@ -677,17 +677,18 @@ __device__ __forceinline__ void buf_store_u32(__amdgpu_buffer_rsrc_t r, uint32_t
 // measured alternatives (static runs, other batch sizes, issue orders, the
 // timing-only build) are in git history (tools/ab_hc_kernels.hip, up to 61a2e0e).
 constexpr int kAnyBatch = 4;
+// The body, a device function: the k_crc_any kernel below, and k_seg_combine
+// for a batch the packed-record stream did not take (the fallback in the same
+// launch).  `lds` holds kFastLdsBytes of tables and one word after them, the
+// workgroup's window counter.
 template <bool kSmallLanes>
-__global__ __launch_bounds__(kFastThreads) void k_crc_any(
-    const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+__device__ __forceinline__ void crc_any_body(
+    uint32_t *lds, const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
-    const uint32_t *__restrict__ seg_flag = nullptr, const unsigned long long *skip_slot = nullptr,
-    uint64_t skip_tag = 0) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4];
-  __shared__ uint32_t s_next;
-  if (seg_flag && *seg_flag == 0) return;  // the packed-record stream (k_seg_*) took the batch
+    const unsigned long long *skip_slot, uint64_t skip_tag) {
+  uint32_t &s_next = lds[kFastLdsBytes / 4];
   // the sweep after k_crc_grp: no block was left to it (Batch::skip_slot)
   if (fast_mask && skip_slot &&
       __hip_atomic_load(skip_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < skip_tag)
@@ -1061,6 +1062,18 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     }
     if (!cur.valid) return;
   }
+}
+
+template <bool kSmallLanes>
+__global__ __launch_bounds__(kFastThreads) void k_crc_any(
+    const uint8_t *base, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+    uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
+    uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
+    unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
+    const unsigned long long *skip_slot = nullptr, uint64_t skip_tag = 0) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 1];
+  crc_any_body<kSmallLanes>(lds, base, offs, lens, stride, ulen, flags, nblocks, fast_mask, lg_chunk, crc_out,
+                            bad_bitmap, first_bad, tables, skip_slot, skip_tag);
 }
 
 // ---------------------------------------------------------------------------
@@ -1894,7 +1907,8 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
                                                       const uint32_t *__restrict__ flag,
                                                       const uint32_t *__restrict__ unit_raw,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
-                                                      const SegTables *__restrict__ st, uint32_t *__restrict__ taken) {
+                                                      const SegTables *__restrict__ st, uint32_t *__restrict__ taken,
+                                                      uint32_t flags, const DeviceTables *__restrict__ tables) {
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
   constexpr uint32_t kUnitRows = 1u << (kU - 10);
   __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024];
@@ -1916,7 +1930,14 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   }
   if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
   __syncthreads();
-  if (*flag) return;
+  if (*flag) {
+    // the stream did not take the batch: k_crc_any's work over every message,
+    // in this launch (round 3 launched k_crc_any after the combine, ~5 us a
+    // call even when it exits at once).  The tables above are not used: the
+    // body fills its own over them, after the barrier.
+    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, 0u, 0u, crc_out, nullptr, nullptr, tables, nullptr, 0);
+    return;
+  }
   const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni(threadIdx.x >> 6);
@@ -1985,12 +2006,12 @@ hipError_t launch_general(const Batch &b, uint32_t fast_mask, int grid, hipStrea
   if (!b.base) return hipErrorInvalidValue;
   if (b.flags & kFlagMessages)
     hipLaunchKernelGGL(k_crc_any<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
-                       b.skip_slot, b.skip_tag);
+                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.skip_slot,
+                       b.skip_tag);
   else
     hipLaunchKernelGGL(k_crc_any<false>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.seg_flag,
-                       b.skip_slot, b.skip_tag);
+                       b.flags, b.nblocks, fast_mask, 0u, b.crc_out, b.bad_bitmap, b.first_bad, b.tables, b.skip_slot,
+                       b.skip_tag);
   return hipGetLastError();
 }
 
@@ -2100,7 +2121,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
                      plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
-                     b.crc_out, st, taken);
+                     b.crc_out, st, taken, b.flags, b.tables);
   return hipGetLastError();
 }
 

@@ -26,9 +26,6 @@ struct Batch {
   uint32_t *bad_bitmap;           // optional (verify)
   unsigned long long *first_bad;  // optional (verify), INT64_MAX when clean
   const DeviceTables *tables;
-  // optional: the flag of a packed-record stream launched before (launch_seg);
-  // k_crc_any does nothing when it is 0 (the stream took the batch)
-  const uint32_t *seg_flag;
   // optional (off/len batches): k_crc_grp raises *skip_slot to at least
   // skip_tag (atomic max) when it leaves a block to k_crc_any, and the k_crc_any
   // sweep after it exits at once while *skip_slot < skip_tag.  Tags increase
@@ -109,7 +106,8 @@ hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 // span's 16 KiB units (seg_max_units of a byte bound on the span); ws holds
 // seg_workspace_bytes(n, max_units) bytes.  A batch that is not packed, is
 // larger than the bound, holds records under ~64 B or over 16 MiB raises ws[0]
-// on the device and writes nothing (k_crc_any with seg_flag = ws then takes it).
+// on the device, and k_seg_combine runs k_crc_any's work over the batch instead
+// (the same launch: the dispatch is three kernels whichever path is taken).
 uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
 // taken (optional, device word): 1 when the stream took the batch, else 0.

@@ -1,8 +1,9 @@
-"""The A/B harnesses tools/kgrp3.hip and tools/kany3.hip build their variants
-from the product kernel source at build time (tools/gen_grp_perm.py,
-tools/gen_any_x.py: textual copies with targeted substitutions; round 3's
-kgrp4 / gen_grp_fin.py, which timed the one-block-at-a-time finalise that
-round 4's paired placement replaced, are in git history), so a variant
+"""The A/B harness tools/kgrp3.hip builds its variant from the product kernel
+source at build time (tools/gen_grp_perm.py: a textual copy with targeted
+substitutions; round 3's kgrp4 / gen_grp_fin.py, which timed the
+one-block-at-a-time finalise that round 4's paired placement replaced, and
+kany3 / gen_any_x.py, whose k_crc_any copy round 4's move of that kernel's
+body into a device function retired, are in git history), so a variant
 always measures the product's current code.  Each generator asserts the text
 it substitutes; this runs each against the current hc_kernels.hip so a product
 change that breaks them fails here, not at the next GPU session."""
@@ -23,10 +24,3 @@ def _gen(script, tmp_path):
 def test_gen_grp_perm_applies(tmp_path):
     k = _gen("gen_grp_perm.py", tmp_path)
     assert "void k_crc_grp_perm(" in k and "perm" in k and "nchunks" in k
-
-
-def test_gen_any_x_applies(tmp_path):
-    k = _gen("gen_any_x.py", tmp_path)
-    assert "void k_crc_any_x(" in k
-    assert "lds[" not in k and "col[32]" not in k  # the tables and per-lane columns are gone
-    assert "xapply(TM" in k and "place_lq(lq, lane" in k

@@ -206,10 +206,7 @@ int main(int argc, char **argv) {
   b.tables = dt;
   auto full = [&](uint32_t *ws, hipStream_t st) {
     hc::Batch bb = b;
-    CK(hc::launch_seg(bb, dst, ws, mu, cus, st, nullptr));
-    bb.seg_flag = ws;
-    CK(hc::launch_grp(bb, cus, st));
-    CK(hc::launch_general(bb, 4095, cus, st));
+    CK(hc::launch_seg(bb, dst, ws, mu, cus, st, nullptr));  // (round 4: the fallback runs inside k_seg_combine)
   };
   std::vector<Variant> vs;
   vs.push_back({"PROD (mallocAsync per call)", [&](hipStream_t st) {
@@ -231,7 +228,7 @@ int main(int argc, char **argv) {
   };
   auto new_combine = [&](hipStream_t st) {
     hipLaunchKernelGGL(hc::k_seg_combine, dim3(cus), dim3(1024), 0, st, b.base, b.off, b.len, n, w_flag, w_raw, w_evh,
-                       crc, dst, nullptr);
+                       crc, dst, nullptr, hc::kFlagMessages, dt);
   };
   vs.push_back({"seg only, r3j combine (22 mul)", [&](hipStream_t st) {
                   hipLaunchKernelGGL(hc::k_seg_plan, dim3(plan_wgs), dim3(256), 0, st, b.base, b.off, b.len, n, mu,
@@ -256,7 +253,7 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(hc::k_seg_stream<KU>, dim3(cus), dim3(hc::kFastThreads), 0, st, b.base, b.off, b.len, n,          \
                        (uint32_t)(LGC), pb_, plan_wgs, f_, fe_, ur_, eh_, dt);                                          \
     hipLaunchKernelGGL(hc::k_seg_combine<KU>, dim3(cus), dim3(1024), 0, st, b.base, b.off, b.len, n, f_, ur_, eh_, crc, \
-                       dst, nullptr);                                                                                  \
+                       dst, nullptr, hc::kFlagMessages, dt);                                                           \
   }
   vs.push_back({"seg only, 8 KiB units, chunk 128", SEGU(13, ws13, mu13, 7), {}});
   vs.push_back({"seg only, 8 KiB units, chunk 256", SEGU(13, ws13, mu13, 8), {}});
