@@ -3,9 +3,9 @@
 // whole dispatch ~82.5 %).  It times, over the same 2M log-uniform records
 // packed at an odd address (bench.py's "records" workload), what hc_api.cpp's
 // dispatch() enqueues per call and parts of it:
-//   PROD      hipMallocAsync(ws) + launch_seg + launch_grp + launch_general + hipFreeAsync
+//   PROD      hipMallocAsync(ws) + launch_seg + hipFreeAsync (round 4: the
+//             fallback for unpacked batches runs inside k_seg_combine)
 //   cached    the same kernels with a workspace allocated once
-//   seg only  launch_seg with the cached workspace (no fallback launches)
 //   r3j       launch_seg's kernels with round 3's first combine (22 multiplies)
 //   combine   the combine kernel alone, production's and r3j's, re-run over
 //             the workspace the previous variant's stream left
@@ -216,12 +216,10 @@ int main(int argc, char **argv) {
                   CK(hipFreeAsync(ws, st));
                 }, {}});
   vs.push_back({"cached workspace", [&](hipStream_t st) { full(ws_cached, st); }, {}});
-  vs.push_back({"seg only (cached)", [&](hipStream_t st) { CK(hc::launch_seg(b, dst, ws_cached, mu, cus, st, nullptr)); },
-                {}});
   // launch_seg's kernels with round 3's first combine (the workspace layout as launch_seg's)
   uint32_t *w_flag = ws_cached, *w_plan = ws_cached + 64, *w_fev = w_plan + hc::kSegPlanMaxWgs,
            *w_raw = w_fev + mu + 1, *w_evh = w_raw + mu;
-  const uint32_t plan_wgs = (uint32_t)std::min<uint64_t>((n + 256) / 256, hc::kSegPlanMaxWgs);
+  const uint32_t plan_wgs = (uint32_t)std::min<uint64_t>((n + 256) / 256, hc::kSegPlanWgs);  // launch_seg's default cap
   auto old_combine = [&](hipStream_t st) {
     hipLaunchKernelGGL(hc::k_seg_combine_r3j, dim3(2 * cus), dim3(1024), 0, st, b.base, b.off, b.len, n, w_flag, w_raw,
                        w_evh, crc, dst, nullptr);
