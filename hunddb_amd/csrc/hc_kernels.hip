@@ -1231,8 +1231,9 @@ __device__ __forceinline__ uint32_t xcd_wg(uint32_t i, uint32_t G) {
 //                  masks.  One block per wave, 4-wave workgroups that exit:
 //                  row steps and the stream combine through XTab (no LDS
 //                  tables to fill), the lane placement against the
-//                  workgroup's LDS copy of its columns.  The row stores go out
-//                  before the hash (the other orders within +-0.5 %).
+//                  workgroup's LDS copy of its columns.  Rows 1-3 are stored
+//                  before the hash (the other orders within +-0.5 %), row 0
+//                  after it with the CRC in front (one write of the line).
 // Round 2's kernel (persistent 16-wave workgroups, 144 KiB of LDS tables)
 // ran 5.10-5.24 TB/s; this one 5.26-5.48 on the same boxes (tools/kframe3).
 // The first block (row 0 would start 4 bytes before src) and the last (ragged
@@ -1344,12 +1345,12 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
     v[r] = u32x4{f.x, f.y, f.z, f.w};
   }
   uint8_t *ob = dst + b * (uint64_t)HC_FRAME_BLOCK + 16u * lane;
+  // Rows 1-3 now; row 0 after the hash, with the CRC in lane 0's word: one
+  // store of the block's first line, not a zero word now and a 4-byte CRC store
+  // later, which left the L2 as a partial write (0.77M partial 32-B write
+  // requests per 1M blocks, profiles/r4/r4jj/; +0.9 %, r4kk/ab_frame/)
 #pragma unroll
-  for (int r = 0; r < 4; r++) {  // lane 0 writes zeros to bytes 0..3 and the CRC over them below
-    u32x4 t = v[r];
-    if (r == 0) t.x = lane == 0 ? 0u : t.x;
-    __builtin_nontemporal_store(t, reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
-  }
+  for (int r = 1; r < 4; r++) __builtin_nontemporal_store(v[r], reinterpret_cast<u32x4 *>(ob + r * kRowBytes));
   uint32_t c[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -1361,7 +1362,9 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
   }
   const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
   const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
-  lane0_store_u32(reinterpret_cast<uint32_t *>(ob), crcv);  // lane 0's ob is the block start
+  u32x4 t0 = v[0];
+  t0.x = lane == 0 ? crcv : t0.x;  // lane 0's ob is the block start
+  __builtin_nontemporal_store(t0, reinterpret_cast<u32x4 *>(ob));
   if (crc_out) lane0_store_u32(crc_out + b, crcv);
 }
 
