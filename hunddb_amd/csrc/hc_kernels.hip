@@ -1384,8 +1384,9 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ src, 
 //     placement is the 32x32 mat-vec against the workgroup's LDS copy of its
 //     columns (place_lq).
 //   * Payload stores are 16-B unaligned stores (output is shifted 4 bytes per
-//     block); lane 0 of a block's first row stores bytes 4..19 instead (lane
-//     1's first word via DPP), overlapping lane 1's store with identical bytes.
+//     block).  The block's first 12 payload bytes: at 4 KiB a 12-B store by
+//     lane 0; at 8/16 KiB lane 0 of group 0 stores bytes 4..19 (lane 1's first
+//     word via DPP), overlapping lane 1's store with identical bytes.
 //     A group's four rows are hashed, then its four stores are issued together
 //     (+3.9 % over storing each row before hashing it, profiles/r2/framing_store/).
 //   * first_bad: a wave lowers it at most once, and only after reading it
@@ -1438,11 +1439,9 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
     for (int r = 0; r < 4; r++) {
       u32x4 t = v[r];
       if (r == 0) {
-        const uint32_t nx = __builtin_amdgcn_update_dpp(0u, t.x, 0x101, 0xF, 0xF, false);  // lane+1's x
-        stored = __builtin_amdgcn_readfirstlane(t.x);                                         // LE32(block[0:4])
-        const u32x4 first = {t.y, t.z, t.w, nx};
-        sv[r] = lane == 0 ? first : t;
-        sa[r] = ob + (lane == 0 ? 4 : 0);
+        stored = __builtin_amdgcn_readfirstlane(t.x);  // LE32(block[0:4])
+        sv[r] = t;
+        sa[r] = ob;
         t.x = lane == 0 ? w0 : t.x;  // Go's init in place of the CRC field
       } else {
         sv[r] = t;
@@ -1452,8 +1451,20 @@ __global__ __launch_bounds__(256) void k_unframe(const uint8_t *blocks, uint64_t
 #pragma unroll
       for (int k = 0; k < 4; k++) c[k] = r == 0 ? w[k] : xapply(TM, c[k], w[k]);
     }
+    // Lane 0's row-0 bytes 4..15 (the block's first 12 payload bytes) go out by
+    // a 12-B store; the row-0 16-B store runs through a buffer range in which
+    // lane 0 is out of range.  Round 3's form (lane 0 storing bytes 4..19, four
+    // of them over lane 1's) ran 76.3 against 77.9 % (profiles/r4/r4pp/ab_unf/);
+    // the same change at 8/16 KiB (group 0's head) lost 1 point (ab_unf8/16).
+    {
+      typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+      const __amdgpu_buffer_rsrc_t r0 = buf_range(out + b * Bp - 4, kRowBytes);
+      __builtin_amdgcn_raw_buffer_store_b128(sv[0], r0, lane == 0 ? 2u * kRowBytes : 16u * lane, 0, 2);
+      const __amdgpu_buffer_rsrc_t rh = buf_range(out + b * Bp, 12u);
+      __builtin_amdgcn_raw_buffer_store_b96(u32x3{sv[0].y, sv[0].z, sv[0].w}, rh, lane == 0 ? 0u : 16u, 0, 2);
+    }
 #pragma unroll
-    for (int r = 0; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
+    for (int r = 1; r < 4; r++) __builtin_nontemporal_store(sv[r], reinterpret_cast<u32x4_u *>(sa[r]));
     const uint32_t d = xapply(TS, xapply(TS, xapply(TS, c[0], c[1]), c[2]), c[3]);
     const uint32_t crcv = wave_xor(place_lq(lq, lane, d)) ^ 0xFFFFFFFFu;
     if (crc_out) lane0_store_u32(crc_out + b, crcv);
