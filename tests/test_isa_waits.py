@@ -10,7 +10,8 @@ source (CPU: hipcc cross-compiles):
   after the load they wait for (vmcnt(6): three rows, the event window, the
   group's two stores), and no loop-latch register copies wait for refills
   (round 4 found hipcc copying the loop-carried rows at the latch after small
-  unrelated edits; that shows as vmcnt(2)/vmcnt(3) waits before the header).
+  unrelated edits; that shows as vmcnt(2)/vmcnt(3) waits before the header);
+* k_unframe has no readfirstlane (waterfall) loops around its buffer stores.
 """
 import os
 import re
@@ -89,3 +90,13 @@ def test_seg_stream_waits_are_exact(isa):
     assert w.count(6) >= 5, w  # the window and the four row folds
     latch = body[body.rfind("buffer_load_dwordx4", 0, header):header]
     assert not re.search(r"s_waitcnt vmcnt\([0-5]\)", latch), "loop-latch copies wait for the refills"
+
+
+def test_framing_kernels_have_no_waterfall_loops(isa):
+    """k_unframe's buffer stores take their descriptors from wave-uniform values.
+    A base computed through a per-lane value makes hipcc wrap the store in a
+    readfirstlane loop (s_cbranch_execnz). Round 4's first 8/16 KiB head-store
+    variant met that and lost 1.7 points (profiles/r4/r4qq/)."""
+    _, bodies = isa
+    for name in _find(bodies, "k_unframe"):
+        assert "s_cbranch_execnz" not in bodies[name], name
