@@ -767,6 +767,30 @@ def test_dev_read_blocks_parity(cuda, hc, oracle, B):
         assert int(fb.item()) == (int(want_bad[0]) if len(want_bad) else 2**63 - 1)
 
 
+@pytest.mark.parametrize("B", [4096, 8192, 16384])
+@pytest.mark.parametrize("shift", [1, 2, 3, 4, 8, 12])
+def test_dev_read_blocks_misaligned_out(cuda, hc, oracle, B, shift):
+    """payload_out at any byte alignment (hundcrc.h: only `blocks` must be
+    16-byte aligned): k_unframe's unaligned 16-B stores and, at 4 KiB, the
+    12-B head store through a buffer range based at out + b (B-4) - 4.  The
+    bytes on both sides of the payload stay untouched."""
+    torch = cuda
+    rng = np.random.default_rng(B + shift)
+    n = 37
+    host = _stamped_blocks(oracle, rng, n, B)
+    want_crc = oracle.crc32_blocks(host, stride=B, ulen=B)
+    d = torch.from_numpy(host).to("cuda")
+    raw = torch.full((n * (B - 4) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    out = raw[shift:shift + n * (B - 4)]
+    crcs = torch.empty(n, dtype=torch.int32, device="cuda")
+    hc.dev_read_blocks(d, B, out=out, crc_out=crcs)
+    torch.cuda.synchronize()
+    got = raw.cpu().numpy()
+    assert got[shift:shift + n * (B - 4)].tobytes() == host.reshape(n, B)[:, 4:].tobytes(), (B, shift)
+    assert (got[:shift] == 0xA5).all() and (got[shift + n * (B - 4):] == 0xA5).all()
+    assert (u32(crcs) == want_crc).all()
+
+
 def test_frame_unframe_round_trip_full_size(cuda, hc):
     """1M blocks: AddCRCsToData (k_frame) then batched ReadFromDisk (k_unframe)
     gives back the payload, every block verifies, and the CRC words agree with
