@@ -19,7 +19,10 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 192
+# HC_FUZZ_SCALE=k runs k times as many seeds of every case family (the default
+# seeds are the first ones of the larger set): a longer sweep on the box
+SCALE = max(1, int(os.environ.get("HC_FUZZ_SCALE", "1")))
+N_CASES = 192 * SCALE
 MAX_BYTES = 24 << 20
 
 
@@ -140,7 +143,7 @@ def test_random_layout(cuda, hc, oracle, seed, monkeypatch):
     assert int(fb.item()) == (min(bad) if bad else 2**63 - 1)
 
 
-N_FRAMING = 48
+N_FRAMING = 48 * SCALE
 
 
 @pytest.mark.parametrize("seed", range(N_FRAMING))
@@ -200,7 +203,7 @@ def test_random_framing_round_trip(cuda, hc, oracle, seed):
             assert g_err is not None and int(g_err.code) == w_rc and hc.last_bad_block() == w_bad
 
 
-N_WAL = 24
+N_WAL = 24 * SCALE
 
 
 @pytest.mark.parametrize("seed", range(N_WAL))
@@ -234,7 +237,7 @@ def test_random_wal_replay(cuda, hc, oracle, seed):
         assert got == b"".join(want)
 
 
-N_READ = 16
+N_READ = 16 * SCALE
 
 
 @pytest.mark.parametrize("seed", range(N_READ))
@@ -276,7 +279,7 @@ def test_random_read_from_disk_verified_mask(cuda, hc, oracle, seed):
     assert np.unpackbits(v.view(np.uint8), bitorder="little")[:k].sum() == k
 
 
-N_MULTI = 16
+N_MULTI = 16 * SCALE
 
 
 @pytest.mark.parametrize("seed", range(N_MULTI))
@@ -305,7 +308,7 @@ def test_random_multi_gpu_plans(cuda, hc, oracle, seed):
     assert np.array_equal(bm, bm1) and fb == fb1 and str(err) == str(err1)
 
 
-N_UNFRAME = 24
+N_UNFRAME = 24 * SCALE
 
 
 @pytest.mark.parametrize("seed", range(N_UNFRAME))
