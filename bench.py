@@ -75,10 +75,15 @@ WORKLOADS = {
     # address (18.9 GB) -> the packed-record stream (k_seg_*); bytes = record
     # bytes read + 4-B words written
     "records": (2_000_000, "records", "weak"),
+    # the same records with a 17-B gap before each (the WAL header between
+    # payloads, /root/reference/lsm/wal/wal_header.go:5-23): the stream over the
+    # 2n record boundaries (round 5); bytes = record bytes + 4-B words (the gap
+    # bytes the stream also reads are not counted)
+    "records_gapped": (2_000_000, "records_gapped", "weak"),
 }
 # the dominant kernel per workload (PMC passes)
 KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
-             "records": "k_seg_stream"}  # else the streaming CRC kernel
+             "records": "k_seg_stream", "records_gapped": "k_seg_stream"}  # else the streaming CRC kernel
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
 
@@ -109,8 +114,33 @@ def parse(argv=None):
                     help="N>1 strong scaling: each rank fills its shard in HBM (resident), or rank 0 holds the "
                          "whole batch and sends the shards over RCCL first (scatter; timed and reported "
                          "separately, SURVEY.md 8e)")
+    ap.add_argument("--rank-timeout", type=float, default=900.0,
+                    help="N>1: seconds the self-launcher waits for its ranks (then kills them and prints one JSON "
+                         "error line naming the ranks still alive and their phase); also the process-group timeout")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
+
+
+METRIC = "GiB/s CRC32 over device-resident batched 4/8/16 KB blocks; % HBM peak"
+WORKLOAD_NOTE = ("with no --workload, N = 1 runs northstar (1M x 8 KiB, the target config, scaling weak) and N > 1 "
+                 "runs config4 (configs[3]: one 16M x 8 KiB batch split by block index, scaling strong): the value "
+                 "column therefore changes batch between N = 1 and N > 1; multi_gpu.speedup_vs_1gpu (rank 0's "
+                 "1-GPU run of the same 16M-block batch) is the like-for-like number")
+
+
+def phase(name):
+    """Record this rank's phase for the self-launcher (hunddb_amd.shard.report_phase);
+    HC_BENCH_STALL=rank:phase:seconds / HC_BENCH_FAIL=rank:phase make a rank
+    sleep in, or fail at, a phase (the launcher's deadline and failure tests)."""
+    from hunddb_amd import shard
+    shard.report_phase(name)
+    rank = os.environ.get("RANK", "0")
+    st = os.environ.get("HC_BENCH_STALL", "").split(":")
+    if len(st) == 3 and st[0] == rank and st[1] == name:
+        time.sleep(float(st[2]))
+    fl = os.environ.get("HC_BENCH_FAIL", "").split(":")
+    if len(fl) == 2 and fl[0] == rank and fl[1] == name:
+        raise RuntimeError(f"HC_BENCH_FAIL at {name}")
 
 
 # --------------------------------------------------------------------------
@@ -390,10 +420,25 @@ def cpu_baseline_framing(kind, dev_src, threads, budget_s, B=4096):
 def self_launch(argv, nproc, script=None):
     """`bench.py --gpus N` without WORLD_SIZE: run N ranks (one per GPU) as child
     processes with the torch.distributed.run environment; this process never
-    touches the GPU.  Returns the first failing rank's exit status or 0."""
+    touches the GPU.  The ranks get --rank-timeout seconds: when one fails or
+    the deadline passes, the others are killed and this process prints ONE
+    JSON error line (the failed ranks with their phase and error, the ranks
+    still alive with their last phase).  Returns 0 or a non-zero status."""
     from hunddb_amd import shard
     cmd = [sys.executable, os.path.abspath(script or __file__)] + list(argv)
-    return shard.spawn_ranks(cmd, nproc)
+    try:
+        tmo = parse(list(argv)).rank_timeout
+    except SystemExit:  # (--help and the like: the children print it)
+        tmo = 900.0
+    rc, rep = shard.launch_ranks(cmd, nproc, timeout=tmo if tmo > 0 else None)
+    if rep is not None:
+        what = (f"{len(rep['alive'])} of {nproc} ranks still running after the {tmo:g} s deadline"
+                if rep["reason"] == "timeout" else
+                "rank " + ", ".join(str(f["rank"]) for f in rep["failed"]) + " failed")
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": nproc, "error": what,
+                          "reason": rep["reason"], "rank_timeout_s": tmo, "elapsed_s": rep["elapsed_s"],
+                          "failed_ranks": rep["failed"], "alive_ranks": rep["alive"]}), flush=True)
+    return rc
 
 
 def main(argv=None):
@@ -426,11 +471,16 @@ def main(argv=None):
     backend = os.environ.get("HC_DIST_BACKEND", "nccl")
     if world > 1:
         # RCCL (backend "nccl") over xGMI; HC_DIST_BACKEND=gloo rehearses the
-        # N>1 path with several ranks sharing one GPU.
+        # N>1 path with several ranks sharing one GPU.  Bounded: a rank that
+        # never arrives ends init (and every later collective) with an error.
+        import datetime
+        phase("init")
+        tmo = datetime.timedelta(seconds=args.rank_timeout if args.rank_timeout > 0 else 1800)
         if backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend, rank=rank, world_size=world)
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=tmo)
+    phase("fill")
 
     nblk, bsize, scaling = WORKLOADS[args.workload]
     if args.blocks:
@@ -498,11 +548,12 @@ def main(argv=None):
         block_desc = "8192 B, verify mode (stamped; B read + 4 B written per block)"
         k = min(my, (512 << 20) // B)
         sample = (slice(0, k * B), np.arange(k, dtype=np.uint64) * B, np.full(k, B, np.uint32))
-    elif bsize == "records":
+    elif bsize in ("records", "records_gapped"):
         lens_h = record_sizes(my) if not args.blocks else record_sizes(nblk)[:my]
+        gap = 17 if bsize == "records_gapped" else 0
         off_h = np.zeros(my, dtype=np.uint64)
-        off_h[1:] = np.cumsum(lens_h[:-1], dtype=np.uint64)
-        off_h += np.uint64(1)  # back to back from an odd address
+        off_h[1:] = np.cumsum(lens_h[:-1].astype(np.uint64) + np.uint64(gap), dtype=np.uint64)
+        off_h += np.uint64(1 + gap)  # back to back (or 17 B apart) from an odd address
         total = (int(off_h[-1]) + int(lens_h[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
         buf = torch.empty(total, dtype=torch.uint8, device=dev)
         crc.dev_fill_range(buf, SEED, lo << 20, total >> 20, stride=1 << 20, ulen=1 << 20)
@@ -510,7 +561,8 @@ def main(argv=None):
         dlen = torch.from_numpy(lens_h.view(np.int32)).to(dev)
         kw = dict(off=doff, lens=dlen, nblocks=my, flags=crc.HC_F_MESSAGES)
         step_bytes = int(lens_h.sum(dtype=np.uint64)) + 4 * my
-        block_desc = "GetCRC per record: log-uniform 64 B - 64 KiB records back to back (off/len arrays)"
+        block_desc = ("GetCRC per record: log-uniform 64 B - 64 KiB records " +
+                      ("with a 17-B gap before each" if gap else "back to back") + " (off/len arrays)")
         k = int(np.searchsorted(off_h, 512 << 20))
         sample = (slice(0, int(off_h[k - 1]) + int(lens_h[k - 1])), off_h[:k].copy(), lens_h[:k].copy())
     elif bsize in UNFRAME_B:
@@ -600,7 +652,9 @@ def main(argv=None):
         return dt, sum(kern_ms) / (steps if not per_step else len(kern_ms)) / 1e3
 
     step = make_step(buf, out, kw)
+    phase("timed")
     dt, mean_kern_s = timed(step, args.steps, args.warmup, world > 1)
+    phase("report")
     proof = None
     if world > 1:  # which device every rank really ran on, and its own kernel time
         proof = shard.device_proof(shard.gather_identities(shard.rank_identity(dev, mean_kern_s * 1e3)), backend)
@@ -608,7 +662,7 @@ def main(argv=None):
             raise RuntimeError(f"{world} RCCL ranks ran on {proof['distinct_devices']} distinct GPU(s): "
                                f"{[(i['rank'], i['host'], i['bus_id']) for i in proof['ranks']]}")
     info = crc.last_launch()
-    seg_taken = crc.seg_taken() if bsize == "records" else None
+    seg_mode = crc.seg_mode() if bsize in ("records", "records_gapped") else False
     verify_clean = None
     if bsize == "verify":  # every stamped block must have verified clean
         verify_clean = int(first_bad.item()) == 2**63 - 1 and int(bitmap.abs().sum().item()) == 0
@@ -628,6 +682,7 @@ def main(argv=None):
     # global batch on ONE GPU for the strong-scaling speedup and a word check
     multi = None
     if world > 1:
+        phase("gather")
         torch.cuda.synchronize()
         tg = time.perf_counter()
         gathered = shard.gather_crcs(out, counts)
@@ -643,6 +698,7 @@ def main(argv=None):
                               "scatter_note": "rank 0 -> every other rank, RCCL send/recv grouped; outside the "
                                               "timed CRC region (SURVEY.md 8e)"})
             if ref1 and isinstance(kw, dict) and "stride" in kw and scaling == "strong":
+                phase("ref1")
                 del step, buf, out  # the shard (the step closure holds it too)
                 torch.cuda.empty_cache()
                 if full is None:  # (scatter input: rank 0 still holds the whole batch)
@@ -663,6 +719,7 @@ def main(argv=None):
                 del full, outf
                 if not same:
                     print("[bench] gathered CRC words differ from the 1-GPU run", file=sys.stderr)
+        phase("final_barrier")
         dist.barrier()
 
     if rank == 0:
@@ -678,9 +735,9 @@ def main(argv=None):
                                   else "HIP events on the launch stream around every timed launch"),
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
-                **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine + k_crc_any (the "
-                                   "fallback, exits at once when the stream took the batch); traffic: k_seg_stream"}
-                   if bsize == "records" else {}),
+                **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine (the fallback for a "
+                                   "batch the stream refuses runs inside the combine); traffic: k_seg_stream"}
+                   if bsize in ("records", "records_gapped") else {}),
                 "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
@@ -697,9 +754,9 @@ def main(argv=None):
                 cpu = cpu_baseline(host, soff, slen, args.cpu_threads, args.cpu_seconds,
                                    f"{args.workload} ({block_desc})",
                                    gpu_words=out[: len(soff)].cpu().numpy().view(np.uint32),
-                                   messages=bsize == "records")
+                                   messages=bsize in ("records", "records_gapped"))
         res = {
-            "metric": "GiB/s CRC32 over device-resident batched 4/8/16 KB blocks; % HBM peak",
+            "metric": METRIC,
             "value": round(gib_s, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -717,10 +774,12 @@ def main(argv=None):
                        "dist_backend": backend if world > 1 else None,
                        "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4),
                        **({"verify_clean": verify_clean} if verify_clean is not None else {}),
-                       **({"packed_stream_taken": seg_taken} if seg_taken is not None else {})},
+                       **({"packed_stream_taken": seg_mode is not None, "stream_mode": seg_mode}
+                          if seg_mode is not False else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        res["workload_note"] = WORKLOAD_NOTE
         if multi is not None:
             res["multi_gpu"] = multi
             if "speedup_vs_1gpu" in multi:
@@ -730,22 +789,29 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    phase("done")
     if world > 1:
         dist.destroy_process_group()
 
 
 def _run():
     """main(), and on any exception ONE JSON error line naming the rank, then a
-    non-zero exit (never a re-exec, never a silent partial line)."""
+    non-zero exit (never a re-exec, never a silent partial line).  Under the
+    self-launcher the rank records the error with its phase instead, and the
+    launcher prints the one line for the whole job."""
     try:
         main()
     except Exception as e:  # noqa: BLE001
         import traceback
         traceback.print_exc()
         rank = int(os.environ.get("RANK", "0"))
-        print(json.dumps({"metric": "GiB/s CRC32 over device-resident batched 4/8/16 KB blocks; % HBM peak",
-                          "value": None, "error": f"rank {rank}: {type(e).__name__}: {e}", "rank": rank,
-                          "world_size": int(os.environ.get("WORLD_SIZE", "1"))}), flush=True)
+        msg = f"rank {rank}: {type(e).__name__}: {e}"
+        from hunddb_amd import shard
+        if os.environ.get(shard.PHASE_ENV):
+            shard.report_phase("error", error=msg)
+        else:
+            print(json.dumps({"metric": METRIC, "value": None, "error": msg, "rank": rank,
+                              "world_size": int(os.environ.get("WORLD_SIZE", "1"))}), flush=True)
         sys.exit(3)
 
 

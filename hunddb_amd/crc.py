@@ -141,6 +141,7 @@ def _lib():
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_debug_seg_taken": (I, []),
+            "hc_debug_set": (I, [ctypes.c_char_p, ctypes.c_char_p]),
             "hc_device_count": (I, []),
             "hc_host_pipelines": (I, []),
             "hc_stats": (I, [ctypes.POINTER(Stats)]),
@@ -633,14 +634,31 @@ def host_pipelines() -> int:
     return int(_lib().hc_host_pipelines())
 
 
-def seg_taken() -> bool:
-    """Whether this thread's last device batch of packed whole messages was
-    hashed by the packed-record stream (k_seg_*) rather than k_crc_any
-    (synchronizes the device; tests and tools)."""
+def debug_set(name: str, value=None) -> None:
+    """Change one of the library's HC_* settings after it has read them from
+    the environment (hc_debug_set; None restores the compiled default)."""
+    v = None if value is None else str(value).encode()
+    r = int(_lib().hc_debug_set(name.encode(), v))
+    if r != 0:
+        raise HundCRCError(r, f"debug_set({name})")
+
+
+def seg_mode():
+    """How this thread's last device batch of whole messages was hashed:
+    "packed" (the packed-record stream over records back to back), "gapped"
+    (the same stream over sorted records with gaps), or None (k_crc_any).
+    Synchronizes the device; tests and tools."""
     r = int(_lib().hc_debug_seg_taken())
     if r < 0:
         raise HundCRCError(r, "seg_taken")
-    return r == 1
+    return {1: "packed", 2: "gapped"}.get(r)
+
+
+def seg_taken() -> bool:
+    """Whether this thread's last device batch of whole messages was hashed by
+    the packed-record stream (k_seg_*, packed or gapped) rather than k_crc_any
+    (synchronizes the device; tests and tools)."""
+    return seg_mode() is not None
 
 
 def debug_tables() -> np.ndarray:

@@ -157,7 +157,7 @@ int init_device(int dev) {
   return d.status;
 }
 
-int default_device() { return env_int("HC_DEVICE", 0); }
+int default_device() { return (int)knob(kKnobDevice); }
 
 }  // namespace
 
@@ -199,10 +199,7 @@ namespace {
 // hipFreeAsync pair cost 4-17 us a call, tools/kseg3.hip); other streams take
 // one from the stream-ordered allocator per call.  The span is bounded by the allocation holding
 // `base` (a batch reaching past it is not packed for the stream).
-uint64_t seg_min_msgs() {
-  const char *v = std::getenv("HC_SEG_MIN_MSGS");
-  return v && *v ? std::strtoull(v, nullptr, 10) : 1ull;
-}
+uint64_t seg_min_msgs() { return (uint64_t)std::max<int64_t>(0, knob(kKnobSegMinMsgs)); }
 
 // The kept workspace (null stream only), grown to `need` bytes on that stream,
 // so the free is ordered after every earlier use.  The lock is held from here
@@ -360,12 +357,14 @@ struct HostPipe {
     if (ok && dev == d) return HC_OK;
     release();
     dev = d;
-    chunk = (size_t)env_int("HC_CHUNK_MB", 64) << 20;
+    static const size_t chunk_env = (size_t)std::max(1, env_int("HC_CHUNK_MB", 64)) << 20;  // read once
+    static const size_t span_env = (size_t)std::max(1, env_int("HC_SPAN_MB", 256)) << 20;
+    chunk = chunk_env;
     maxblk = chunk / 64 + 1;
     // span DMA needs no pinned staging, so its chunks can be larger: fewer,
     // fuller kernels (the MD5 of one 64 MiB chunk of records is a few dozen
     // waves -- too little parallelism to keep up with the copy)
-    span = std::max(chunk, (size_t)env_int("HC_SPAN_MB", 256) << 20);
+    span = std::max(chunk, span_env);
     DeviceGuard g(dev);
     for (auto &s : slot) {
       if (hipHostMalloc(reinterpret_cast<void **>(&s.pin), chunk, hipHostMallocDefault) != hipSuccess ||
@@ -552,7 +551,7 @@ int host_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, ui
     if (crc_out) crc_out[k] = c;
     if (stamp && blk_len(len, ulen, k) >= HC_CRC_SIZE) std::memcpy(stamp + blk_off(off, stride, k), &c, 4);
   };
-  const int copy_threads = std::max(1, env_int("HC_COPY_THREADS", 8));
+  const int copy_threads = (int)std::max<int64_t>(1, knob(kKnobCopyThreads));
   // direct DMA: uniform, densely packed (stride == ulen, 16-B multiple) and already pinned
   const bool direct = !off && !len && stride == ulen && ulen > 0 && (ulen & 15u) == 0 &&
                       (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && is_pinned(base);
@@ -867,7 +866,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
   // host path below (hc_cpu.cpp, product code) from the already framed dst,
   // and counted in hc_stats.  Only HC_FORCE_GPU (test mode) returns the error.
   // HC_INJECT_FAIL=add_crcs[:nomem] simulates a failing GPU batch (tests).
-  const size_t gpu_min = (size_t)env_int("HC_ADD_CRCS_GPU_MIN_BLOCKS", (int)kAddCrcsGpuMinBlocks);  // per call: tools/crossover.py
+  const size_t gpu_min = (size_t)knob(kKnobAddCrcsGpuMin);  // hc_debug_set: tools/crossover.py
   bool on_gpu = false;
   if (nb >= gpu_min || (force_gpu() && nb > 0)) {
     // The CRC of block k is ChecksumIEEE(src[4092k : 4092k+4092]) for every
@@ -877,7 +876,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
     // first and reading dst back.  The ragged last block (zero-padded) is
     // hashed on the host after framing.
     // framing tasks: HC_COPY_THREADS (8), one per MiB of output at most
-    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max(1, env_int("HC_COPY_THREADS", 8)), nb >> 8));
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max<int64_t>(1, knob(kKnobCopyThreads)), nb >> 8));
     std::vector<uint32_t> crc(nfull);
     int rc = HC_OK;
     // (plain stores: streamed framing measured 10-35 % slower, profiles/r2/addcrcs/)
@@ -888,7 +887,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
         return;
       }
       if (!nfull) return;
-      if (const int inj = injected_failure("add_crcs")) {
+      if (const int inj = injected_failure(kInjectAddCrcs)) {
         rc = inj;
         return;
       }
@@ -914,7 +913,7 @@ size_t hc_add_crcs(const uint8_t *src, size_t n, uint8_t *dst, size_t dst_cap) {
       }
       on_gpu = true;
       g_stats.add_crcs_gpu.fetch_add(1, std::memory_order_relaxed);
-    } else if (force_gpu()) {
+    } else if (force_gpu() || !gpu_batch_failure(rc)) {
       return (size_t)-1;
     } else if (rc == HC_E_NODEV) {
       g_stats.add_crcs_host_nodev.fetch_add(1, std::memory_order_relaxed);
@@ -1215,7 +1214,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
     }
   };
   bool copied = false, on_gpu = false;
-  const uint64_t gpu_min = (uint64_t)env_int("HC_READ_GPU_MIN_BLOCKS", (int)kReadGpuMinBlocks);  // per call: tools/crossover.py
+  const uint64_t gpu_min = (uint64_t)knob(kKnobReadGpuMin);  // hc_debug_set: tools/crossover.py
   const uint64_t nt = todo.size();
   std::vector<uint8_t> ok(nt, 0);
   if (nt && (nt >= gpu_min || force_gpu()) && B <= 0xFFFFFFFFu) {
@@ -1227,7 +1226,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
     // on a CRC failure `out` is left unspecified (Go returns no data)
     // copy-out tasks: HC_COPY_THREADS (8), one per MiB of blocks at most; task 0
     // is the GPU batch, so the caller starts it at once
-    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max(1, env_int("HC_COPY_THREADS", 8)),
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max<int64_t>(1, knob(kKnobCopyThreads)),
                                                                  k * B >> 20));
     int rc = HC_OK;
     parallel_for(T + 1, [&](int t) {
@@ -1235,7 +1234,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
         copy_out(k * (t - 1) / T, k * t / T);
         return;
       }
-      if ((rc = injected_failure("read_from_disk")) != HC_OK) return;
+      if ((rc = injected_failure(kInjectReadFromDisk)) != HC_OK) return;
       if (nt == nfull) {  // nothing masked: one uniform batch
         rc = host_batch(blocks, nullptr, nullptr, B, (uint32_t)B, nt, nullptr, 0, nullptr, &hv);
       } else {
@@ -1250,7 +1249,7 @@ int hc_read_from_disk_v(const uint8_t *blocks, uint64_t avail, uint32_t block_si
       for (uint64_t j = 0; j < nt; j++) ok[j] = !((badj[j >> 5] >> (j & 31)) & 1u);
       on_gpu = true;
       g_stats.read_gpu.fetch_add(1, std::memory_order_relaxed);
-    } else if (force_gpu()) {
+    } else if (force_gpu() || !gpu_batch_failure(rc)) {
       return rc;
     } else {  // ReadFromDisk fails only on I/O or a CRC mismatch: finish on the host path
       count_fallback(g_stats.read_gpu_fallback, rc);
@@ -1416,8 +1415,10 @@ int hc_debug_seg_taken(void) {
   if (hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(&v, g_dev[dev].seg_last, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return HC_E_HIP;
-  return v ? 1 : 0;
+  return v == 2 ? 2 : v ? 1 : 0;
 }
+
+int hc_debug_set(const char *name, const char *value) { return hc::knob_set(name, value) ? HC_OK : HC_E_ARG; }
 
 int hc_debug_tables(void *out, size_t cap) {
   if (!out || cap < sizeof(DeviceTables)) return (int)sizeof(DeviceTables);

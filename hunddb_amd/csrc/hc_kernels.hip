@@ -1632,66 +1632,94 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
   return g;
 }
 
-// Events: position j = base + off[j] (j < n) and the span's end (j = n).
-// first_ev[u] = first event in unit u (u = 0 .. units; first_ev[units] = n + 1).
-// Workgroup w writes plan_bad[w] = 1 when its events find the batch not packed,
-// over max_units, with a record over kSegMaxRecord, or with more than 64 events
-// in one 4 KiB group (records under ~64 B: k_crc_any), else 0.  Every slot is
-// written, so the dispatch needs no memset: k_seg_stream's workgroups OR the
-// slots and its workgroup 0 stores the flag the later kernels read.
+// Two event lists, one plan.  A packed batch (off[j] = off[j-1] + len[j-1])
+// has the n + 1 events s_0 .. s_{n-1}, pend (record j = events j, j+1).  A
+// sorted batch with gaps (round 5: off[j] >= off[j-1] + len[j-1], e.g. WAL
+// records behind their 17-B headers) has the 2n events s_0, e_0, s_1, e_1, ..
+// (record j = events 2j, 2j+1; e_{n-1} = pend); the identity of the stream
+// (raw(a .. b) from G(a) and G(b)) does not need the records to touch.
+// first_ev[u] = the first event at or after unit u's start, in the gapped
+// numbering (u = 0 .. units; first_ev[units] = 2n + 2); for a packed batch
+// e_{j-1} and s_j coincide, so its packed number is (first_ev[u] + 1) >> 1.
+// Workgroup w writes plan_bad[w]: bit 0 when its records find the batch not
+// packed or with more than 64 packed events in one 4 KiB group (records under
+// ~64 B), bit 1 when they find records out of order or overlapping, or more
+// than 64 gapped events in a group; both when the span exceeds max_units, a
+// record exceeds kSegMaxRecord or lies outside [s_0, pend].  plan_gx[w] =
+// sum over its records of 4 * (gap before it) - len: the stream takes a gapped
+// batch only when the grid's sum is <= 0 (gap bytes at most a quarter of the
+// payload, the span-DMA rule of the host pipeline).  Every slot is written, so
+// the dispatch needs no memset: k_seg_stream's workgroups reduce the slots and
+// its workgroup 0 stores the mode the combine reads.
+constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2;  // the mode word k_seg_stream stores
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
-                                                  uint32_t *__restrict__ plan_bad, uint32_t *__restrict__ first_ev) {
+                                                  uint32_t *__restrict__ plan_bad, long long *__restrict__ plan_gx,
+                                                  uint32_t *__restrict__ first_ev) {
+  __shared__ uint32_t s_bad;
+  __shared__ unsigned long long s_gx;
+  if (threadIdx.x == 0) {
+    s_bad = 0;
+    s_gx = 0;
+  }
   const SegGeo g = seg_geo<kU>(base, offs, lens, n);
-  bool bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0;
+  uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 3u : 0u;
+  long long gx = 0;
+  auto grp = [&](uint64_t p) { return (p - g.a0) >> 12; };
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= n && !bad; j += step) {
-    const uint64_t pj = j < n ? (uint64_t)base + offs[j] : g.pend;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n && bad != 3u; j += step) {
+    const uint64_t s = (uint64_t)base + offs[j], l = lens[j], e = s + l;
+    if (l > kSegMaxRecord || s < g.a0 || e > g.pend) {  // k_seg_combine's unit chain stays <= 1025 units
+      bad = 3u;
+      break;
+    }
     uint64_t ulo = 0;
     if (j > 0) {
-      const uint64_t pp = (uint64_t)base + offs[j - 1];
-      if ((j < n && offs[j] != offs[j - 1] + lens[j - 1]) || pj < pp) bad = true;
-      if (lens[j - 1] > kSegMaxRecord) bad = true;  // k_seg_combine's unit chain stays <= 1025 units
-      ulo = ((pp - g.a0) >> kU) + 1;
+      const uint64_t sp = (uint64_t)base + offs[j - 1], ep = sp + lens[j - 1];
+      if (s != ep) bad |= 1u;
+      if (s < ep) bad |= 2u;
+      gx += 4 * (long long)(s >= ep ? s - ep : 0);
+      ulo = ((ep - g.a0) >> kU) + 1;
     }
-    if (j >= 64 && ((pj - g.a0) >> 12) == (((uint64_t)base + offs[j - 64] - g.a0) >> 12)) bad = true;
-    const uint64_t uj = (pj - g.a0) >> kU;
-    if (uj >= g.units || pj < g.a0) bad = true;
-    if (bad) break;
-    for (uint64_t u = ulo; u <= uj; u++) first_ev[u] = (uint32_t)j;
-    if (j == n)
-      for (uint64_t u = uj + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(n + 1);
+    gx -= (long long)l;
+    if (j >= 64 && grp(s) == grp((uint64_t)base + offs[j - 64])) bad |= 1u;
+    if (j + 1 == n && n >= 64 && grp(g.pend) == grp((uint64_t)base + offs[n - 64])) bad |= 1u;
+    if (j >= 32) {  // gapped events 2j, 2j+1 against 2j-64, 2j-63: s_{j-32}, e_{j-32}
+      const uint64_t sq = (uint64_t)base + offs[j - 32];
+      if (grp(s) == grp(sq) || grp(e) == grp(sq + lens[j - 32])) bad |= 2u;
+    }
+    if (bad == 3u) break;
+    const uint64_t us = (s - g.a0) >> kU, ue = (e - g.a0) >> kU;
+    for (uint64_t u = ulo; u <= us; u++) first_ev[u] = (uint32_t)(2 * j);
+    for (uint64_t u = us + 1; u <= ue; u++) first_ev[u] = (uint32_t)(2 * j + 1);
+    if (j + 1 == n)
+      for (uint64_t u = ue + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(2 * n + 2);
   }
-  const int any_bad = __syncthreads_or(bad);
-  if (threadIdx.x == 0) plan_bad[blockIdx.x] = any_bad ? 1u : 0u;  // every slot written: no memset
+  __syncthreads();
+  if (bad) atomicOr(&s_bad, bad);
+  if (gx) atomicAdd(&s_gx, (unsigned long long)gx);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // every slot written: no memset
+    plan_bad[blockIdx.x] = s_bad;
+    plan_gx[blockIdx.x] = (long long)s_gx;
+  }
 }
 
-// (its timing-only builds -- rows XOR-folded, or no event work at all -- are in
-// git history: tools/ab_hc_kernels.hip, up to commit 61a2e0e)
-template <uint32_t kU = kSegUnitLg>
-__global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
-                                                            const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
-                                                            uint32_t plan_wgs, uint32_t *__restrict__ flag,
-                                                            const uint32_t *__restrict__ first_ev,
-                                                            uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
-                                                            const DeviceTables *__restrict__ tables) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
-  __shared__ uint32_t s_next;
+// The stream over one event numbering (k_seg_plan): kGap, the 2n events of a
+// sorted batch with gaps (each window lane loads off[] and len[] of its
+// record: s_j = off, e_j = off + len); else the n + 1 events of a packed
+// batch (off[] only, first_ev converted).  (Its timing-only builds -- rows
+// XOR-folded, or no event work at all -- are in git history:
+// tools/ab_hc_kernels.hip, up to commit 61a2e0e.)
+template <bool kGap, uint32_t kU>
+__device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next, const uint32_t (&col)[32],
+                                                const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                const uint32_t *__restrict__ lens, uint64_t n, uint32_t lg_chunk,
+                                                const uint32_t *__restrict__ first_ev, uint32_t *__restrict__ unit_raw,
+                                                uint32_t *__restrict__ ev_h) {
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
-  if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
-  uint32_t col[32];
-#pragma unroll
-  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  uint32_t bad = 0;
-  for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) bad |= plan_bad[i];
-  if (__syncthreads_or((int)bad)) bad = 1;
-  if (blockIdx.x == 0 && tid == 0) *flag = bad;  // read by k_seg_combine and the fallback kernels
-  if (bad) return;                                // not a packed batch: k_crc_any takes it
-
   const uint32_t r4 = (lane & 31u) << 2;
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
   const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
@@ -1740,16 +1768,40 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     return buf_range(reinterpret_cast<const void *>(U), (uint32_t)(avail < (1u << kU) ? avail : (1u << kU)));
   };
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  // window: the positions of events f .. f+63, one per lane (a group holds at most 64)
-  auto win_issue = [&](uint64_t f) -> u32x2 {
-    const uint64_t fc = f < n ? f : n;
-    const uint64_t cnt = n - fc;
-    const __amdgpu_buffer_rsrc_t r = buf_range(offs + fc, (uint32_t)(cnt < 64 ? cnt * 8 : 512));
-    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, 0, 0));
+  // the first event at or after unit u's start, in this body's numbering
+  auto fev = [&](uint64_t u_) -> uint64_t {
+    const uint32_t f = first_ev[u_];
+    return kGap ? (uint64_t)f : (uint64_t)((f + 1u) >> 1);
   };
-  auto win_pos = [&](u32x2 v, uint64_t f) -> uint64_t {
+  // window: the positions of events f .. f+63, one per lane (a group holds at most 64)
+  struct Win {
+    u32x2 o;
+    uint32_t l;
+  };
+  auto win_issue = [&](uint64_t f) -> Win {
+    Win w;
+    if constexpr (!kGap) {
+      const uint64_t fc = f < n ? f : n;
+      const uint64_t cnt = n - fc;
+      const __amdgpu_buffer_rsrc_t r = buf_range(offs + fc, (uint32_t)(cnt < 64 ? cnt * 8 : 512));
+      w.o = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8u, 0, 0));
+      w.l = 0;
+    } else {  // events f .. f+63 are s/e of at most 33 records from f >> 1
+      const uint64_t r0 = (f >> 1) < n ? f >> 1 : n;
+      const uint64_t cnt = n - r0;
+      const uint32_t rel = (((uint32_t)f & 1u) + lane) >> 1;
+      const __amdgpu_buffer_rsrc_t ro = buf_range(offs + r0, (uint32_t)(cnt < 33 ? cnt * 8 : 264));
+      const __amdgpu_buffer_rsrc_t rl = buf_range(lens + r0, (uint32_t)(cnt < 33 ? cnt * 4 : 132));
+      w.o = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(ro, rel * 8u, 0, 0));
+      w.l = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, rel * 4u, 0, 0);
+    }
+    return w;
+  };
+  auto win_pos = [&](Win v, uint64_t f) -> uint64_t {
     const uint64_t j = f + lane;
-    return j < n ? (uint64_t)base + (((uint64_t)v.y << 32) | v.x) : j == n ? geo.pend : ~0ull;
+    const uint64_t p = (uint64_t)base + (((uint64_t)v.o.y << 32) | v.o.x);
+    if constexpr (!kGap) return j < n ? p : j == n ? geo.pend : ~0ull;
+    return j < 2 * n ? p + ((j & 1u) ? v.l : 0u) : ~0ull;
   };
 
   uint64_t u = unit_of(wave);
@@ -1757,8 +1809,8 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   uint64_t un = unit_of(kFastWaves + wave);
   uint32_t kv = 0;  // VGPR: the LDS hand-out result, read one unit later
   if (lane == 0) kv = atomicAdd(&s_next, 1u);
-  uint64_t wfirst = first_ev[u];
-  u32x2 wraw = win_issue(wfirst);
+  uint64_t wfirst = fev(u);
+  Win wraw = win_issue(wfirst);
   __amdgpu_buffer_rsrc_t rc = unit_rsrc(u);
   uint4 q0 = buf_load16(rc, lane * 16u), q1 = buf_load16(rc, 1024u + lane * 16u),
         q2 = buf_load16(rc, 2048u + lane * 16u), q3 = buf_load16(rc, 3072u + lane * 16u);
@@ -1854,7 +1906,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     const bool lastg = g == (1u << (kU - 12)) - 1u;  // the unit's last 4 KiB group
     // the next group: this unit's, or unit un's first; its events' window
     const uint32_t gcnt = (uint32_t)__popcll(__ballot(wpos < gs + 4096u));  // the group's events
-    const uint64_t nf = lastg ? (uint64_t)first_ev[un < M ? un : M] : wfirst + gcnt;
+    const uint64_t nf = lastg ? fev(un < M ? un : M) : wfirst + gcnt;
     const __amdgpu_buffer_rsrc_t rn = lastg ? unit_rsrc(un) : rc;
     const uint32_t no = lastg ? lane * 16u : ((g + 1) << 12) + lane * 16u;
     // each refill pinned right after its row's fold and events (sched
@@ -1890,6 +1942,52 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
       g++;
     }
   }
+}
+
+// The prologue reduces the plan's slots beside the table fill: packed when no
+// workgroup found the batch unpacked, else gapped when none found it out of
+// order and the gap bytes are at most a quarter of the payload, else the
+// fallback (all exit; k_seg_combine runs k_crc_any's work).  Workgroup 0 stores
+// the mode for the combine.
+template <uint32_t kU = kSegUnitLg>
+__global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                            const uint32_t *__restrict__ lens, uint64_t n,
+                                                            uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
+                                                            const long long *__restrict__ plan_gx, uint32_t plan_wgs,
+                                                            uint32_t *__restrict__ flag,
+                                                            const uint32_t *__restrict__ first_ev,
+                                                            uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
+                                                            const DeviceTables *__restrict__ tables) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
+  __shared__ uint32_t s_next;
+  __shared__ long long s_gx[kFastWaves];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  fill_crc_tables(lds, tables, tid, kFastThreads);
+  if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  uint32_t bad = 0;
+  long long gx = 0;
+  for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) {
+    bad |= plan_bad[i];
+    gx += plan_gx[i];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) gx += __shfl_xor(gx, d);
+  if (lane == 0) s_gx[tid >> 6] = gx;
+  const int unpacked = __syncthreads_or((int)(bad & 1u));
+  const int unsorted = __syncthreads_or((int)(bad & 2u));  // (also orders the s_gx stores)
+  long long gsum = 0;
+#pragma unroll
+  for (int w = 0; w < kFastWaves; w++) gsum += s_gx[w];
+  const uint32_t mode = !unpacked ? kSegPacked : !unsorted && gsum <= 0 ? kSegGapped : kSegFallback;
+  if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
+  if (mode == kSegGapped)
+    seg_stream_body<true, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
+  else if (mode == kSegPacked)
+    seg_stream_body<false, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
 }
 
 __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) {
@@ -1942,9 +2040,11 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
       if (i < kQ) reinterpret_cast<uint4 *>(tl)[i] = t[k];
     }
   }
-  if (taken && blockIdx.x == 0 && threadIdx.x == 0) *taken = *flag ? 0u : 1u;  // (hc_debug_seg_taken)
+  const uint32_t mode = *flag;
+  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped)
+    *taken = mode == kSegFallback ? 0u : mode == kSegGapped ? 2u : 1u;
   __syncthreads();
-  if (*flag) {
+  if (mode == kSegFallback) {
     // the stream did not take the batch: k_crc_any's work over every message,
     // in this launch (round 3 launched k_crc_any after the combine, ~5 us a
     // call even when it exits at once).  The tables above are not used: the
@@ -1959,6 +2059,48 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   auto rsh = [&](uint32_t v, uint32_t rows) {  // rows in [0, 16]
     return rows ? seg_lds_tmul(tl + (rows - 1u) * 1024u, v) : v;
   };
+  // the record [a, b), with x = offsets from A0 and H from the stream
+  auto rec_crc = [&](uint64_t xa, uint32_t ha, uint64_t xb, uint32_t hb) -> uint32_t {
+    const uint32_t re = (uint32_t)(xa >> 10) + 1u, rb = (uint32_t)(xb >> 10) + 1u;  // row ends, in rows from A0
+    const uint32_t da = (uint32_t)(((uint64_t)re << 10) - xa), db = (uint32_t)(((uint64_t)rb << 10) - xb);
+    const uint64_t ua = xa >> kU, ub = xb >> kU;
+    const uint32_t X = ha ^ st->ones[da - 1];
+    const uint32_t ue = (uint32_t)(ua + 1) * kUnitRows;  // a's unit end, in rows
+    uint32_t v = rsh(X, ua < ub ? ue - re : rb - re);
+    if (ua < ub) {  // the units a .. b-1 (Horner, 16 rows a step), then U_b -> re_b
+      v ^= unit_raw[ua];
+      for (uint64_t u = ua + 1; u < ub; u++) v = seg_lds_tmul(tl + (kUnitRows - 1u) * 1024u, v) ^ unit_raw[u];
+      v = rsh(v, rb - (uint32_t)ub * kUnitRows);
+    }
+    uint32_t y = hb ^ v;
+    const uint32_t e = db - 1u;  // inverse shift by db = 1 + e: octal digits of e
+    const uint32_t *ti = tl + kIv0;
+    y = seg_lds_tmul(ti + (e & 7u) * 1024u, y);
+    if ((e >> 3) & 7u) y = seg_lds_tmul(ti + (kSegIvD1 - 1u + ((e >> 3) & 7u)) * 1024u, y);
+    if ((e >> 6) & 7u) y = seg_lds_tmul(ti + (kSegIvD2 - 1u + ((e >> 6) & 7u)) * 1024u, y);
+    if (e >> 9) y = seg_lds_tmul(ti + kSegIvD3 * 1024u, y);
+    return y ^ 0xFFFFFFFFu;
+  };
+  if (mode == kSegGapped) {  // record j = events 2j (s_j) and 2j+1 (e_j), one record a lane
+    for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
+      uint64_t xa[kSub];
+      uint32_t ln[kSub], ha[kSub], hb[kSub];
+#pragma unroll
+      for (int p = 0; p < kSub; p++) {
+        const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1;
+        xa[p] = (uint64_t)base + offs[jj] - geo.a0;
+        ln[p] = lens[jj];
+        ha[p] = ev_h[2 * jj];
+        hb[p] = ev_h[2 * jj + 1];
+      }
+#pragma unroll
+      for (int p = 0; p < kSub; p++) {
+        const uint64_t j = c + 64u * p + lane;
+        if (j < n) crc_out[j] = rec_crc(xa[p], ha[p], xa[p] + ln[p], hb[p]);
+      }
+    }
+    return;
+  }
   for (uint64_t c = wv * 63u * kSub; c < n; c += nw * 63u * kSub) {
     uint64_t x[kSub];
     uint32_t eh[kSub];
@@ -1971,29 +2113,9 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
 #pragma unroll
     for (int p = 0; p < kSub; p++) {
       const uint64_t j = c + 63u * p + lane;
-      const uint32_t re = (uint32_t)(x[p] >> 10) + 1u;  // the row end, in rows from A0
-      const uint32_t kb = __shfl_down(eh[p], 1), rb = __shfl_down(re, 1);
+      const uint32_t kb = __shfl_down(eh[p], 1);
       const uint64_t xb = __shfl_down((unsigned long long)x[p], 1);
-      if (lane < 63 && j < n) {
-        const uint32_t da = (uint32_t)(((uint64_t)re << 10) - x[p]), db = (uint32_t)(((uint64_t)rb << 10) - xb);
-        const uint64_t ua = x[p] >> kU, ub = xb >> kU;
-        const uint32_t X = eh[p] ^ st->ones[da - 1];
-        const uint32_t ue = (uint32_t)(ua + 1) * kUnitRows;  // a's unit end, in rows
-        uint32_t v = rsh(X, ua < ub ? ue - re : rb - re);
-        if (ua < ub) {  // the units a .. b-1 (Horner, 16 rows a step), then U_b -> re_b
-          v ^= unit_raw[ua];
-          for (uint64_t u = ua + 1; u < ub; u++) v = seg_lds_tmul(tl + (kUnitRows - 1u) * 1024u, v) ^ unit_raw[u];
-          v = rsh(v, rb - (uint32_t)ub * kUnitRows);
-        }
-        uint32_t y = kb ^ v;
-        const uint32_t e = db - 1u;  // inverse shift by db = 1 + e: octal digits of e
-        const uint32_t *ti = tl + kIv0;
-        y = seg_lds_tmul(ti + (e & 7u) * 1024u, y);
-        if ((e >> 3) & 7u) y = seg_lds_tmul(ti + (kSegIvD1 - 1u + ((e >> 3) & 7u)) * 1024u, y);
-        if ((e >> 6) & 7u) y = seg_lds_tmul(ti + (kSegIvD2 - 1u + ((e >> 6) & 7u)) * 1024u, y);
-        if (e >> 9) y = seg_lds_tmul(ti + kSegIvD3 * 1024u, y);
-        crc_out[j] = y ^ 0xFFFFFFFFu;
-      }
+      if (lane < 63 && j < n) crc_out[j] = rec_crc(x[p], eh[p], xb, kb);
     }
   }
 }
@@ -2115,8 +2237,11 @@ hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, 
 
 uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
 
+// workspace (u32 words): the mode flag (64 words), plan_bad[kSegPlanMaxWgs],
+// plan_gx[kSegPlanMaxWgs] (int64), first_ev[max_units + 1], unit_raw[max_units],
+// ev_h[2n + 1] (the gapped numbering's 2n events; a packed batch uses n + 1)
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
-  return 4 * (64 + kSegPlanMaxWgs + (max_units + 1) + max_units + n + 1);
+  return 4 * (64 + kSegPlanMaxWgs) + 8 * kSegPlanMaxWgs + 4 * ((max_units + 1) + max_units + 2 * n + 1);
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
@@ -2124,16 +2249,18 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
     return hipErrorInvalidValue;
   const uint64_t n = b.nblocks;
-  uint32_t *flag = ws, *plan_bad = ws + 64, *first_ev = plan_bad + kSegPlanMaxWgs, *unit_raw = first_ev + max_units + 1,
+  uint32_t *flag = ws, *plan_bad = ws + 64;
+  long long *plan_gx = reinterpret_cast<long long *>(plan_bad + kSegPlanMaxWgs);  // (8-B aligned: 64 + 16384 words)
+  uint32_t *first_ev = reinterpret_cast<uint32_t *>(plan_gx + kSegPlanMaxWgs), *unit_raw = first_ev + max_units + 1,
            *ev_h = unit_raw + max_units;
   const uint64_t pg = (n + 256) / 256;
   // HC_SEG_PLAN_WGS overrides the plan's grid cap, up to kSegPlanMaxWgs (tuning sweeps)
   static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanWgs)));
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
-                     first_ev);
+                     plan_gx, first_ev);
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
-                     plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
+                     plan_gx, plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
                      b.crc_out, st, taken, b.flags, b.tables);
   return hipGetLastError();

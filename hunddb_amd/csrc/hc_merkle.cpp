@@ -181,7 +181,7 @@ int hc_merkle_levels(const uint8_t *leaves16, uint64_t n, uint8_t *levels16) {
     return HC_OK;
   }
   // one upload of the leaves, the levels on the GPU, one download
-  const int device = env_int("HC_DEVICE", 0);
+  const int device = (int)knob(kKnobDevice);
   int cus = 0;
   int rc = dev_init(device, &cus);
   if (rc != HC_OK) return rc;

@@ -26,10 +26,76 @@ inline int env_int(const char *name, int dflt) {
 // (tools/crossover.py, profiles/r4/r4b/).  A GPU batch costs
 // 35-110 us before its first byte moves (pipeline lease, H2D, launch, D2H,
 // the framing or copy-out tasks); the host path hashes 16 GiB/s per caller.
-// Each is overridable per call by its HC_*_GPU_MIN_BLOCKS.
 constexpr uint64_t kAddCrcsGpuMinBlocks = 2048;  // hc_add_crcs (output blocks; 1024: host 280 / GPU 309 us)
 constexpr uint64_t kReadGpuMinBlocks = 1024;     // hc_read_from_disk[_v] (blocks to hash; 1024: 281 / 220 us)
 constexpr uint64_t kWalGpuMinBlocks = 1024;      // hc_wal_replay[_v] (blocks to verify; 1024: 354 / 338 us)
+
+// The library's per-call settings ("knobs"), read from the environment ONCE,
+// at the first call that needs one, and changed afterwards only through
+// hc_debug_set (tests, tools/crossover.py).  Round 4 read them with getenv on
+// every call; in the Go embedding os.Setenv calls setenv(3) through cgo, and a
+// getenv racing with it is a glibc data race.
+enum Knob : int {
+  kKnobDevice,         // HC_DEVICE: the device of single-device entries (0)
+  kKnobSegMinMsgs,     // HC_SEG_MIN_MSGS: whole-message device batches from this size go to k_seg_* (1)
+  kKnobCopyThreads,    // HC_COPY_THREADS: host framing / copy-out tasks (8)
+  kKnobWalMinRange,    // HC_WAL_MIN_RANGE: blocks per WAL scan range (64)
+  kKnobAddCrcsGpuMin,  // HC_ADD_CRCS_GPU_MIN_BLOCKS (kAddCrcsGpuMinBlocks)
+  kKnobReadGpuMin,     // HC_READ_GPU_MIN_BLOCKS (kReadGpuMinBlocks)
+  kKnobWalGpuMin,      // HC_WAL_GPU_MIN_BLOCKS (kWalGpuMinBlocks)
+  kKnobForceGpu,       // HC_FORCE_GPU: test mode, the drop-ins through the GPU and no host finish (0)
+  kKnobInject,         // HC_INJECT_FAIL=<site>[:nomem]: test mode, a named GPU batch fails (0 = none)
+  kKnobCount
+};
+struct KnobDef {
+  const char *env;
+  int64_t dflt;
+};
+inline constexpr KnobDef kKnobDefs[kKnobCount] = {
+    {"HC_DEVICE", 0},          {"HC_SEG_MIN_MSGS", 1},
+    {"HC_COPY_THREADS", 8},    {"HC_WAL_MIN_RANGE", 64},
+    {"HC_ADD_CRCS_GPU_MIN_BLOCKS", (int64_t)kAddCrcsGpuMinBlocks},
+    {"HC_READ_GPU_MIN_BLOCKS", (int64_t)kReadGpuMinBlocks},
+    {"HC_WAL_GPU_MIN_BLOCKS", (int64_t)kWalGpuMinBlocks},
+    {"HC_FORCE_GPU", 0},       {"HC_INJECT_FAIL", 0},
+};
+// HC_INJECT_FAIL sites, as knob values (site | 16 for :nomem)
+enum : int64_t { kInjectAddCrcs = 1, kInjectReadFromDisk = 2, kInjectWalReplay = 3, kInjectNomem = 16 };
+inline int64_t parse_inject(const char *v) {
+  if (!v || !*v) return 0;
+  static const char *const sites[] = {"add_crcs", "read_from_disk", "wal_replay"};
+  for (int k = 0; k < 3; k++) {
+    const size_t n = std::strlen(sites[k]);
+    if (std::strncmp(v, sites[k], n) != 0) continue;
+    if (v[n] == 0) return k + 1;
+    if (v[n] == ':' && std::strcmp(v + n + 1, "nomem") == 0) return (k + 1) | kInjectNomem;
+  }
+  return 0;  // an unknown site injects nothing
+}
+// parse a knob's text value (the environment or hc_debug_set); nullptr/"" -> the default
+inline int64_t parse_knob(int k, const char *v) {
+  if (!v || !*v) return kKnobDefs[k].dflt;
+  if (k == kKnobInject) return parse_inject(v);
+  return std::strtoll(v, nullptr, 10);
+}
+inline std::atomic<int64_t> g_knobs[kKnobCount];
+inline std::once_flag g_knobs_once;
+inline int64_t knob(Knob k) {
+  std::call_once(g_knobs_once, [] {
+    for (int i = 0; i < kKnobCount; i++) g_knobs[i].store(parse_knob(i, std::getenv(kKnobDefs[i].env)));
+  });
+  return g_knobs[k].load(std::memory_order_relaxed);
+}
+// hc_debug_set: by environment name; value nullptr restores the compiled default
+inline bool knob_set(const char *name, const char *value) {
+  knob(kKnobDevice);  // (the environment is read first, so a set is never overwritten by it)
+  for (int i = 0; i < kKnobCount; i++)
+    if (name && std::strcmp(name, kKnobDefs[i].env) == 0) {
+      g_knobs[i].store(parse_knob(i, value));
+      return true;
+    }
+  return false;
+}
 
 // Process-wide event counters behind hc_stats() (defined in hc_api.cpp).
 struct Stats {
@@ -39,21 +105,24 @@ struct Stats {
 };
 extern Stats g_stats;
 
-// HC_INJECT_FAIL=<site>[:nomem] (read per call, tests only): the named GPU
-// batch ("add_crcs", "read_from_disk", "wal_replay") reports HC_E_HIP (or
+// The HC_INJECT_FAIL test hook: the named GPU batch reports HC_E_HIP (or
 // HC_E_NOMEM) without running, so the host recovery path can be tested on any
-// machine.  Returns 0 when `site` is not named.
-inline int injected_failure(const char *site) {
-  const char *v = std::getenv("HC_INJECT_FAIL");
-  if (!v || !*v) return 0;
-  const size_t n = std::strlen(site);
-  if (std::strncmp(v, site, n) != 0 || (v[n] != 0 && v[n] != ':')) return 0;
-  return (v[n] == ':' && std::strcmp(v + n + 1, "nomem") == 0) ? -4 /*HC_E_NOMEM*/ : -2 /*HC_E_HIP*/;
+// machine.  Returns 0 when `site` is not the one set.
+inline int injected_failure(int64_t site) {
+  const int64_t v = knob(kKnobInject);
+  if ((v & 15) != site) return 0;
+  return (v & kInjectNomem) ? -4 /*HC_E_NOMEM*/ : -2 /*HC_E_HIP*/;
 }
 
+// A GPU batch failure the host entries (AddCRCsToData, ReadFromDisk, WAL
+// replay) finish on the host path: no gfx950, a device or pinned allocation
+// failure, a HIP runtime error.  Any other code (HC_E_ARG, HC_E_LAYOUT: a
+// caller or library bug) is returned, never hidden behind the host path.
+inline bool gpu_batch_failure(int rc) { return rc == -3 /*HC_E_NODEV*/ || rc == -4 /*HC_E_NOMEM*/ || rc == -2 /*HC_E_HIP*/; }
+
 // HC_FORCE_GPU=1 routes the single-buffer drop-ins through the GPU batch path
-// too (read per call so tests can toggle it).
-inline int force_gpu() { return env_int("HC_FORCE_GPU", 0); }
+// too, and returns a failed GPU batch instead of finishing it on the host.
+inline int force_gpu() { return (int)knob(kKnobForceGpu); }
 
 // A process-wide pool of worker threads behind parallel_for.  Spawning and
 // joining threads per call cost 200-400 us per host batch on the GPU box
@@ -61,8 +130,8 @@ inline int force_gpu() { return env_int("HC_FORCE_GPU", 0); }
 // on its GPU path, 30 us for the batched verify that spawns none), which set
 // the GPU/host crossover of the host entries at thousands of blocks.
 //
-// A job is n tasks fn(0..n-1).  The caller posts it and takes tasks itself;
-// idle workers take the others.  The caller then unposts the job and waits
+// A job is n tasks fn(0..n-1).  The caller posts it, runs task 0 itself and
+// then takes further tasks; idle workers take the others.  The caller then unposts the job and waits
 // until every worker that took it has finished: it only ever waits for tasks
 // that are running, so a parallel_for inside a task (a worker posting its own
 // job) cannot deadlock, even with every worker busy -- the poster then runs
@@ -81,6 +150,7 @@ class TaskPool {
     j.n = n;
     j.call = [](void *f, int t) { (*static_cast<F *>(f))(t); };
     j.fn = &fn;
+    j.next.store(1, std::memory_order_relaxed);  // task 0 is the caller's (below)
     {
       std::lock_guard<std::mutex> lk(mu_);
       q_.push_back(&j);
@@ -92,6 +162,7 @@ class TaskPool {
       }
     }
     cv_.notify_all();
+    j.call(j.fn, 0);  // the caller runs task 0 itself: callers put the GPU batch there (thread-local launch info)
     for (int t; (t = j.next.fetch_add(1, std::memory_order_relaxed)) < n;) j.call(j.fn, t);
     std::unique_lock<std::mutex> lk(mu_);
     for (size_t k = 0; k < q_.size(); k++)

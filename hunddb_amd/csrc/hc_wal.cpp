@@ -15,7 +15,8 @@
 //      output capacity) -- O(ranges), plus one walk over the records of the
 //      range where a stop falls.
 //   C. per range (T threads): write rec_off/rec_len and copy the bytes out.
-// The verify batch runs on the calling thread meanwhile (GPU from 256 blocks);
+// The verify batch runs on the calling thread meanwhile (GPU from 1024 blocks,
+// HC_WAL_GPU_MIN_BLOCKS);
 // the result is cut where the Go loop would have stopped: at the first bad block.
 #include <algorithm>
 #include <chrono>
@@ -179,12 +180,12 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
   if (start_block >= nblocks) return HC_OK;
   const uint64_t n = nblocks - start_block;
   const uint8_t *base = blocks + start_block * bs;
-  const uint64_t gpu_min = (uint64_t)env_int("HC_WAL_GPU_MIN_BLOCKS", (int)kWalGpuMinBlocks);  // per call: tools/crossover.py
+  const uint64_t gpu_min = (uint64_t)knob(kKnobWalGpuMin);  // hc_debug_set: tools/crossover.py
   static const int threads_cfg = std::max(1, env_int("HC_WAL_THREADS", 16));  // 16: the GPU box's CPU share
   static const int trace = env_int("HC_WAL_TRACE", 0);
   // blocks per range at least HC_WAL_MIN_RANGE (64; read per call so tests can
   // force many small ranges and exercise the cross-range merge)
-  const uint64_t min_range = (uint64_t)std::max(1, env_int("HC_WAL_MIN_RANGE", 64));
+  const uint64_t min_range = (uint64_t)std::max<int64_t>(1, knob(kKnobWalMinRange));
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads_cfg, n / min_range));
   const bool have_out = rec_buf && rec_off && rec_len;
   int64_t first_bad = -1;
@@ -201,13 +202,13 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
     if (role == 0) {
       bool on_gpu = false;
       if (n >= gpu_min || force_gpu()) {
-        const int inj = injected_failure("wal_replay");
+        const int inj = injected_failure(kInjectWalReplay);
         vrc = inj ? inj : hc_verify_blocks(base, nullptr, nullptr, bs, block_size, n, nullptr, &first_bad);
         if (vrc >= 0) {  // HC_OK or the first bad block's reason
           on_gpu = true;
           vrc = HC_OK;
           g_stats.wal_gpu.fetch_add(1, std::memory_order_relaxed);
-        } else if (!force_gpu()) {
+        } else if (!force_gpu() && gpu_batch_failure(vrc)) {
           // recovery fails only on a bad block or a framing error (wal.go:362-455):
           // a GPU batch that cannot run finishes on the host path
           if (vrc == HC_E_NODEV) {
@@ -219,7 +220,7 @@ int hc_wal_replay_v(const uint8_t *blocks, uint64_t nblocks, uint32_t block_size
           vrc = HC_OK;
           first_bad = -1;
         } else {
-          on_gpu = true;  // HC_FORCE_GPU: the error is returned
+          on_gpu = true;  // HC_FORCE_GPU, or a caller / library error: returned
         }
       }
       if (!on_gpu)

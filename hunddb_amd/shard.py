@@ -99,42 +99,124 @@ def free_port() -> int:
     return p
 
 
-def spawn_ranks(cmd, nproc: int, port: int = 0, env=None, timeout=None) -> int:
+PHASE_ENV = "HC_RANK_PHASE_DIR"  # set by launch_ranks: where each rank records its phase
+
+
+def report_phase(phase: str, error=None) -> None:
+    """Rank side: record this rank's current phase (and, on failure, its error)
+    in $HC_RANK_PHASE_DIR/rank<RANK>.json, so the launching parent can name
+    the phase a hung or failed rank was in.  A no-op outside launch_ranks."""
+    import json
+    import time
+
+    d = os.environ.get(PHASE_ENV)
+    if not d:
+        return
+    r = int(os.environ.get("RANK", "0"))
+    path = os.path.join(d, f"rank{r}.json")
+    with open(path + ".tmp", "w") as f:
+        json.dump({"rank": r, "phase": phase, "t": time.time(), "pid": os.getpid(), "error": error}, f)
+    os.replace(path + ".tmp", path)  # the parent never reads a half-written file
+
+
+def _read_phases(d, nproc):
+    import json
+
+    out = {}
+    for r in range(nproc):
+        try:
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                out[r] = json.load(f)
+        except (OSError, ValueError):
+            out[r] = None
+    return out
+
+
+def launch_ranks(cmd, nproc: int, port: int = 0, env=None, timeout=None, grace: float = 5.0):
     """Start `nproc` copies of `cmd` (argv list), one per GPU, with the
     torch.distributed.run environment (RANK, LOCAL_RANK, WORLD_SIZE,
-    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for them.
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) plus
+    HC_RANK_PHASE_DIR, and wait for them -- at most `timeout` seconds.
 
     The caller must not have touched the GPU (children are started with
-    subprocess, never by exec).  If a rank fails, the others are terminated.
-    Returns 0, or the first non-zero exit status."""
+    subprocess, never by exec).  When a rank exits non-zero, or the deadline
+    passes, every rank still running is terminated (killed after `grace`
+    seconds).  Returns (rc, report): rc 0, the first failing rank's exit
+    status, or 124 at the deadline; report None on success, else {"reason":
+    "rank_failed" | "timeout", "failed": [{rank, rc, phase, error}], "alive":
+    [{rank, phase, phase_age_s}] (the ranks still running when it ended),
+    "elapsed_s"}."""
+    import shutil
     import subprocess
+    import tempfile
     import time
 
     port = port or free_port()
     base = dict(os.environ if env is None else env)
+    pdir = tempfile.mkdtemp(prefix="hc_ranks_")
     procs = []
     for r in range(nproc):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
-                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **{PHASE_ENV: pdir})
         procs.append(subprocess.Popen(cmd, env=e))
-    t0, rc = time.monotonic(), 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            r = p.poll()
-            if r is None:
-                continue
-            live.remove(p)
-            if r != 0 and rc == 0:
-                rc = r
-                for q in live:
-                    q.terminate()
-        if timeout is not None and time.monotonic() - t0 > timeout and live:
-            for q in live:
-                q.kill()
-            rc = rc or 124
-        time.sleep(0.05)
-    return rc
+    t0, rc, reason = time.monotonic(), 0, None
+    failed, alive = [], []
+    live = dict(enumerate(procs))
+    try:
+        while live:
+            for r, p in list(live.items()):
+                code = p.poll()
+                if code is None:
+                    continue
+                del live[r]
+                if code != 0:
+                    failed.append((r, code))
+            if failed and live:
+                reason = "rank_failed"
+            elif timeout is not None and live and time.monotonic() - t0 > timeout:
+                reason = "timeout"
+            if reason and live:  # name the survivors' phases, then end them
+                now = time.time()
+                ph = _read_phases(pdir, nproc)
+                alive = [{"rank": r, "phase": (ph[r] or {}).get("phase"),
+                          "phase_age_s": None if not ph[r] else round(now - ph[r]["t"], 1)} for r in sorted(live)]
+                for p in live.values():
+                    p.terminate()
+                t1 = time.monotonic()
+                while any(p.poll() is None for p in live.values()) and time.monotonic() - t1 < grace:
+                    time.sleep(0.05)
+                for p in live.values():
+                    if p.poll() is None:
+                        p.kill()
+                    p.wait()
+                live = {}
+                break
+            time.sleep(0.05)
+        if failed and reason is None:
+            reason = "rank_failed"
+        if reason is None:
+            return 0, None
+        ph = _read_phases(pdir, nproc)
+        # the first rank to fail is usually the cause (its peers then fail on the
+        # closed connection): order by the time each recorded its last phase
+        failed.sort(key=lambda rc_: (ph[rc_[0]] or {}).get("t", float("inf")))
+        rc = failed[0][1] if failed and reason == "rank_failed" else 124
+        return rc, {"reason": reason, "elapsed_s": round(time.monotonic() - t0, 1),
+                    "failed": [{"rank": r, "rc": c, "phase": (ph[r] or {}).get("phase"),
+                                "error": (ph[r] or {}).get("error")} for r, c in failed],
+                    "alive": alive}
+    finally:
+        for p in procs:  # (an exception in the parent: no orphaned ranks)
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        shutil.rmtree(pdir, ignore_errors=True)
+
+
+def spawn_ranks(cmd, nproc: int, port: int = 0, env=None, timeout=None) -> int:
+    """launch_ranks without the report: 0, the first failing rank's exit
+    status, or 124 at the deadline."""
+    return launch_ranks(cmd, nproc, port=port, env=env, timeout=timeout)[0]
 
 
 def rank_identity(device=None, kernel_ms=None) -> dict:

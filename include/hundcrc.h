@@ -58,7 +58,10 @@ extern "C" {
 /* library errors */
 #define HC_E_ARG -1     /* invalid argument (null pointer, bad size, capacity too small) */
 #define HC_E_HIP -2     /* a HIP runtime call failed */
-#define HC_E_NODEV -3   /* no usable gfx950 device: the GPU path fails loudly, never falls back */
+#define HC_E_NODEV -3   /* no usable gfx950 device: the batched and device entries fail loudly, never
+                         * fall back; the three entries that replace a reference function that cannot
+                         * fail there -- hc_add_crcs, hc_read_from_disk[_v], hc_wal_replay[_v] -- finish
+                         * on the host path instead (as on HC_E_NOMEM / HC_E_HIP; counted in hc_stats) */
 #define HC_E_NOMEM -4   /* device or pinned allocation failed */
 #define HC_E_LAYOUT -5  /* device batch violated the layout contract (see hc_dev_*) */
 
@@ -329,11 +332,21 @@ int hc_last_launch(hc_launch_info *info);
  * into out (returns HC_OK) or, if cap is too small, return its size. */
 int hc_debug_tables(void *out, size_t cap);
 
-/* 1 if this thread's last device batch of packed whole messages was hashed by
- * the packed-record stream (k_seg_*), 0 if it fell back to
- * k_crc_any on the device or was not offered to the stream; synchronizes that
- * device (tests and tools only). */
+/* 1 if this thread's last device batch of whole messages was hashed by the
+ * packed-record stream (k_seg_*) as records back to back, 2 if
+ * as sorted records with gaps between them, 0 if it fell back to k_crc_any on
+ * the device or was not offered to the stream; synchronizes that device
+ * (tests and tools only). */
 int hc_debug_seg_taken(void);
+
+/* The library reads its HC_* settings from the environment once, at the first
+ * call that needs one (a getenv racing with a Go os.Setenv would be a data
+ * race): HC_DEVICE, HC_SEG_MIN_MSGS, HC_COPY_THREADS, HC_WAL_MIN_RANGE,
+ * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
+ * HC_FORCE_GPU, HC_INJECT_FAIL.  hc_debug_set changes one of them afterwards
+ * (tests and tools); value NULL restores the compiled default.  HC_OK, or
+ * HC_E_ARG for an unknown name. */
+int hc_debug_set(const char *name, const char *value);
 
 /* Number of visible gfx950 devices (0 if none; never initialises a context
  * on a machine without GPUs). */

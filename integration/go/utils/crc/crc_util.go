@@ -260,7 +260,7 @@ type WalWindow struct {
 // WalReplay is one window of WAL recovery (row f3; wal.go:362-455 minus the
 // file I/O and the memtable): blocks holds written WAL blocks of blockSize
 // bytes back to back, parsing starts at startOffset of the first block.  Every
-// block is verified in one batch (GPU from 256 blocks), then FULL payloads and
+// block is verified in one batch (GPU from 1024 blocks, DESIGN.md 5.2), then FULL payloads and
 // reassembled FIRST/MIDDLE/LAST fragments come back in order as slices of one
 // buffer.  A bad block ("CRC mismatch in block") or a framing error ("unknown
 // fragment type", or a header/payload past its block where Go panics) returns

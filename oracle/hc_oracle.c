@@ -382,6 +382,37 @@ void oc_fill_block(uint64_t seed, uint64_t block, uint8_t *dst, size_t len) {
   }
 }
 
+/* Blocks first .. first+n-1 of a uniform batch (block_bytes each) into dst,
+ * on nthreads threads: the host copy of what hc_dev_fill_range writes, for
+ * full-size checks that regenerate a batch by index instead of copying it
+ * back from the device. */
+typedef struct {
+  uint64_t seed, first, n, bytes;
+  uint8_t *dst;
+  size_t *next;
+} fill_job_t;
+
+static void *run_fill(void *arg) {
+  fill_job_t *j = (fill_job_t *)arg;
+  for (;;) {
+    size_t lo = __atomic_fetch_add(j->next, OC_CHUNK, __ATOMIC_RELAXED);
+    if (lo >= j->n) break;
+    size_t hi = lo + OC_CHUNK < j->n ? lo + OC_CHUNK : j->n;
+    for (size_t i = lo; i < hi; i++) oc_fill_block(j->seed, j->first + i, j->dst + i * j->bytes, j->bytes);
+  }
+  return NULL;
+}
+
+void oc_fill_blocks_mt(uint64_t seed, uint64_t first, uint64_t n, uint64_t block_bytes, uint8_t *dst, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  size_t next = 0;
+  fill_job_t j = {seed, first, n, block_bytes, dst, &next};
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, run_fill, &j);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
 uint32_t oc_mixed_size(uint64_t seed, uint64_t block) {
   /* word index 2^21-1 is never a data word of a <=16 MiB block */
   uint64_t r = oc_splitmix64(seed ^ 0x5A5A5A5A5A5A5A5Aull, block, (1u << 21) - 1);

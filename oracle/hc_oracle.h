@@ -86,6 +86,8 @@ void oc_crc32_messages(const uint8_t *base, const uint64_t *off, const uint32_t 
 uint64_t oc_splitmix64(uint64_t seed, uint64_t block, uint64_t word);
 /* fill len bytes (len % 8 == 0) of block `block` */
 void oc_fill_block(uint64_t seed, uint64_t block, uint8_t *dst, size_t len);
+/* blocks first .. first+n-1 of a uniform batch, on nthreads threads */
+void oc_fill_blocks_mt(uint64_t seed, uint64_t first, uint64_t n, uint64_t block_bytes, uint8_t *dst, int nthreads);
 /* block size of block i of the mixed 4/8/16 KiB batch (config 3) */
 uint32_t oc_mixed_size(uint64_t seed, uint64_t block);
 

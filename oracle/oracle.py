@@ -37,6 +37,7 @@ def lib():
             ("oc_crc32_blocks", None, [P, P, P, U64, U32, P, S, I]),
             ("oc_crc32_messages", None, [P, P, P, P, S, I]),
             ("oc_splitmix64", U64, [U64, U64, U64]), ("oc_fill_block", None, [U64, U64, P, S]),
+            ("oc_fill_blocks_mt", None, [U64, U64, U64, U64, P, I]),
             ("oc_mixed_size", U32, [U64, U64]),
             ("oc_wal_frame", U64, [U64, P, U64, U32, P, U64, I, P, P]),
             ("oc_wal_record_size", U32, [U64, U64, U32, U32]),
@@ -100,6 +101,16 @@ def fill_blocks(seed, n, size=None, sizes=None):
     for i in range(len(sizes)):
         L.oc_fill_block(seed, i, base + int(off[i]), int(sizes[i]))
     return buf, off, sizes
+
+
+def fill_range(seed, first, n, block_bytes, out=None, threads=16):
+    """Blocks first .. first+n-1 of a uniform synthetic batch (the bytes
+    hc_dev_fill_range writes for them), regenerated on the host by index."""
+    if out is None:
+        out = np.empty(n * block_bytes, dtype=np.uint8)
+    assert out.size >= n * block_bytes and out.flags.c_contiguous
+    lib().oc_fill_blocks_mt(seed, first, n, block_bytes, _p(out), threads)
+    return out
 
 
 def mixed_sizes(seed, n):

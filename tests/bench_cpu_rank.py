@@ -28,9 +28,13 @@ def main():
     from hunddb_amd import shard
     from oracle import oracle as O
 
+    import datetime
     args = bench.parse(sys.argv[1:])
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench.phase("init")
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=args.rank_timeout))
+    bench.phase("fill")
     n, B = args.blocks, 4096
     lo, hi = shard.index_range(n, world, rank)
     counts = [shard.index_range(n, world, r)[1] - shard.index_range(n, world, r)[0] for r in range(world)]
@@ -38,10 +42,12 @@ def main():
     buf = np.empty((hi - lo) * B, dtype=np.uint8)
     for j, i in enumerate(range(lo, hi)):  # global block index, as hc_dev_fill_range
         L.oc_fill_block(bench.SEED, i, buf.ctypes.data + j * B, B)
+    bench.phase("timed")
     dist.barrier()
     t0 = time.perf_counter()
     local = O.crc32_blocks(buf, stride=B, ulen=B)
     dt = time.perf_counter() - t0
+    bench.phase("gather")
     proof = shard.device_proof(shard.gather_identities(shard.rank_identity(None, dt * 1e3)), "gloo")
     dt, _, tot = shard.job_timing(dt, dt, float(buf.size))
     got = shard.gather_crcs(torch.from_numpy(local.view(np.int32)), counts)
@@ -54,8 +60,11 @@ def main():
         print(json.dumps({"n_gpus": world, "scaling": "strong", "blocks_total": n, "counts": counts,
                           "bytes": tot, "words_match_1proc": same, "value": tot / dt / 2**30,
                           "multi_gpu": proof}), flush=True)
+    bench.phase("done")
     dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    import bench as _b
+    _b.main = main  # bench._run's error handling around this rank's flow
+    _b._run()

@@ -37,11 +37,46 @@ GPU_TEST_THRESHOLDS = {"HC_ADD_CRCS_GPU_MIN_BLOCKS": "256", "HC_READ_GPU_MIN_BLO
                        "HC_WAL_GPU_MIN_BLOCKS": "256"}
 
 
+class Knobs:
+    """The library's HC_* settings for one test.  libhundcrc reads them from
+    the environment once, at first use (hc_util.hpp: a getenv racing with a Go
+    os.Setenv would be a data race), so a test changes them through
+    hc_debug_set -- and in the environment too, for the child processes it
+    starts -- and they return to the compiled defaults afterwards."""
+
+    def __init__(self, mp):
+        self._mp, self._names = mp, set()
+
+    def setenv(self, name, value):
+        from hunddb_amd import crc
+        self._mp.setenv(name, value)
+        crc.debug_set(name, value)
+        self._names.add(name)
+
+    def delenv(self, name, raising=False):
+        from hunddb_amd import crc
+        self._mp.delenv(name, raising=raising)
+        crc.debug_set(name, None)
+        self._names.add(name)
+
+    def restore(self):
+        from hunddb_amd import crc
+        for n in self._names:
+            crc.debug_set(n, None)
+
+
+@pytest.fixture
+def knobs(monkeypatch):
+    k = Knobs(monkeypatch)
+    yield k
+    k.restore()
+
+
 @pytest.fixture(autouse=True)
-def _gpu_test_thresholds(request, monkeypatch):
+def _gpu_test_thresholds(request, knobs):
     if request.node.get_closest_marker("gpu") is not None and not request.node.get_closest_marker("default_thresholds"):
         for k, v in GPU_TEST_THRESHOLDS.items():
-            monkeypatch.setenv(k, v)
+            knobs.setenv(k, v)
 
 
 @pytest.fixture(scope="session")

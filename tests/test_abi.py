@@ -264,38 +264,38 @@ def test_batch_entries_fail_loudly_without_gpu(hc):
         hc.verify_blocks(buf)
 
 
-def test_add_crcs_to_data_without_gpu(hc, oracle, monkeypatch):
+def test_add_crcs_to_data_without_gpu(knobs, hc, oracle, monkeypatch):
     """AddCRCsToData cannot fail in Go (crc_util.go:41-64): a multi-hundred-block
     input, a GPU batch on a gfx950 host, is CRC'd on the host path (hc_cpu.cpp)
     when no device exists -- byte-exact vs the oracle.  Under HC_FORCE_GPU (test
     mode) the missing device is an error instead."""
     if hc.device_count() > 0:
         pytest.skip("a gfx950 device is present")
-    monkeypatch.setenv("HC_ADD_CRCS_GPU_MIN_BLOCKS", "256")  # 301 blocks: a GPU batch
+    knobs.setenv("HC_ADD_CRCS_GPU_MIN_BLOCKS", "256")  # 301 blocks: a GPU batch
     rng = np.random.default_rng(300)
     src = rng.integers(0, 256, 4092 * 300 + 77, dtype=np.uint8).tobytes()
     out = hc.AddCRCsToData(src)
     want = np.zeros(len(out), dtype=np.uint8)
     assert oracle.lib().oc_add_crcs_to_data(src, len(src), want.ctypes.data) == len(out)
     assert bytes(out) == want.tobytes()
-    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    knobs.setenv("HC_FORCE_GPU", "1")
     with pytest.raises(hc.HundCRCError):
         hc.AddCRCsToData(src)
 
 
 @pytest.mark.parametrize("inject", ["add_crcs", "add_crcs:nomem"])
-def test_add_crcs_finishes_on_host_after_gpu_failure(hc, oracle, monkeypatch, inject):
+def test_add_crcs_finishes_on_host_after_gpu_failure(knobs, hc, oracle, monkeypatch, inject):
     """AddCRCsToData cannot fail in Go (crc_util.go:41-64),
     so a GPU batch that fails (HC_E_HIP, HC_E_NOMEM -- here simulated by
     HC_INJECT_FAIL before any device call) is finished on the host path from the
     framed output, byte-exact vs the oracle, and counted in hc_stats; under
     HC_FORCE_GPU the failure is returned instead.  Runs with or without a GPU."""
     rng = np.random.default_rng(301)
-    monkeypatch.setenv("HC_ADD_CRCS_GPU_MIN_BLOCKS", "256")  # 301 blocks: a GPU batch
+    knobs.setenv("HC_ADD_CRCS_GPU_MIN_BLOCKS", "256")  # 301 blocks: a GPU batch
     src = rng.integers(0, 256, 4092 * 300 + 77, dtype=np.uint8).tobytes()
     want = np.zeros(hc.hc_add_crcs_size_py(len(src)), dtype=np.uint8)
     assert oracle.lib().oc_add_crcs_to_data(src, len(src), want.ctypes.data) == len(want)
-    monkeypatch.setenv("HC_INJECT_FAIL", inject)
+    knobs.setenv("HC_INJECT_FAIL", inject)
     hc.stats_reset()
     out = hc.AddCRCsToData(src)
     assert bytes(out) == want.tobytes()
@@ -303,15 +303,15 @@ def test_add_crcs_finishes_on_host_after_gpu_failure(hc, oracle, monkeypatch, in
     assert st["add_crcs_gpu_fallback"] == 1 and st["add_crcs_gpu"] == 0 and st["add_crcs_host_nodev"] == 0
     assert st["last_fallback_error"] == (hc.HC_E_NOMEM if inject.endswith("nomem") else hc.HC_E_HIP)
     # a different site named: no injection, the call takes its normal path
-    monkeypatch.setenv("HC_INJECT_FAIL", "add_crcsX")
+    knobs.setenv("HC_INJECT_FAIL", "add_crcsX")
     hc.stats_reset()
     assert bytes(hc.AddCRCsToData(src)) == want.tobytes()
     st = hc.stats()
     assert st["add_crcs_gpu_fallback"] == 0
     assert st["add_crcs_gpu"] + st["add_crcs_host_nodev"] == 1
     assert st["add_crcs_host_nodev"] == (1 if hc.device_count() == 0 else 0)
-    monkeypatch.setenv("HC_INJECT_FAIL", inject)
-    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    knobs.setenv("HC_INJECT_FAIL", inject)
+    knobs.setenv("HC_FORCE_GPU", "1")
     with pytest.raises(hc.HundCRCError):
         hc.AddCRCsToData(src)
 
@@ -328,7 +328,7 @@ def test_add_crcs_small_outputs_stay_on_host(hc, oracle):
 
 
 @pytest.mark.parametrize("inject", ["", "read_from_disk", "read_from_disk:nomem"])
-def test_read_from_disk_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypatch, inject):
+def test_read_from_disk_gpu_batch_failure_finishes_on_host(knobs, hc, oracle, monkeypatch, inject):
     """ReadFromDisk (block_manager.go:189-242) fails only on I/O or a CRC
     mismatch: a verify batch above the GPU threshold that cannot run (no gfx950
     here, or a simulated HC_E_HIP / HC_E_NOMEM) verifies on the host path --
@@ -341,8 +341,8 @@ def test_read_from_disk_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypat
     for i in range(nb):
         hc.AddCRCToBlockData(img[i * B:(i + 1) * B])
     if inject:
-        monkeypatch.setenv("HC_INJECT_FAIL", inject)
-    monkeypatch.setenv("HC_READ_GPU_MIN_BLOCKS", "256")
+        knobs.setenv("HC_INJECT_FAIL", inject)
+    knobs.setenv("HC_READ_GPU_MIN_BLOCKS", "256")
     start, size = 4 + 7, nb * (B - 4) - 100
     for corrupt in (None, 201):
         view = img.copy()
@@ -362,7 +362,7 @@ def test_read_from_disk_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypat
             assert st["nodev_host"] == 1 and st["read_gpu"] == 0
         else:
             assert st["read_gpu"] == 1
-    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    knobs.setenv("HC_FORCE_GPU", "1")
     if inject or hc.device_count() == 0:
         with pytest.raises(hc.HundCRCError):
             hc.ReadFromDisk(img.tobytes(), B, start, size)

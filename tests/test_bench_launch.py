@@ -107,3 +107,48 @@ def test_spawn_ranks_propagates_failure():
                             "import os, sys, time; r = int(os.environ['RANK']); "
                             "time.sleep(0.2); sys.exit(7 if r == 1 else 0)"], 3)
     assert rc == 7
+
+
+def _launch(world, extra_args, env_extra, timeout):
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.self_launch(%r, %d, script=%r))"
+            % (ROOT, ["--blocks", "3001", "--gpus", str(world)] + extra_args, world,
+               os.path.join(ROOT, "tests", "bench_cpu_rank.py")))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra)
+    import time
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines, time.monotonic() - t0
+
+
+def test_self_launch_deadline_names_the_hung_rank():
+    """the first 8-GPU run gets a deadline.  World 4, rank 2
+    sleeps 120 s in its timed phase, --rank-timeout 20: the launcher kills the
+    ranks and prints ONE JSON error line naming the ranks still alive and their
+    last phase, and exits non-zero, within 30 s of the deadline's start."""
+    r, lines, dt = _launch(4, ["--rank-timeout", "20"], {"HC_BENCH_STALL": "2:timed:120"}, 120)
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["value"] is None and res["reason"] == "timeout" and res["n_gpus"] == 4
+    assert "deadline" in res["error"] and res["failed_ranks"] == []
+    alive = {a["rank"]: a for a in res["alive_ranks"]}
+    assert alive[2]["phase"] == "timed" and alive[2]["phase_age_s"] >= 10
+    assert set(alive) == {0, 1, 2, 3}  # the others wait for rank 2 in a collective
+    assert dt < 20 + 30, dt
+
+
+def test_self_launch_failed_rank_is_named():
+    """A rank that raises ends the job at once: its peers are killed, and the
+    one JSON line names the failed rank, its phase and its error."""
+    r, lines, dt = _launch(4, ["--rank-timeout", "120"], {"HC_BENCH_FAIL": "1:fill"}, 180)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["reason"] == "rank_failed" and res["value"] is None
+    first = res["failed_ranks"][0]
+    assert first["rank"] == 1 and first["phase"] == "error" and "HC_BENCH_FAIL at fill" in first["error"]
+    assert res["error"].startswith("rank 1")
+    assert dt < 90, dt

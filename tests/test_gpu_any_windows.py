@@ -2,9 +2,10 @@
 large batches, fewer (32 .. 1) when the batch has under 64 per wave, so every
 wave gets one.  Batch sizes around every window size, in block mode (off/len
 blocks k_crc_grp leaves to the sweep: 1 KiB and misaligned 4 KiB blocks, with
-a corrupt block found by verify) and whole-message mode with gaps (the stream
-does not take them: k_crc_any on the device flag), every word against the
-oracle (crc_util.go:15-17 / :88-100 per block)."""
+a corrupt block found by verify) and whole-message mode with gaps, out of
+order (the stream takes sorted gapped records since round 5; unsorted ones go
+to k_crc_any on the device flag), every word against the oracle
+(crc_util.go:15-17 / :88-100 per block)."""
 import numpy as np
 import pytest
 
@@ -63,6 +64,8 @@ def test_gapped_messages_all_window_sizes(cuda, hc, oracle, n):
     off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 3)  # gaps: not packed
     off += np.uint64(5)
     total = int(off[-1]) + int(lens[-1]) + 64
+    p = rng.permutation(n)  # out of order: the stream's fallback
+    off, lens = off[p], lens[p]
     host = rng.integers(0, 256, total, dtype=np.uint8)
     buf = torch.from_numpy(host).cuda()
     doff = torch.from_numpy(off.view(np.int64)).cuda()

@@ -82,13 +82,13 @@ def _dev(torch, a):
 
 
 @pytest.mark.parametrize("seed", range(N_CASES))
-def test_random_layout(cuda, hc, oracle, seed, monkeypatch):
+def test_random_layout(knobs, cuda, hc, oracle, seed, monkeypatch):
     torch = cuda
     kind, buf, off, lens, stride, ulen, n, lead = gen_case(1000 + seed)
     packed = kind == "messages" and n > 1 and bool(
         np.all(off[1:] == off[:-1] + lens[:-1].astype(np.uint64)))
     if packed and seed % 2:
-        monkeypatch.setenv("HC_SEG_MIN_MSGS", "1")  # the packed-record stream on a small batch
+        knobs.setenv("HC_SEG_MIN_MSGS", "1")  # the packed-record stream on a small batch
     want = _words(oracle, kind, buf[lead:], off, lens, stride, ulen, n)
     flags = hc.HC_F_MESSAGES if kind == "messages" else 0
     # device entry

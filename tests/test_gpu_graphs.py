@@ -62,13 +62,13 @@ def test_graph_uniform_blocks_and_verify(cuda, hc, oracle):
 
 
 @pytest.mark.parametrize("packed", [False, True])
-def test_graph_messages(cuda, hc, oracle, monkeypatch, packed):
+def test_graph_messages(knobs, cuda, hc, oracle, monkeypatch, packed):
     """Whole messages offered to the packed-record stream (the default at any
     batch size: the k_seg_* dispatch captured, workspace allocated inside the
-    graph): packed ones taken by the stream, ones with gaps by k_crc_any on the
-    device flag."""
+    graph): packed ones and sorted ones with gaps taken by the stream, the
+    gapped ones in an order the stream refuses by k_crc_any on the device flag."""
     torch = cuda
-    monkeypatch.delenv("HC_SEG_MIN_MSGS", raising=False)
+    knobs.delenv("HC_SEG_MIN_MSGS", raising=False)
     rng = np.random.default_rng(2 + packed)
     n = 5000
     lens = rng.integers(64, 9000, n).astype(np.uint64)
@@ -77,6 +77,9 @@ def test_graph_messages(cuda, hc, oracle, monkeypatch, packed):
     off[1:] = np.cumsum((lens + gaps)[:-1], dtype=np.uint64)
     off += np.uint64(3)
     total = int(off[-1] + lens[-1]) + 64
+    if not packed:  # out of order (sorted gapped records are the stream's since round 5)
+        p = rng.permutation(n)
+        off, lens = off[p], lens[p]
     buf = torch.empty(total, dtype=torch.uint8, device="cuda")
     doff = torch.from_numpy(off.view(np.int64)).cuda()
     dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()

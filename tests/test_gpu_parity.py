@@ -428,13 +428,13 @@ def test_add_crcs_to_data_gpu(cuda, hc, oracle):
 
 
 @pytest.mark.default_thresholds
-def test_default_thresholds_route(cuda, hc, oracle, monkeypatch):
+def test_default_thresholds_route(knobs, cuda, hc, oracle):
     """The production GPU/host crossovers (hc_util.hpp): an
     AddCRCsToData output, a ReadFromDisk and a WAL replay just below their
     threshold run on the host path, at it as one GPU batch (hc_stats), each
     byte-exact vs the oracle."""
     for k in ("HC_ADD_CRCS_GPU_MIN_BLOCKS", "HC_READ_GPU_MIN_BLOCKS", "HC_WAL_GPU_MIN_BLOCKS"):
-        monkeypatch.delenv(k, raising=False)
+        knobs.delenv(k, raising=False)
     rng = np.random.default_rng(31)
     for nb, gpu in ((2047, False), (2048, True)):
         n = nb * 4092 - 100  # nb output blocks, the last one ragged
@@ -470,7 +470,7 @@ def test_default_thresholds_route(cuda, hc, oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("inject", ["", "add_crcs", "add_crcs:nomem"])
-def test_add_crcs_gpu_failure_finishes_on_host(cuda, hc, oracle, monkeypatch, inject):
+def test_add_crcs_gpu_failure_finishes_on_host(knobs, cuda, hc, oracle, monkeypatch, inject):
     """VERDICT r3 weak 3 on the box: with a gfx950 present the multi-block
     AddCRCsToData is one GPU batch (hc_stats add_crcs_gpu); a failing batch
     (HC_INJECT_FAIL: HC_E_HIP / HC_E_NOMEM) is finished on the host path,
@@ -481,7 +481,7 @@ def test_add_crcs_gpu_failure_finishes_on_host(cuda, hc, oracle, monkeypatch, in
     want = np.zeros(hc.lib().hc_add_crcs_size(n), dtype=np.uint8)
     assert oracle.lib().oc_add_crcs_to_data(src, n, want.ctypes.data) == len(want)
     if inject:
-        monkeypatch.setenv("HC_INJECT_FAIL", inject)
+        knobs.setenv("HC_INJECT_FAIL", inject)
     hc.stats_reset()
     out = hc.AddCRCsToData(src)
     assert bytes(out) == want.tobytes()
@@ -490,7 +490,7 @@ def test_add_crcs_gpu_failure_finishes_on_host(cuda, hc, oracle, monkeypatch, in
     if inject:
         assert st["add_crcs_gpu_fallback"] == 1 and st["add_crcs_gpu"] == 0
         assert st["last_fallback_error"] == (hc.HC_E_NOMEM if "nomem" in inject else hc.HC_E_HIP)
-        monkeypatch.setenv("HC_FORCE_GPU", "1")
+        knobs.setenv("HC_FORCE_GPU", "1")
         with pytest.raises(hc.HundCRCError):
             hc.AddCRCsToData(src)
     else:
@@ -521,7 +521,7 @@ def test_add_crcs_to_data_gpu_sources(cuda, hc, oracle, mem):
 
 
 @pytest.mark.parametrize("B", [4096, 8192, 5000])
-def test_read_from_disk_gpu_copyout_shapes(cuda, hc, oracle, monkeypatch, B):
+def test_read_from_disk_gpu_copyout_shapes(knobs, cuda, hc, oracle, monkeypatch, B):
     """ReadFromDisk's payload copy-out runs on HC_COPY_THREADS threads while the
     GPU batch verifies; every block's output position comes from a closed form.
     Odd start offsets, sizes ending mid-block, images shorter than the touched
@@ -529,7 +529,7 @@ def test_read_from_disk_gpu_copyout_shapes(cuda, hc, oracle, monkeypatch, B):
     rng = np.random.default_rng(B)
     img = _stamped_blocks(oracle, rng, 1200, B)
     for threads in ["1", "3"]:
-        monkeypatch.setenv("HC_COPY_THREADS", threads)
+        knobs.setenv("HC_COPY_THREADS", threads)
         for start, size, cut in [(0, 1100 * (B - 4) + 333, 0), (7, 1000 * (B - 4), 0), (B + 123, 900 * (B - 4) + 1, 0),
                                  (4, 1150 * (B - 4), B * 60 + 77)]:
             view = img[(start // B) * B:].tobytes()
@@ -544,8 +544,8 @@ def test_read_from_disk_gpu_copyout_shapes(cuda, hc, oracle, monkeypatch, B):
                 assert hc.last_bad_block() == wbad
 
 
-def test_force_gpu_dropins(cuda, hc, golden, monkeypatch):
-    monkeypatch.setenv("HC_FORCE_GPU", "1")
+def test_force_gpu_dropins(knobs, cuda, hc, golden, monkeypatch):
+    knobs.setenv("HC_FORCE_GPU", "1")
     assert hc.GetCRC(b"123456789") == 0xCBF43926
     for v in golden["known"]["vectors"]:
         if v["hex"] is not None:
@@ -967,8 +967,9 @@ def test_verify_every_block_bad(cuda, hc, path):
 
 def test_config4_full_size_sampled_and_sharded(cuda, hc, oracle):
     """configs[3] at full size on one GPU: 16M x 8 KiB = 131 GB resident.
-    The oracle re-generates 20k sampled blocks on the host (the fill is keyed by
-    block index) and checks their CRC words; the index-sharded launches of 8
+    The oracle re-generates ALL 16M blocks on the host by index (the fill is
+    keyed by block index; 16 threads, 1 GiB slices) and checks every CRC word
+    (crc_util.go:15-17,88-100); the index-sharded launches of 8
     ranks (hunddb_amd.shard.index_range, what bench.py --gpus 8 runs) give the
     same words as the whole batch; a stamp -> verify pass over all 131 GB finds
     exactly the blocks corrupted at far-apart indices (block offsets past 2^32
@@ -989,15 +990,15 @@ def test_config4_full_size_sampled_and_sharded(cuda, hc, oracle):
     torch.cuda.synchronize()
     assert torch.equal(whole, parts)
     got = u32(whole)
-    rng = np.random.default_rng(4)
-    idx = np.unique(np.concatenate([rng.integers(0, n, 20_000), [0, 1, n // 2, n - 2, n - 1]]))
-    host = np.empty(B, dtype=np.uint8)
-    L = oracle.lib()
-    want = np.empty(idx.size, dtype=np.uint32)
-    for k, i in enumerate(idx):
-        L.oc_fill_block(seed, int(i), host.ctypes.data, B)
-        want[k] = oracle.crc32_blocks(host, stride=B, ulen=B)[0]
-    assert np.array_equal(got[idx], want)
+    per = (1 << 30) // B  # blocks per 1 GiB host slice
+    host = np.empty(per * B, dtype=np.uint8)
+    for lo in range(0, n, per):
+        k = min(per, n - lo)
+        oracle.fill_range(seed, lo, k, B, out=host, threads=16)
+        want = oracle.crc32_blocks(host, stride=B, ulen=B, nblocks=k, threads=16)
+        bad = np.flatnonzero(got[lo:lo + k] != want)
+        assert bad.size == 0, (lo + bad[:8], got[lo + bad[:8]], want[bad[:8]])
+    del host
     # stamp all, corrupt a few far-apart blocks, verify all
     hc.dev_crc32_blocks(buf, None, stride=B, ulen=B, nblocks=n, flags=hc.HC_F_STAMP)
     victims = [524_289, 8_388_609, n - 1]  # byte offsets > 2^32, > 2^36, the last block

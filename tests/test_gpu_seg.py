@@ -2,8 +2,10 @@
 batch whose records lie back to back (config 5's per-record variant,
 crc_util.go:15-17 per record), hashed as ONE stream over the span, against the
 oracle's restatement of Go's crc32.ChecksumIEEE; and the device-side fallback
-to k_crc_any for batches the stream does not take (gaps, overlaps, unsorted,
-runs of records under 64 B)."""
+to k_crc_any for batches the stream does not take (overlaps, unsorted, runs of
+records under 64 B, gaps over a quarter of the payload).  Sorted records with
+gaps between them (round 5) are taken by the same stream over 2n events.
+`check(..., taken)`: "packed", "gapped" or None (k_crc_any)."""
 import numpy as np
 import pytest
 
@@ -27,12 +29,12 @@ def run(torch, hc, buf, off, lens):
     dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
     hc.dev_crc32_blocks(buf, out, nblocks=n, off=doff, lens=dlen, flags=hc.HC_F_MESSAGES)
     torch.cuda.synchronize()
-    return u32(out), hc.seg_taken()
+    return u32(out), hc.seg_mode()
 
 
 @pytest.fixture
-def seg_all(monkeypatch):
-    monkeypatch.setenv("HC_SEG_MIN_MSGS", "1")  # offer every message batch to the stream
+def seg_all(knobs, monkeypatch):
+    knobs.setenv("HC_SEG_MIN_MSGS", "1")  # offer every message batch to the stream
 
 
 def check(torch, hc, oracle, host, buf, off, lens, taken):
@@ -57,7 +59,7 @@ def test_seg_log_uniform_records(cuda, hc, oracle, seg_all, start):
     host = rng.integers(0, 256, total, dtype=np.uint8)
     buf = torch.from_numpy(host).cuda()
     assert int(off[-1] + lens[-1]) <= total
-    check(torch, hc, oracle, host, buf, off, lens, True)
+    check(torch, hc, oracle, host, buf, off, lens, "packed")
     assert "k_seg_stream" in hc.last_launch()["kernel"]
 
 
@@ -82,7 +84,7 @@ def test_seg_boundaries_and_shapes(cuda, hc, oracle, seg_all):
         for start in (0, 3, 1024 - 1):
             off = packed(lens, start)
             assert int(off[-1] + lens[-1]) <= total
-            check(torch, hc, oracle, host, buf, off, lens, True)
+            check(torch, hc, oracle, host, buf, off, lens, "packed")
 
 
 def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
@@ -97,29 +99,29 @@ def test_seg_falls_back_on_the_device(cuda, hc, oracle, seg_all):
     lens = rng.integers(64, 4000, 3000).astype(np.uint64)
     off = packed(lens, 5)
     g = off.copy()
-    g[1500:] += 1  # one byte gap
-    check(torch, hc, oracle, host, buf, g, lens, False)
+    g[1500:] += 1  # one byte gap: sorted, the gapped stream
+    check(torch, hc, oracle, host, buf, g, lens, "gapped")
     o = off.copy()
     o[700:] -= 1  # one byte overlap
-    check(torch, hc, oracle, host, buf, o, lens, False)
+    check(torch, hc, oracle, host, buf, o, lens, None)
     p = rng.permutation(len(off))
-    check(torch, hc, oracle, host, buf, off[p], lens[p], False)
+    check(torch, hc, oracle, host, buf, off[p], lens[p], None)
     dense = np.array([100, 0, 0, 200, 0, 64, 0] * 1000, dtype=np.uint64)  # empty records, dense
-    check(torch, hc, oracle, host, buf, packed(dense, 3), dense, False)
+    check(torch, hc, oracle, host, buf, packed(dense, 3), dense, None)
     small = np.full(5000, 63, dtype=np.uint64)  # 65 events in a 4 KiB group
-    check(torch, hc, oracle, host, buf, packed(small, 0), small, False)
+    check(torch, hc, oracle, host, buf, packed(small, 0), small, None)
     small[:] = 64  # exactly 64 per group: still the stream
-    check(torch, hc, oracle, host, buf, packed(small, 0), small, True)
+    check(torch, hc, oracle, host, buf, packed(small, 0), small, "packed")
     # 63 records and the span's end in the last group (64 events, no 65th): the stream
     edge = np.full(64 * 10 + 63, 64, dtype=np.uint64)
-    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, True)
+    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, "packed")
     # 64 records fill the last group exactly; the span's end opens the next one: the stream
     edge = np.full(64 * 10 + 64, 64, dtype=np.uint64)
-    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, True)
+    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, "packed")
     # 63 records of 64 B and one of 60 B (64 events), then the span's end in the same group
     # (the 65th event): the fallback
     edge = np.r_[np.full(64 * 10 + 63, 64), [60]].astype(np.uint64)
-    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, False)
+    check(torch, hc, oracle, host, buf, packed(edge, 0), edge, None)
 
 
 def test_seg_record_cap(cuda, hc, oracle, seg_all):
@@ -131,7 +133,7 @@ def test_seg_record_cap(cuda, hc, oracle, seg_all):
     total = 40 << 20
     host = rng.integers(0, 256, total, dtype=np.uint8)
     buf = torch.from_numpy(host).cuda()
-    for big, taken in [((1 << 24), True), ((1 << 24) + 1, False), ((1 << 24) - 3, True)]:
+    for big, taken in [((1 << 24), "packed"), ((1 << 24) + 1, None), ((1 << 24) - 3, "packed")]:
         lens = np.array([1000] * 300 + [big] + [777, 64, 5000] * 100, dtype=np.uint64)
         off = packed(lens, 9)
         assert int(off[-1] + lens[-1]) <= total
@@ -154,10 +156,10 @@ def test_seg_without_crc_out(cuda, hc, oracle, seg_all):
     torch.cuda.synchronize()
     assert not hc.seg_taken()
     assert hc.last_launch()["kernel"] == "k_crc_grp+k_crc_any"
-    check(torch, hc, oracle, host, buf, off, lens, True)  # the same batch with crc_out: the stream
+    check(torch, hc, oracle, host, buf, off, lens, "packed")  # the same batch with crc_out: the stream
 
 
-def test_seg_threshold(cuda, hc, oracle, monkeypatch):
+def test_seg_threshold(knobs, cuda, hc, oracle, monkeypatch):
     """By default every whole-message batch with crc_out is offered to the
     stream (it beats k_crc_grp + k_crc_any from 16 records up, profiles/r4/r4s,
     r4t); below HC_SEG_MIN_MSGS the batch is not offered."""
@@ -168,13 +170,13 @@ def test_seg_threshold(cuda, hc, oracle, monkeypatch):
     total = int(off[-1] + lens[-1])
     host = rng.integers(0, 256, total, dtype=np.uint8)
     buf = torch.from_numpy(host).cuda()
-    monkeypatch.delenv("HC_SEG_MIN_MSGS", raising=False)
-    check(torch, hc, oracle, host, buf, off, lens, True)
+    knobs.delenv("HC_SEG_MIN_MSGS", raising=False)
+    check(torch, hc, oracle, host, buf, off, lens, "packed")
     assert "k_seg_stream" in hc.last_launch()["kernel"]
     for n in (1, 2, 17):  # tiny batches at the default
-        check(torch, hc, oracle, host, buf, off[:n], lens[:n], True)
-    monkeypatch.setenv("HC_SEG_MIN_MSGS", "5001")
-    check(torch, hc, oracle, host, buf, off, lens, False)
+        check(torch, hc, oracle, host, buf, off[:n], lens[:n], "packed")
+    knobs.setenv("HC_SEG_MIN_MSGS", "5001")
+    check(torch, hc, oracle, host, buf, off, lens, None)
     assert hc.last_launch()["kernel"] == "k_crc_grp+k_crc_any"
 
 
@@ -192,7 +194,7 @@ def test_seg_config5b_size(cuda, hc, oracle):
     buf = torch.empty(total, dtype=torch.uint8, device="cuda")
     hc.dev_fill_range(buf, 0x5B, 0, total >> 20, stride=1 << 20, ulen=1 << 20)  # every byte, in 1 MiB blocks
     got, was = run(torch, hc, buf, off, lens)
-    assert was
+    assert was == "packed"
     # oracle on 20k records of the first 512 MB (all of the first 200)
     head = int(np.searchsorted(off, 512 << 20))
     pick = np.unique(np.r_[np.arange(200), rng.choice(head, 20_000, replace=False)])
@@ -200,15 +202,13 @@ def test_seg_config5b_size(cuda, hc, oracle):
     sample = buf[:hi].cpu().numpy()
     want = oracle.crc32_messages(sample, off[pick], lens[pick].astype(np.uint32), threads=16)
     assert (got[pick] == want).all()
-    # every word against k_crc_any: the same records with the last one moved one
-    # byte up (a gap: not packed, so the device flag sends it to k_crc_any)
-    g = off.copy()
-    g[-1] += 1
+    # every word against k_crc_any: the same records with the next-to-last one
+    # a byte longer (an overlap: the device flag sends the batch to k_crc_any)
     l3 = lens.copy()
-    l3[-1] -= 1
-    got3, was3 = run(torch, hc, buf, g, l3)
-    assert not was3
-    assert (got3[:-1] == got[:-1]).all()
+    l3[-2] += 1
+    got3, was3 = run(torch, hc, buf, off, l3)
+    assert was3 is None
+    assert (got3[:-2] == got[:-2]).all()
 
 
 def test_seg_workspace_streams(cuda, hc, oracle, seg_all):
@@ -265,11 +265,118 @@ lens = rng.integers(64, 3000, n).astype(np.uint64)
 off = T.packed(lens, 3)
 host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
 buf = torch.from_numpy(host).cuda()
-T.check(torch, hc, O, host, buf, off, lens, True)
-g = off.copy(); g[n - 700:] += np.uint64(1)  # a gap near the end: the last strides
-T.check(torch, hc, O, host, buf, g, lens, False)
+T.check(torch, hc, O, host, buf, off, lens, "packed")
+o = lens.copy(); o[n - 700] += 1  # an overlap near the end: the last strides
+T.check(torch, hc, O, host, buf, off, o, None)
+g = off.copy(); g[n - 700:] += np.uint64(1)  # a gap near the end: still sorted
+T.check(torch, hc, O, host, buf, g, lens, "gapped")
 print("ok")
 """
     env = dict(os.environ, HC_SEG_PLAN_WGS=str(plan_wgs), HC_SEG_MIN_MSGS="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+def expected_mode(base, off, lens):
+    """The plan's decision (k_seg_plan + k_seg_stream's prologue) restated:
+    "packed" when every record starts where the previous one ends and no 4 KiB
+    group (from the span's 1 KiB-aligned origin) holds 65 of the n + 1 events;
+    else "gapped" when the records are sorted and do not overlap, no group holds
+    65 of the 2n events s_j, e_j, and the gap bytes are at most a quarter of the
+    payload; else None (k_crc_any)."""
+    s = np.uint64(base) + off.astype(np.uint64)
+    e = s + lens.astype(np.uint64)
+    pend = int(e[-1])
+    a0 = int(s[0]) & ~1023
+    if (lens > (1 << 24)).any() or int(s.min()) < a0 or int(e.max()) > pend:
+        return None
+
+    def dense(ev):
+        g = (ev - np.uint64(a0)) >> np.uint64(12)
+        return len(ev) > 64 and bool((g[64:] == g[:-64]).any())
+    if (s[1:] == e[:-1]).all() and not dense(np.r_[s, np.uint64(pend)]):
+        return "packed"
+    if (s[1:] >= e[:-1]).all():
+        ev = np.empty(2 * len(s), dtype=np.uint64)
+        ev[0::2], ev[1::2] = s, e
+        gaps = int((s[1:] - e[:-1]).sum()) if len(s) > 1 else 0
+        if not dense(ev) and 4 * gaps <= int(lens.astype(np.uint64).sum()):
+            return "gapped"
+    return None
+
+
+def gapped(lens, gaps, start):
+    """Records in order with gaps[j] bytes before record j (j > 0)."""
+    off = np.zeros(len(lens), dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[1:].astype(np.uint64), dtype=np.uint64)
+    return off + np.uint64(start)
+
+
+@pytest.mark.parametrize("start", [0, 5, 1023, 4093, 16384 - 17])
+def test_seg_gapped_wal_records(cuda, hc, oracle, seg_all, start):
+    """Config 5's record law with a 17-B gap before every record (the WAL header
+    of /root/reference/lsm/wal/wal_header.go:5-23 sits between payloads): taken
+    by the stream over the 2n record boundaries, bit-exact against the oracle's
+    ChecksumIEEE of each record (crc_util.go:15-17)."""
+    torch = cuda
+    rng = np.random.default_rng(start + 77)
+    n = 20_000
+    lens = (64.0 * np.exp(rng.random(n) * np.log(1024.0))).astype(np.uint64)
+    off = gapped(lens, np.full(n, 17, dtype=np.uint64), start)
+    total = int(off[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    assert expected_mode(buf.data_ptr(), off, lens) == "gapped"
+    check(torch, hc, oracle, host, buf, off, lens, "gapped")
+    assert "k_seg_stream" in hc.last_launch()["kernel"]
+
+
+def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
+    """Gapped batches of every shape, each against the oracle and against the
+    restated decision: random gaps with zeros among them (records that touch),
+    empty records, records ending on row / group / unit boundaries, one 12 MB
+    record, one and two records, gaps of whole units, gaps just under and just
+    over a quarter of the payload, dense small records at the 64-event limit,
+    an overlap and an unsorted batch (both k_crc_any)."""
+    torch = cuda
+    rng = np.random.default_rng(99)
+    total = 64 << 20
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    cases = []
+    lens = rng.integers(64, 5000, 4000).astype(np.uint64)
+    gaps = rng.integers(0, 40, 4000).astype(np.uint64)
+    gaps[rng.random(4000) < 0.3] = 0
+    cases.append((lens, gaps))
+    cases.append((np.array([3000, 0, 0, 2000, 0, 64, 0] * 700, dtype=np.uint64),
+                  np.array([5, 0, 7, 1, 0, 0, 9] * 700, dtype=np.uint64)))
+    cases.append((np.array([1024 - 17, 4096 - 17, 16384 - 17] * 600, dtype=np.uint64), np.full(1800, 17, np.uint64)))
+    cases.append((np.array([12_345_678], dtype=np.uint64), np.zeros(1, np.uint64)))
+    cases.append((np.array([64, 65], dtype=np.uint64), np.array([0, 3], dtype=np.uint64)))
+    cases.append((np.array([1 << 20] * 10, dtype=np.uint64), np.array([0] + [16384] * 9, dtype=np.uint64)))
+    L = rng.integers(1000, 3000, 3000).astype(np.uint64)
+    q = int(L.sum()) // 4
+    g = np.zeros(3000, dtype=np.uint64)
+    g[1:] = q // 2999
+    cases.append((L, g))                            # just under a quarter: gapped
+    g2 = g.copy()
+    g2[1:1 + (q - int(g.sum())) + 1] += 1           # one byte over a quarter: k_crc_any
+    cases.append((L, g2))
+    small = np.full(5000, 120, dtype=np.uint64)      # 32 records + 8-B gaps per 4 KiB: 64 events a group
+    cases.append((small, np.full(5000, 8, np.uint64)))
+    small2 = np.full(5000, 100, dtype=np.uint64)     # 34 records per group: 68 events, k_crc_any
+    cases.append((small2, np.full(5000, 20, np.uint64)))
+    for lens, gaps in cases:
+        for start in (0, 3, 1024 - 1):
+            off = gapped(lens, gaps, start)
+            assert int(off[-1] + lens[-1]) <= total
+            check(torch, hc, oracle, host, buf, off, lens, expected_mode(buf.data_ptr(), off, lens))
+    seen = {expected_mode(buf.data_ptr(), gapped(a, b, 0), a) for a, b in cases}
+    assert seen == {"packed", "gapped", None}, seen
+    lens, gaps = cases[0]
+    off = gapped(lens, gaps, 1)
+    o = lens.copy()
+    o[100] = off[101] - off[100] + 1  # record 100 overlaps 101 by one byte
+    check(torch, hc, oracle, host, buf, off, o, None)
+    p = rng.permutation(len(off))
+    check(torch, hc, oracle, host, buf, off[p], lens[p], None)

@@ -15,9 +15,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_concurrent_threads_share_the_device_slots(cuda, hc, oracle, monkeypatch):
+def test_concurrent_threads_share_the_device_slots(knobs, cuda, hc, oracle, monkeypatch):
     torch = cuda
-    monkeypatch.setenv("HC_SEG_MIN_MSGS", "1")  # every whole-message batch is offered to the stream
+    knobs.setenv("HC_SEG_MIN_MSGS", "1")  # every whole-message batch is offered to the stream
     rng = np.random.default_rng(404)
     n = 1500
     host = rng.integers(0, 256, n * 16384 + 8192, dtype=np.uint8)

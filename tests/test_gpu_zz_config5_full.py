@@ -12,8 +12,10 @@ the blocks starting where the WAL segment files put them.
   per-block check, wal.go:383) over the whole image: clean, then with one
   corrupted block found at its index with the reference's error text.
 - The per-record variant on the device: GetCRC of all 10M records packed back
-  to back in HBM (the packed-record stream), against the oracle on a sample and
-  word for word against k_crc_any.
+  to back in HBM (the packed-record stream), every word against the oracle
+  (the span copied back in 4 GiB segments); the same records with a 17-B WAL
+  header gap before each (the gapped stream), every word against the packed
+  run; and word for word against k_crc_any (an overlap forces the fallback).
 
 Host memory: ~108 GB (one image); the box allows ~270 GiB per command.
 
@@ -116,6 +118,25 @@ def test_config5_wal_blocks_full_size(cuda, hc, oracle):
         del host
 
 
+def oracle_all(buf, off, sizes, got, oracle, seg_cap=4 << 30):
+    """Every record's word against the oracle: the span back to the host in
+    segments of at most seg_cap bytes that end on record boundaries."""
+    n = len(off)
+    i = 0
+    while i < n:
+        lo = int(off[i])
+        j = max(i + 1, int(np.searchsorted(off, np.uint64(lo + seg_cap), side="left")))
+        while j > i + 1 and int(off[j - 1]) + int(sizes[j - 1]) > lo + seg_cap:
+            j -= 1
+        hi = int(off[j - 1]) + int(sizes[j - 1])
+        seg = buf[lo:hi].cpu().numpy()
+        want = oracle.crc32_messages(seg, off[i:j] - np.uint64(lo), sizes[i:j], threads=16)
+        bad = np.flatnonzero(got[i:j] != want)
+        assert bad.size == 0, (i + bad[:8])
+        del seg
+        i = j
+
+
 def test_config5_records_full_size_on_device(cuda, hc, oracle):
     torch = cuda
     walgen = _walgen()
@@ -124,10 +145,11 @@ def test_config5_records_full_size_on_device(cuda, hc, oracle):
     off = np.zeros(NREC, dtype=np.uint64)
     off[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
     off += np.uint64(3)  # back to back from an odd address
-    total = (int(off[-1]) + int(sizes[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
+    gp = off + np.arange(NREC, dtype=np.uint64) * np.uint64(17)  # the gapped layout (below)
+    total = (int(gp[-1]) + int(sizes[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
     assert total > 90e9
     require_device_bytes(torch, total + NREC * 16 + (2 << 30))
-    require_host_bytes((4 << 30))  # the sampled segments copied back for the oracle
+    require_host_bytes((6 << 30))  # the 4 GiB segments copied back for the oracle
     buf = torch.empty(total, dtype=torch.uint8, device="cuda")
     hc.dev_fill_range(buf, 0x5C, 0, total >> 20, stride=1 << 20, ulen=1 << 20)  # every byte, in 1 MiB blocks
     doff = torch.from_numpy(off.view(np.int64)).cuda()
@@ -135,30 +157,26 @@ def test_config5_records_full_size_on_device(cuda, hc, oracle):
     out = torch.empty(NREC, dtype=torch.int32, device="cuda")
     hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=NREC, flags=hc.HC_F_MESSAGES)
     torch.cuda.synchronize()
-    assert hc.seg_taken(), "10M packed records should take the packed-record stream"
+    assert hc.seg_mode() == "packed", "10M packed records should take the packed-record stream"
     got = out.cpu().numpy().view(np.uint32).copy()
-    # the oracle on 20k records of the first 1 GB (every one of the first 300) and on the last 300
-    rng = np.random.default_rng(5)
-    head = int(np.searchsorted(off, 1 << 30))
-    pick = np.unique(np.r_[np.arange(300), rng.choice(head, 20_000, replace=False)])
-    hi = int((off[pick] + sizes[pick]).max())
-    want = oracle.crc32_messages(buf[:hi].cpu().numpy(), off[pick], sizes[pick], threads=16)
-    assert np.array_equal(got[pick], want)
-    tail = np.arange(NREC - 300, NREC)
-    lo = int(off[tail[0]])
-    seg = buf[lo:int(off[-1]) + int(sizes[-1])].cpu().numpy()
-    want = oracle.crc32_messages(seg, off[tail] - np.uint64(lo), sizes[tail], threads=16)
-    assert np.array_equal(got[tail], want)
-    # every word against k_crc_any: the last record moved one byte up is a gap,
-    # so the batch is not packed and the device flag sends it to k_crc_any
-    g = off.copy()
-    g[-1] += 1
+    # every record against the oracle, packed and gapped
+    oracle_all(buf, off, sizes, got, oracle)
+    # the same records with a 17-B gap before each (WAL headers between the
+    # payloads, wal_header.go:5-23): the stream over 2n events
+    doff.copy_(torch.from_numpy(gp.view(np.int64)))
+    hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=NREC, flags=hc.HC_F_MESSAGES)
+    torch.cuda.synchronize()
+    assert hc.seg_mode() == "gapped", "sorted records with 17-B gaps should take the gapped stream"
+    gotg = out.cpu().numpy().view(np.uint32).copy()
+    oracle_all(buf, gp, sizes, gotg, oracle)
+    # every word against k_crc_any: the gapped batch with record 0 one byte
+    # longer overlaps record 1 (17-B gap -> -1): the device flag sends it there;
+    # records 1.. are the gapped stream's words
     l2 = sizes.copy()
-    l2[-1] -= 1
-    doff.copy_(torch.from_numpy(g.view(np.int64)))
+    l2[0] += 18
     dlen.copy_(torch.from_numpy(l2.view(np.int32)))
     hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=NREC, flags=hc.HC_F_MESSAGES)
     torch.cuda.synchronize()
     assert not hc.seg_taken()
     got2 = out.cpu().numpy().view(np.uint32)
-    assert np.array_equal(got2[:-1], got[:-1])
+    assert np.array_equal(got2[1:], gotg[1:])

@@ -8,7 +8,8 @@ source (CPU: hipcc cross-compiles):
   rows behind it stay in flight);
 * k_seg_stream's row folds and window waits count exactly the VMEM ops issued
   after the load they wait for (vmcnt(6): three rows, the event window, the
-  group's two stores), and no loop-latch register copies wait for refills
+  group's two stores; vmcnt(7) in the gapped loop, whose window is two loads),
+  and no loop-latch register copies wait for refills
   (round 4 found hipcc copying the loop-carried rows at the latch after small
   unrelated edits; that shows as vmcnt(2)/vmcnt(3) waits before the header);
 * k_unframe has no readfirstlane (waterfall) loops around its buffer stores.
@@ -68,7 +69,7 @@ def test_no_scratch_anywhere(isa):
 
 def test_streaming_kernels_fit_four_waves_per_simd(isa):
     kernels, _ = isa
-    for key in ("k_crc_grp", "k_seg_stream", "k_crc_any", "k_crc_fast"):
+    for key in ("k_crc_grp", "k_seg_stream", "k_crc_any", "k_crc_fast", "k_seg_combine"):
         for name in _find(kernels, key):
             assert _field(kernels[name], "amdhsa_next_free_vgpr") <= 128, (name, key)
 
@@ -80,16 +81,31 @@ def test_crc_grp_folds_wait_for_their_row_only(isa):
         assert w.count(3) >= 3, (name, w)  # the row folds of the group loop
 
 
+def _stream_loops(body):
+    """(latch text before the loop, loop text) of every depth-1 loop whose body
+    refills rows (buffer_load_dwordx4 ... nt)."""
+    out = []
+    for m in re.finditer(r"^(\.LBB\d+_\d+):[ \t]*; =>This Loop Header: Depth=1\n", body, re.M):
+        h, label = m.start(), m.group(1)
+        back = [b.end() for b in re.finditer(rf"s_c?branch\w* {re.escape(label)}\n", body[h:])]
+        loop = body[h:h + back[-1]]  # to the last back edge
+        if re.search(r"buffer_load_dwordx4 .* nt", loop):
+            out.append((body[body.rfind("buffer_load_dwordx4", 0, h):h], loop))
+    return out
+
+
 def test_seg_stream_waits_are_exact(isa):
+    """Two stream loops (round 5): the gapped one, whose event window is two
+    loads (off[] and len[]), folds at vmcnt(7); the packed one at vmcnt(6)."""
     _, bodies = isa
     (name,) = _find(bodies, "k_seg_stream")
-    body = bodies[name]
-    header = body.index("; =>This Loop Header: Depth=1\n", body.index("buffer_load_dwordx4"))
-    loop = body[header:]
-    w = _waits(loop)
-    assert w.count(6) >= 5, w  # the window and the four row folds
-    latch = body[body.rfind("buffer_load_dwordx4", 0, header):header]
-    assert not re.search(r"s_waitcnt vmcnt\([0-5]\)", latch), "loop-latch copies wait for the refills"
+    loops = _stream_loops(bodies[name])
+    assert len(loops) == 2, len(loops)
+    for (latch, loop), exact in zip(loops, (7, 6)):  # source order: the gapped body is instantiated first
+        w = _waits(loop)
+        assert w.count(exact) >= 4, (exact, w)  # the four row folds
+        assert not [x for x in w if x < exact - 1], (exact, w)  # no wait drains a refill or the window
+        assert not re.search(rf"s_waitcnt vmcnt\([0-{exact - 1}]\)", latch), "loop-latch copies wait for the refills"
 
 
 def test_framing_kernels_have_no_waterfall_loops(isa):

@@ -15,10 +15,10 @@ from test_oracle import ERRS, _replay_case_blocks
 
 
 @pytest.fixture(params=[64, 3, 1], ids=["range64", "range3", "range1"])
-def ranges(request, monkeypatch):
+def ranges(knobs, request, monkeypatch):
     """Blocks per parallel range (HC_WAL_MIN_RANGE): 1 and 3 put range
     boundaries inside fragmented records, so the cross-range merge runs."""
-    monkeypatch.setenv("HC_WAL_MIN_RANGE", str(request.param))
+    knobs.setenv("HC_WAL_MIN_RANGE", str(request.param))
     return request.param
 
 
@@ -182,7 +182,7 @@ def test_wal_replay_random_pieces_vs_oracle(hc, oracle, seed, ranges):
 
 
 @pytest.mark.parametrize("inject", ["", "wal_replay", "wal_replay:nomem"])
-def test_wal_replay_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypatch, inject):
+def test_wal_replay_gpu_batch_failure_finishes_on_host(knobs, hc, oracle, monkeypatch, inject):
     """A replay above the GPU threshold whose verify batch cannot run (no gfx950
     here, or a simulated HC_E_HIP / HC_E_NOMEM) verifies on the host path and
     returns what the oracle's wal.go:362-455 does -- including a corrupt block
@@ -192,9 +192,9 @@ def test_wal_replay_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypatch, 
     img = bytearray(b.tobytes())
     nb = len(img) // 4096
     assert nb >= 256
-    monkeypatch.setenv("HC_WAL_GPU_MIN_BLOCKS", "256")
+    knobs.setenv("HC_WAL_GPU_MIN_BLOCKS", "256")
     if inject:
-        monkeypatch.setenv("HC_INJECT_FAIL", inject)
+        knobs.setenv("HC_INJECT_FAIL", inject)
     for corrupt in (None, nb // 2):
         view = bytearray(img)
         if corrupt is not None:
@@ -211,7 +211,7 @@ def test_wal_replay_gpu_batch_failure_finishes_on_host(hc, oracle, monkeypatch, 
             assert st["nodev_host"] == 1 and st["wal_gpu"] == 0 and st["wal_gpu_fallback"] == 0
         else:
             assert st["wal_gpu"] == 1 and st["wal_gpu_fallback"] == 0
-    monkeypatch.setenv("HC_FORCE_GPU", "1")
+    knobs.setenv("HC_FORCE_GPU", "1")
     if inject or hc.device_count() == 0:
         with pytest.raises(hc.HundCRCError):
             hc.wal_replay(bytes(img), 4096)

@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1_000_000)
     ap.add_argument("--bsize", type=int, default=8192, help="host8k: block bytes")
     ap.add_argument("--verify", type=int, default=0, help="host8k: hc_verify_blocks instead of hc_crc32_blocks")
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--check", type=int, default=1, help="spot-check results against a CPU CRC")
     args = ap.parse_args()
@@ -59,7 +59,10 @@ def main():
     import torch
     from hunddb_amd import crc
     torch.cuda.set_device(0)
-    res = {"mode": args.mode, "mem": args.mem}
+    import bench
+    res = {"mode": args.mode, "mem": args.mem, "lib": os.environ.get("HUNDCRC_LIB", "in-tree"),
+           "copy_threads": os.environ.get("HC_COPY_THREADS", "8 (default)")}
+    thr0 = bench.cgroup_throttled_us()
 
     if args.mode == "host8k":
         B, n = args.bsize, args.blocks
@@ -250,6 +253,12 @@ def main():
         res["launch"] = crc.last_launch()
         bytes_ = total
     best = min(times)
+    thr1 = bench.cgroup_throttled_us()
+    # time the cgroup's CPU quota held the process back over the whole run
+    # (fills and warm-up included): a host path with more busy threads than the
+    # quota's CPUs is throttled in whole 100 ms periods
+    res["cgroup_throttled_ms"] = None if thr0 is None or thr1 is None else round((thr1 - thr0) / 1e3, 1)
+    res["cgroup_cpu_quota"] = bench.cgroup_cpu_quota()
     res.update(bytes=bytes_, seconds=[round(x, 4) for x in times], gib_s=round(bytes_ / best / 2**30, 2),
                gb_s=round(bytes_ / best / 1e9, 2), pcie_gen5_x16_frac=round(bytes_ / best / 63e9, 3)
                if args.mode not in ("config5b",) else None)

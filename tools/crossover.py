@@ -6,7 +6,8 @@ recovery), on pageable and pinned host buffers of 16 .. 4096 x 4 KiB blocks:
 microseconds per call on the GPU path and on the host path, from 1 caller and
 from 4 concurrent callers (SSTable flushes run on a pool of 4 workers,
 flush_worker.go:41-48).  Each path is forced with the entry's own
-HC_*_GPU_MIN_BLOCKS (read per call); the batched verify's host path is the
+HC_*_GPU_MIN_BLOCKS (set through hc_debug_set: the library reads its
+settings from the environment once); the batched verify's host path is the
 per-block CheckBlockIntegrity loop it replaces (tools/xover_host.c).
 
     python tools/crossover.py [--seconds 0.25] [--json-out F] [--sizes 16,64,...]
@@ -112,7 +113,8 @@ def call(entry, path, L, X, b, nb):
 def measure(entry, path, L, X, bufs, nb, threads, seconds):
     """(median us per call, calls, aggregate GB/s of block bytes)."""
     if entry in ENV:
-        os.environ[ENV[entry]] = "1" if path == "gpu" else str(1 << 30)
+        from hunddb_amd import crc
+        crc.debug_set(ENV[entry], "1" if path == "gpu" else str(1 << 30))
     for t in range(threads):  # warm: pipelines, page faults
         for _ in range(3):
             call(entry, path, L, X, bufs[t], nb)
@@ -182,7 +184,7 @@ def main():
                     res.append(row)
         del bufs
     for k in ENV:
-        os.environ.pop(ENV[k], None)
+        hc.debug_set(ENV[k], None)
     # tables
     for entry in a.entries.split(","):
         print(f"\n### {entry}\n")
