@@ -80,10 +80,14 @@ WORKLOADS = {
     # 2n record boundaries (round 5); bytes = record bytes + 4-B words (the gap
     # bytes the stream also reads are not counted)
     "records_gapped": (2_000_000, "records_gapped", "weak"),
+    # GetCRC of 1M aligned 4 KiB records in shuffled order: the
+    # stream refuses them; its fallback runs k_crc_grp's body inside the combine
+    "records4k_shuffled": (1_000_000, "records4k_shuffled", "weak"),
 }
 # the dominant kernel per workload (PMC passes)
 KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
-             "records": "k_seg_stream", "records_gapped": "k_seg_stream"}  # else the streaming CRC kernel
+             "records": "k_seg_stream", "records_gapped": "k_seg_stream",
+             "records4k_shuffled": "k_seg_combine"}  # else the streaming CRC kernel
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
 
@@ -114,6 +118,8 @@ def parse(argv=None):
                     help="N>1 strong scaling: each rank fills its shard in HBM (resident), or rank 0 holds the "
                          "whole batch and sends the shards over RCCL first (scatter; timed and reported "
                          "separately, SURVEY.md 8e)")
+    ap.add_argument("--host-leg", choices=["auto", "on", "off"], default="auto",
+                    help="N=1: the host-inclusive leg (blocks in host memory, PCIe included; auto = northstar only)")
     ap.add_argument("--rank-timeout", type=float, default=900.0,
                     help="N>1: seconds the self-launcher waits for its ranks (then kills them and prints one JSON "
                          "error line naming the ranks still alive and their phase); also the process-group timeout")
@@ -417,6 +423,100 @@ def cpu_baseline_framing(kind, dev_src, threads, budget_s, B=4096):
 
 
 # --------------------------------------------------------------------------
+# Host-inclusive leg (N = 1, outside the timed device region): the blocks start
+# and end in host memory (WAL segment files, SSTable files), so BASELINE.json's
+# north star also asks for the rate with the H2D copy of the blocks and the D2H
+# copy of the CRC words overlapped on side streams (the library's host
+# pipelines), against the link's own pinned hipMemcpyAsync peak.
+def _best_rate(fn, nbytes, reps):
+    fn()  # warm: pipelines, page faults
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        best = min(best, time.perf_counter() - t0)
+    return nbytes / best / 1e9, best
+
+
+def h2d_peak(torch, pinned, seconds=1.0):
+    """GB/s of pinned host -> device hipMemcpyAsync (torch copies), 256 MiB
+    chunks on two streams: the link's practical ceiling on this box."""
+    chunk = 256 << 20
+    n = pinned.numel() // chunk
+    dst = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    best = 0.0
+    t_end = time.perf_counter() + seconds
+    while True:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n):
+            with torch.cuda.stream(streams[k % 2]):
+                dst[k % 3].copy_(pinned[k * chunk:(k + 1) * chunk], non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, n * chunk / (time.perf_counter() - t0) / 1e9)
+        if time.perf_counter() > t_end:
+            return best
+
+
+def host_inclusive(torch, crc, dev_buf, dev_words, B, reps=3, wal_records=2_000_000):
+    """hc_crc32_blocks over the north-star batch from pinned and from pageable
+    host memory (words against the device run), hc_verify_blocks over a
+    config-5-shaped WAL image in pinned memory (2M records framed as
+    lsm/wal/wal.go:177-283, tools/walgen.c), and the same run's pinned H2D
+    peak; rates in GB/s of block bytes per wall second, best of `reps`."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import walgen
+    t_leg = time.perf_counter()
+    n = dev_words.numel()
+    nbytes = n * B
+    want = dev_words.cpu().numpy().view(np.uint32)
+    pinned = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(dev_buf[:nbytes])
+    peak = h2d_peak(torch, pinned)
+    res = {"h2d_peak_gb_s": round(peak, 2), "pcie_nominal_gb_s": 63.0,
+           "h2d_peak_note": "pinned hipMemcpyAsync H2D, 256 MiB chunks on 2 streams, this run"}
+    words = {}
+
+    def leg(name, host):
+        out = {}
+        r, t = _best_rate(lambda: out.__setitem__("w", crc.crc32_blocks(host, stride=B, ulen=B, nblocks=n)),
+                          nbytes, reps)
+        words[name] = out["w"]
+        res[name] = {"workload": f"hc_crc32_blocks, {n} x {B} B", "gb_s": round(r, 2), "s": round(t, 4),
+                     "frac_h2d_peak": round(r / peak, 3), "frac_pcie_gen5_x16": round(r / 63.0, 3),
+                     "words_match_device": bool(np.array_equal(out["w"], want))}
+    leg("crc32_blocks_pinned", pinned.numpy())
+    pageable = np.empty(nbytes, dtype=np.uint8)
+    pageable[:] = pinned.numpy()
+    del pinned
+    leg("crc32_blocks_pageable", pageable)
+    del pageable
+    plan = walgen.WalPlan(0x57414C, nrec=wal_records)
+    nb = plan.nblocks
+    img = torch.empty(nb * 4096, dtype=torch.uint8, pin_memory=True)
+    host = img.numpy()
+    step = 1 << 18
+    for b0 in range(0, nb, step):
+        plan.render(b0, min(nb, b0 + step), out=host[b0 * 4096:min(nb, b0 + step) * 4096], threads=cores_available())
+    got = {}
+    r, t = _best_rate(lambda: got.__setitem__("v", crc.verify_blocks(host, stride=4096, ulen=4096, nblocks=nb)),
+                      nb * 4096, reps)
+    err, bm, fb = got["v"]
+    res["wal_verify_pinned"] = {"workload": f"hc_verify_blocks over a config-5 WAL image: {wal_records} records "
+                                            f"(64 B - 64 KiB log-uniform) framed into {nb} x 4 KiB blocks",
+                                "gb_s": round(r, 2), "s": round(t, 4), "frac_h2d_peak": round(r / peak, 3),
+                                "frac_pcie_gen5_x16": round(r / 63.0, 3),
+                                "all_blocks_verify": err is None and fb == -1 and not bm.any()}
+    del img
+    res["words_match_device"] = all(res[k]["words_match_device"] for k in ("crc32_blocks_pinned",
+                                                                            "crc32_blocks_pageable"))
+    res["leg_s"] = round(time.perf_counter() - t_leg, 1)
+    return res
+
+
+# --------------------------------------------------------------------------
 def self_launch(argv, nproc, script=None):
     """`bench.py --gpus N` without WORLD_SIZE: run N ranks (one per GPU) as child
     processes with the torch.distributed.run environment; this process never
@@ -565,6 +665,19 @@ def main(argv=None):
                       ("with a 17-B gap before each" if gap else "back to back") + " (off/len arrays)")
         k = int(np.searchsorted(off_h, 512 << 20))
         sample = (slice(0, int(off_h[k - 1]) + int(lens_h[k - 1])), off_h[:k].copy(), lens_h[:k].copy())
+    elif bsize == "records4k_shuffled":
+        buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
+        crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
+        perm = np.random.default_rng(SEED).permutation(my).astype(np.uint64)
+        off_h = perm * np.uint64(4096)
+        lens_h = np.full(my, 4096, dtype=np.uint32)
+        doff = torch.from_numpy(off_h.view(np.int64)).to(dev)
+        dlen = torch.from_numpy(lens_h.view(np.int32)).to(dev)
+        kw = dict(off=doff, lens=dlen, nblocks=my, flags=crc.HC_F_MESSAGES)
+        step_bytes = my * 4096 + 4 * my
+        block_desc = "GetCRC per record: aligned 4 KiB records in shuffled order (off/len arrays)"
+        k = min(my, (512 << 20) // 4096)
+        sample = (slice(0, my * 4096), off_h[:k].copy(), lens_h[:k].copy())
     elif bsize in UNFRAME_B:
         UB = UNFRAME_B[bsize]
         buf = torch.empty(my * UB, dtype=torch.uint8, device=dev)
@@ -662,7 +775,7 @@ def main(argv=None):
             raise RuntimeError(f"{world} RCCL ranks ran on {proof['distinct_devices']} distinct GPU(s): "
                                f"{[(i['rank'], i['host'], i['bus_id']) for i in proof['ranks']]}")
     info = crc.last_launch()
-    seg_mode = crc.seg_mode() if bsize in ("records", "records_gapped") else False
+    seg_mode = crc.seg_path() if bsize in ("records", "records_gapped", "records4k_shuffled") else False
     verify_clean = None
     if bsize == "verify":  # every stamped block must have verified clean
         verify_clean = int(first_bad.item()) == 2**63 - 1 and int(bitmap.abs().sum().item()) == 0
@@ -737,10 +850,14 @@ def main(argv=None):
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
                 **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine (the fallback for a "
                                    "batch the stream refuses runs inside the combine); traffic: k_seg_stream"}
-                   if bsize in ("records", "records_gapped") else {}),
+                   if bsize in ("records", "records_gapped", "records4k_shuffled") else {}),
                 "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}
+        host_leg = None
+        if world == 1 and (args.host_leg == "on" or (args.host_leg == "auto" and args.workload == "northstar")):
+            phase("host_leg")
+            host_leg = host_inclusive(torch, crc, buf, out, bsize)
         cpu = None
         if not args.cpu_threads:
             args.cpu_threads = cores_available()
@@ -754,7 +871,7 @@ def main(argv=None):
                 cpu = cpu_baseline(host, soff, slen, args.cpu_threads, args.cpu_seconds,
                                    f"{args.workload} ({block_desc})",
                                    gpu_words=out[: len(soff)].cpu().numpy().view(np.uint32),
-                                   messages=bsize in ("records", "records_gapped"))
+                                   messages=bsize in ("records", "records_gapped", "records4k_shuffled"))
         res = {
             "metric": METRIC,
             "value": round(gib_s, 2),
@@ -774,11 +891,13 @@ def main(argv=None):
                        "dist_backend": backend if world > 1 else None,
                        "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4),
                        **({"verify_clean": verify_clean} if verify_clean is not None else {}),
-                       **({"packed_stream_taken": seg_mode is not None, "stream_mode": seg_mode}
+                       **({"packed_stream_taken": seg_mode in ("packed", "gapped"), "stream_mode": seg_mode}
                           if seg_mode is not False else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if host_leg is not None:
+            res["host_inclusive"] = host_leg
         res["workload_note"] = WORKLOAD_NOTE
         if multi is not None:
             res["multi_gpu"] = multi

@@ -157,7 +157,12 @@ def _lib():
             "hc_merkle_validate": (I, [P, U64, P, U64, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                if os.environ.get("HUNDCRC_LIB"):  # an older A/B build: entries it lacks fail when called
+                    continue
+                raise
             fn.restype, fn.argtypes = res, args
         _LIB = L
     return _LIB
@@ -643,21 +648,30 @@ def debug_set(name: str, value=None) -> None:
         raise HundCRCError(r, f"debug_set({name})")
 
 
-def seg_mode():
+def seg_path():
     """How this thread's last device batch of whole messages was hashed:
     "packed" (the packed-record stream over records back to back), "gapped"
-    (the same stream over sorted records with gaps), or None (k_crc_any).
-    Synchronizes the device; tests and tools."""
+    (the same stream over sorted records with gaps), "fallback_grp" (the
+    stream's fallback: k_crc_grp, then k_crc_any over what it skipped) or
+    "fallback" (k_crc_any alone, or not offered to the stream).  Synchronizes
+    the device; tests and tools."""
     r = int(_lib().hc_debug_seg_taken())
     if r < 0:
         raise HundCRCError(r, "seg_taken")
-    return {1: "packed", 2: "gapped"}.get(r)
+    return {1: "packed", 2: "gapped", 3: "fallback_grp"}.get(r, "fallback")
+
+
+def seg_mode():
+    """"packed" or "gapped" when the packed-record stream took this thread's
+    last device batch of whole messages, else None (synchronizes the device)."""
+    p = seg_path()
+    return p if p in ("packed", "gapped") else None
 
 
 def seg_taken() -> bool:
     """Whether this thread's last device batch of whole messages was hashed by
-    the packed-record stream (k_seg_*, packed or gapped) rather than k_crc_any
-    (synchronizes the device; tests and tools)."""
+    the packed-record stream (k_seg_*, packed or gapped) rather than a
+    fallback (synchronizes the device; tests and tools)."""
     return seg_mode() is not None
 
 

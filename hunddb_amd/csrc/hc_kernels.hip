@@ -353,18 +353,19 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
 // The variants measured against this one before round 4 (static deal, batched
 // refills, nibble finalise tables, timing-only build) are in git history
 // (tools/ab_hc_kernels.hip, up to commit 61a2e0e).
-template <bool kArrays, bool kXcd = false>
-__global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
-                                                         const uint32_t *__restrict__ lens, uint64_t stride,
-                                                         uint32_t ulen, uint32_t flags, uint64_t nblocks,
-                                                         uint32_t lg_chunk, uint32_t *__restrict__ crc_out,
-                                                         uint32_t *__restrict__ bad_bitmap,
-                                                         unsigned long long *__restrict__ first_bad,
-                                                         const DeviceTables *__restrict__ tables,
-                                                         unsigned long long *__restrict__ skip_slot = nullptr,
-                                                         uint64_t skip_tag = 0) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 2048];
-  __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
+// The body, a device function: the k_crc_grp kernel below, and k_seg_combine
+// for a batch of mostly 4 KiB-multiple records the packed-record stream did not
+// take (out of order, overlapping: the fallback in the same launch).  `lds`
+// holds kFastLdsBytes of tables and the 8 KiB sh512 table after them.
+template <bool kArrays, bool kXcd>
+__device__ __forceinline__ void crc_grp_body(uint32_t *lds, uint32_t &s_next, const uint8_t *base,
+                                             const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+                                             uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks,
+                                             uint32_t lg_chunk, uint32_t *__restrict__ crc_out,
+                                             uint32_t *__restrict__ bad_bitmap,
+                                             unsigned long long *__restrict__ first_bad,
+                                             const DeviceTables *__restrict__ tables,
+                                             unsigned long long *__restrict__ skip_slot, uint64_t skip_tag) {
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   fill_crc_tables(lds, tables, tid, kFastThreads);
@@ -602,6 +603,22 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
       gp = np;
     }
   }
+}
+
+template <bool kArrays, bool kXcd = false>
+__global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ lens, uint64_t stride,
+                                                         uint32_t ulen, uint32_t flags, uint64_t nblocks,
+                                                         uint32_t lg_chunk, uint32_t *__restrict__ crc_out,
+                                                         uint32_t *__restrict__ bad_bitmap,
+                                                         unsigned long long *__restrict__ first_bad,
+                                                         const DeviceTables *__restrict__ tables,
+                                                         unsigned long long *__restrict__ skip_slot = nullptr,
+                                                         uint64_t skip_tag = 0) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 2048];
+  __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
+  crc_grp_body<kArrays, kXcd>(lds, s_next, base, offs, lens, stride, ulen, flags, nblocks, lg_chunk, crc_out,
+                              bad_bitmap, first_bad, tables, skip_slot, skip_tag);
 }
 
 // ---------------------------------------------------------------------------
@@ -1651,17 +1668,26 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 // payload, the span-DMA rule of the host pipeline).  Every slot is written, so
 // the dispatch needs no memset: k_seg_stream's workgroups reduce the slots and
 // its workgroup 0 stores the mode the combine reads.
-constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2;  // the mode word k_seg_stream stores
+// the mode word k_seg_stream stores: kSegFallbackGrp is the fallback for a batch
+// whose records are mostly 16-B aligned 4 KiB multiples (k_crc_grp's blocks)
+constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2, kSegFallbackGrp = 3;
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
                                                   uint32_t *__restrict__ plan_bad, long long *__restrict__ plan_gx,
-                                                  uint32_t *__restrict__ first_ev) {
-  __shared__ uint32_t s_bad;
+                                                  uint32_t *__restrict__ plan_conf, uint32_t *__restrict__ first_ev) {
+  __shared__ uint32_t s_bad, s_conf;
   __shared__ unsigned long long s_gx;
   if (threadIdx.x == 0) {
     s_bad = 0;
+    s_conf = 0;
     s_gx = 0;
+  }
+  // records k_crc_grp would take (the fallback's choice: k_seg_stream prologue)
+  uint32_t conf = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t l = lens[j];
+    conf += ((((uintptr_t)base + offs[j]) & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
   }
   const SegGeo g = seg_geo<kU>(base, offs, lens, n);
   uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 3u : 0u;
@@ -1699,10 +1725,12 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
   __syncthreads();
   if (bad) atomicOr(&s_bad, bad);
   if (gx) atomicAdd(&s_gx, (unsigned long long)gx);
+  if (conf) atomicAdd(&s_conf, conf);
   __syncthreads();
   if (threadIdx.x == 0) {  // every slot written: no memset
     plan_bad[blockIdx.x] = s_bad;
     plan_gx[blockIdx.x] = (long long)s_gx;
+    plan_conf[blockIdx.x] = s_conf;
   }
 }
 
@@ -1953,7 +1981,8 @@ template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
                                                             uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
-                                                            const long long *__restrict__ plan_gx, uint32_t plan_wgs,
+                                                            const long long *__restrict__ plan_gx,
+                                                            const uint32_t *__restrict__ plan_conf, uint32_t plan_wgs,
                                                             uint32_t *__restrict__ flag,
                                                             const uint32_t *__restrict__ first_ev,
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
@@ -1961,6 +1990,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
   __shared__ uint32_t s_next;
   __shared__ long long s_gx[kFastWaves];
+  __shared__ uint32_t s_conf[kFastWaves];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   fill_crc_tables(lds, tables, tid, kFastThreads);
@@ -1968,21 +1998,38 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   uint32_t col[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
-  uint32_t bad = 0;
+  uint32_t bad = 0, conf = 0;
   long long gx = 0;
   for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) {
     bad |= plan_bad[i];
     gx += plan_gx[i];
+    conf += plan_conf[i];
   }
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) gx += __shfl_xor(gx, d);
-  if (lane == 0) s_gx[tid >> 6] = gx;
+  for (int d = 32; d >= 1; d >>= 1) {
+    gx += __shfl_xor(gx, d);
+    conf += __shfl_xor(conf, d);
+  }
+  if (lane == 0) {
+    s_gx[tid >> 6] = gx;
+    s_conf[tid >> 6] = conf;
+  }
   const int unpacked = __syncthreads_or((int)(bad & 1u));
-  const int unsorted = __syncthreads_or((int)(bad & 2u));  // (also orders the s_gx stores)
+  const int unsorted = __syncthreads_or((int)(bad & 2u));  // (also orders the s_gx / s_conf stores)
   long long gsum = 0;
+  uint64_t csum = 0;
 #pragma unroll
-  for (int w = 0; w < kFastWaves; w++) gsum += s_gx[w];
-  const uint32_t mode = !unpacked ? kSegPacked : !unsorted && gsum <= 0 ? kSegGapped : kSegFallback;
+  for (int w = 0; w < kFastWaves; w++) {
+    gsum += s_gx[w];
+    csum += s_conf[w];
+  }
+  // the fallback: k_crc_grp's body first when at least half of the records are
+  // its blocks (aligned 4 KiB multiples out of order, or far apart), else
+  // k_crc_any's alone (the per-record body ran 57-62 % on them)
+  const uint32_t mode = !unpacked                   ? kSegPacked
+                        : !unsorted && gsum <= 0    ? kSegGapped
+                        : 2 * csum >= n             ? kSegFallbackGrp
+                                                    : kSegFallback;
   if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
   if (mode == kSegGapped)
     seg_stream_body<true, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
@@ -2020,7 +2067,8 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
                                                       const uint32_t *__restrict__ unit_raw,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken,
-                                                      uint32_t flags, const DeviceTables *__restrict__ tables) {
+                                                      uint32_t flags, uint32_t grp_lg,
+                                                      const DeviceTables *__restrict__ tables) {
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
   constexpr uint32_t kUnitRows = 1u << (kU - 10);
   __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024];
@@ -2041,15 +2089,26 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
     }
   }
   const uint32_t mode = *flag;
-  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped)
-    *taken = mode == kSegFallback ? 0u : mode == kSegGapped ? 2u : 1u;
+  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks)
+    *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : 0u;
   __syncthreads();
-  if (mode == kSegFallback) {
+  if (mode == kSegFallback || mode == kSegFallbackGrp) {
     // the stream did not take the batch: k_crc_any's work over every message,
     // in this launch (round 3 launched k_crc_any after the combine, ~5 us a
     // call even when it exits at once).  The tables above are not used: the
-    // body fills its own over them, after the barrier.
-    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, 0u, 0u, crc_out, nullptr, nullptr, tables, nullptr, 0);
+    // bodies fill their own over them, after the barrier.  kSegFallbackGrp:
+    // k_crc_grp's work first (its hand-out counter past its 8 KiB sh512
+    // table), then the k_crc_any sweep over the records it skipped (fast_mask
+    // 4095).  (One call site of crc_any_body: two inlined copies spilled.)
+    static_assert(kFastLdsBytes / 4 + 2048 + 1 <= (kSegRs + kSegIv) * 1024, "k_crc_grp's LDS fits the combine's");
+    const bool grp = mode == kSegFallbackGrp;
+    if (grp) {
+      crc_grp_body<true, false>(tl, tl[kFastLdsBytes / 4 + 2048], base, offs, lens, 0, 0, flags, n, grp_lg, crc_out,
+                                nullptr, nullptr, tables, nullptr, 0);
+      __syncthreads();
+    }
+    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, grp ? 4095u : 0u, 0u, crc_out, nullptr, nullptr, tables,
+                       nullptr, 0);
     return;
   }
   const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
@@ -2238,10 +2297,12 @@ hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, 
 uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
 
 // workspace (u32 words): the mode flag (64 words), plan_bad[kSegPlanMaxWgs],
-// plan_gx[kSegPlanMaxWgs] (int64), first_ev[max_units + 1], unit_raw[max_units],
+// plan_gx[kSegPlanMaxWgs] (int64), plan_conf[kSegPlanMaxWgs],
+// first_ev[max_units + 1], unit_raw[max_units],
 // ev_h[2n + 1] (the gapped numbering's 2n events; a packed batch uses n + 1)
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
-  return 4 * (64 + kSegPlanMaxWgs) + 8 * kSegPlanMaxWgs + 4 * ((max_units + 1) + max_units + 2 * n + 1);
+  return 4 * (64 + kSegPlanMaxWgs) + 8 * kSegPlanMaxWgs + 4 * kSegPlanMaxWgs +
+         4 * ((max_units + 1) + max_units + 2 * n + 1);
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
@@ -2251,18 +2312,18 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint64_t n = b.nblocks;
   uint32_t *flag = ws, *plan_bad = ws + 64;
   long long *plan_gx = reinterpret_cast<long long *>(plan_bad + kSegPlanMaxWgs);  // (8-B aligned: 64 + 16384 words)
-  uint32_t *first_ev = reinterpret_cast<uint32_t *>(plan_gx + kSegPlanMaxWgs), *unit_raw = first_ev + max_units + 1,
-           *ev_h = unit_raw + max_units;
+  uint32_t *plan_conf = reinterpret_cast<uint32_t *>(plan_gx + kSegPlanMaxWgs), *first_ev = plan_conf + kSegPlanMaxWgs,
+           *unit_raw = first_ev + max_units + 1, *ev_h = unit_raw + max_units;
   const uint64_t pg = (n + 256) / 256;
   // HC_SEG_PLAN_WGS overrides the plan's grid cap, up to kSegPlanMaxWgs (tuning sweeps)
   static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanWgs)));
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
-                     plan_gx, first_ev);
+                     plan_gx, plan_conf, first_ev);
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
-                     plan_gx, plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
+                     plan_gx, plan_conf, plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
-                     b.crc_out, st, taken, b.flags, b.tables);
+                     b.crc_out, st, taken, b.flags, grp_lg_chunk(n, grid, 0), b.tables);
   return hipGetLastError();
 }
 

@@ -332,11 +332,12 @@ int hc_last_launch(hc_launch_info *info);
  * into out (returns HC_OK) or, if cap is too small, return its size. */
 int hc_debug_tables(void *out, size_t cap);
 
-/* 1 if this thread's last device batch of whole messages was hashed by the
- * packed-record stream (k_seg_*) as records back to back, 2 if
- * as sorted records with gaps between them, 0 if it fell back to k_crc_any on
- * the device or was not offered to the stream; synchronizes that device
- * (tests and tools only). */
+/* How this thread's last device batch of whole messages was hashed: 1 by the
+ * packed-record stream (k_seg_*) as records back to back, 2 by
+ * the same stream as sorted records with gaps between them, 3 by the stream's
+ * fallback with k_crc_grp first (mostly aligned 4 KiB-multiple records out of
+ * order), 0 by k_crc_any alone on the device or not offered to the stream;
+ * synchronizes that device (tests and tools only). */
 int hc_debug_seg_taken(void);
 
 /* The library reads its HC_* settings from the environment once, at the first

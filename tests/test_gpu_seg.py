@@ -380,3 +380,41 @@ def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
     check(torch, hc, oracle, host, buf, off, o, None)
     p = rng.permutation(len(off))
     check(torch, hc, oracle, host, buf, off[p], lens[p], None)
+
+
+def test_seg_fallback_runs_crc_grp_on_aligned_records(cuda, hc, oracle, seg_all):
+    """a whole-message batch the stream refuses whose
+    records are mostly 16-B aligned 4 KiB multiples (out of order, or far
+    apart) runs k_crc_grp's body first inside k_seg_combine, then the k_crc_any
+    sweep over the rest ("fallback_grp"); under half of them: k_crc_any alone.
+    Every word against the oracle."""
+    torch = cuda
+    rng = np.random.default_rng(41)
+    n = 6000
+    lens = (4096 << rng.integers(0, 3, n)).astype(np.uint64)   # 4 / 8 / 16 KiB
+    off = packed(lens, 0)
+    total = int(off[-1] + lens[-1]) + 4096
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    assert buf.data_ptr() % 16 == 0
+    p = rng.permutation(n)
+    check(torch, hc, oracle, host, buf, off[p], lens[p], None)          # out of order: all k_crc_grp's
+    assert hc.seg_path() == "fallback_grp"
+    far = (np.arange(n, dtype=np.uint64) * np.uint64(16384 * 2))[: n // 4]  # gaps over a quarter
+    fl = np.full(n // 4, 16384, dtype=np.uint64)
+    big = torch.zeros(int(far[-1]) + 16384 + 64, dtype=torch.uint8, device="cuda")
+    bh = rng.integers(0, 256, big.numel(), dtype=np.uint8)
+    big.copy_(torch.from_numpy(bh))
+    check(torch, hc, oracle, bh, big, far, fl, None)
+    assert hc.seg_path() == "fallback_grp"
+    mixed = lens[p].copy()
+    k = rng.choice(n, int(0.4 * n), replace=False)
+    mixed[k] -= np.uint64(100)  # 40 % not 4 KiB multiples: k_crc_grp first, the sweep after
+    check(torch, hc, oracle, host, buf, off[p], mixed, None)
+    assert hc.seg_path() == "fallback_grp"
+    mixed[rng.choice(n, int(0.7 * n), replace=False)] -= np.uint64(7)  # most not: k_crc_any alone
+    check(torch, hc, oracle, host, buf, off[p], mixed, None)
+    assert hc.seg_path() == "fallback"
+    mis = off[p] + np.uint64(4)  # misaligned 4 KiB multiples (sizes stay in the buffer: -4 from each)
+    check(torch, hc, oracle, host, buf, mis, lens[p] - np.uint64(4096), None)
+    assert hc.seg_path() == "fallback"

@@ -1,12 +1,14 @@
-"""Several host threads enqueueing device batches at once: the
-per-device words shared by every call -- k_crc_grp's "left a block to the
-sweep" slot (Batch::skip_slot) and the packed-record stream's "did not take
-the batch" slot (Batch::seg_slot) -- are raised to per-call tags that increase
-across calls, so a call can only run a fallback it did not need, never skip one
-it needs.  4 threads, each on its own stream, alternate conforming off/len
-batches with ones holding non-conforming blocks (misaligned, short), and
-packed record batches with ones that have a gap; every word of every call is
-checked against the oracle (crc_util.go:15-17 / ChecksumIEEE per block)."""
+"""Several host threads enqueueing device batches at once.
+k_crc_grp's "left a block to the sweep" word (Batch::skip_slot) is shared by
+every call on a device and raised to per-call tags that increase across
+calls, so a call can only run a sweep it did not need, never skip one it
+needs.  The packed-record stream's mode word is word 0 of its workspace: kept
+on the null stream (one stream orders every use) and allocated per call on
+other streams, so concurrent calls never share it.  4 threads, each on its own
+stream, alternate conforming off/len batches with ones holding non-conforming
+blocks (misaligned, short), and packed record batches with ones that the
+stream refuses; every word of every call is checked against the oracle
+(crc_util.go:15-17 / ChecksumIEEE per block)."""
 import threading
 
 import numpy as np
@@ -33,6 +35,9 @@ def test_concurrent_threads_share_the_device_slots(knobs, cuda, hc, oracle, monk
     gap_off = rec_off.copy()
     gap_off[n // 3:] += np.uint64(1)
     gap_want = oracle.crc32_messages(host, gap_off, rec_len.astype(np.uint32), threads=8)
+    ovl_off = rec_off.copy()
+    ovl_off[n // 3:] -= np.uint64(1)  # records n/3 - 1 and n/3 overlap: the stream's fallback
+    ovl_want = oracle.crc32_messages(host, ovl_off, rec_len.astype(np.uint32), threads=8)
 
     def variant(k):
         """(off, len, flags, want) of call k of a thread"""
@@ -51,7 +56,9 @@ def test_concurrent_threads_share_the_device_slots(knobs, cuda, hc, oracle, monk
             return off, lens, 0, want
         if kind == 2:
             return rec_off, rec_len.astype(np.uint32), hc.HC_F_MESSAGES, rec_want
-        return gap_off, rec_len.astype(np.uint32), hc.HC_F_MESSAGES, gap_want
+        if k % 8 == 3:  # sorted with a gap: the stream's gapped mode
+            return gap_off, rec_len.astype(np.uint32), hc.HC_F_MESSAGES, gap_want
+        return ovl_off, rec_len.astype(np.uint32), hc.HC_F_MESSAGES, ovl_want
 
     errors = []
 

@@ -56,7 +56,7 @@ for s in "${LIST[@]}"; do
     st bench 600 python bench.py $BENCH_ARGS --json-out "$OUT/bench.json" || stop $? ;;
   rocprof)
     (cd /tmp && st rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-      -- python3 "$R/bench.py" $BENCH_ARGS --pmc off --cpu-seconds 0 --json-out "$OUT/bench_under_rocprof.json") || stop $? ;;
+      -- python3 "$R/bench.py" $BENCH_ARGS --pmc off --cpu-seconds 0 --host-leg off --json-out "$OUT/bench_under_rocprof.json") || stop $? ;;
   workloads)
     for w in $WORKLOADS; do
       st "bench_$w" 600 python bench.py --workload "$w" $BENCH_ARGS --json-out "$OUT/bench_$w.json" || stop $?

@@ -10,7 +10,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 for w in "$@"; do
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_$w" -o run \
-     -- python3 "$R/bench.py" --workload "$w" --pmc off --cpu-seconds 0 --json-out "$out/bench_${w}_under_rocprof.json" \
+     -- python3 "$R/bench.py" --workload "$w" --pmc off --cpu-seconds 0 --host-leg off --json-out "$out/bench_${w}_under_rocprof.json" \
      > "$out/prof_$w.log" 2>&1) || exit $?
   python3 - "$out/prof_$w/run_kernel_stats.csv" "$out/bench_${w}_under_rocprof.json" <<'PY'
 import csv, json, sys
