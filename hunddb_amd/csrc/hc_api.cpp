@@ -291,7 +291,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
         if (ws) {
           // word 0 of ws: raised when the stream did not take the batch; then
           // k_seg_combine runs k_crc_any's work over every message itself
-          e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last);
+          e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last, (uint64_t)knob(kKnobSegGrpMin));
           seg = true;
         }
       }

@@ -39,6 +39,12 @@ namespace hc {
 
 namespace {
 
+// The mode word k_seg_stream stores for its batch:
+// kSegFallbackGrp is the fallback for a batch whose records are mostly 16-B
+// aligned 4 KiB multiples (k_crc_grp's blocks): k_crc_grp and the k_crc_any
+// sweep, launched after the combine with this word as their gate.
+constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2, kSegFallbackGrp = 3;
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
@@ -614,9 +620,11 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_grp(const uint8_t *base, c
                                                          unsigned long long *__restrict__ first_bad,
                                                          const DeviceTables *__restrict__ tables,
                                                          unsigned long long *__restrict__ skip_slot = nullptr,
-                                                         uint64_t skip_tag = 0) {
+                                                         uint64_t skip_tag = 0,
+                                                         const uint32_t *__restrict__ gate = nullptr) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 2048];
   __shared__ uint32_t s_next;  // next hand-out index of this workgroup's block sequence
+  if (gate && *gate != kSegFallbackGrp) return;  // the packed-record stream's fallback only (launch_seg)
   crc_grp_body<kArrays, kXcd>(lds, s_next, base, offs, lens, stride, ulen, flags, nblocks, lg_chunk, crc_out,
                               bad_bitmap, first_bad, tables, skip_slot, skip_tag);
 }
@@ -1087,8 +1095,10 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
-    const unsigned long long *skip_slot = nullptr, uint64_t skip_tag = 0) {
+    const unsigned long long *skip_slot = nullptr, uint64_t skip_tag = 0,
+    const uint32_t *__restrict__ gate = nullptr) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 1];
+  if (gate && *gate != kSegFallbackGrp) return;  // the packed-record stream's fallback only (launch_seg)
   crc_any_body<kSmallLanes>(lds, base, offs, lens, stride, ulen, flags, nblocks, fast_mask, lg_chunk, crc_out,
                             bad_bitmap, first_bad, tables, skip_slot, skip_tag);
 }
@@ -1668,9 +1678,6 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 // payload, the span-DMA rule of the host pipeline).  Every slot is written, so
 // the dispatch needs no memset: k_seg_stream's workgroups reduce the slots and
 // its workgroup 0 stores the mode the combine reads.
-// the mode word k_seg_stream stores: kSegFallbackGrp is the fallback for a batch
-// whose records are mostly 16-B aligned 4 KiB multiples (k_crc_grp's blocks)
-constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2, kSegFallbackGrp = 3;
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
@@ -1850,6 +1857,14 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
   uint32_t hv = 0;  // lane k: H of the group's event wfirst + k (stored once per group)
   uint32_t ur_pend = 0, ur_bytes = 0;  // the last unit's raw CRC, stored after the next group
   uint64_t u_pend = 0;
+  // kGap: the stream hashes the span with every gap byte [e_{j-1}, s_j) zeroed.
+  // Zeros do not change a raw CRC, so H(s_j) is H(e_{j-1}) shifted to s_j's row
+  // (or 0 in a later unit) and the combine derives it: H is needed at the
+  // record ends e_j (odd events) and at s_0 only -- one placement per record, as
+  // a packed batch.  `ingap` (wave-uniform): the current row starts inside a
+  // gap; at a unit's start, when its first event is a record start s_j (j > 0).
+  auto gap_at = [&](uint64_t f) -> uint32_t { return kGap && f > 0 && f < 2 * n && !(f & 1u) ? 1u : 0u; };
+  uint32_t ingap = gap_at(wfirst);
 
   // H at the events of the row starting at rs (uniform mask evm of window
   // lanes), from the streams c with the row already folded in: H(x) is the
@@ -1915,14 +1930,49 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
     typedef unsigned int r32x4 __attribute__((ext_vector_type(4)));
     r32x4 qq = __builtin_bit_cast(r32x4, q);
     asm volatile("" : "+v"(qq));
-    const uint4 w = __builtin_bit_cast(uint4, qq);
+    uint4 w = __builtin_bit_cast(uint4, qq);
+    const uint64_t evm = __ballot(wpos >= rs && wpos < rs + 1024u);
+    uint64_t evh = evm;  // the events that need H
+    if constexpr (kGap) {
+      // window lanes k with wfirst + k odd: record ends (they open a gap; the
+      // even ones, record starts, close it)
+      const uint64_t ends = (wfirst & 1u) ? 0x5555555555555555ull : 0xAAAAAAAAAAAAAAAAull;
+      evh = evm & (ends | (wfirst == 0 ? 1ull : 0ull));
+      if (ingap || evm) {
+        uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, lo = 0;
+        uint32_t open = ingap;
+        auto zero = [&](uint32_t a, uint32_t b) {  // row bytes [a, b)
+          const int qa = min(max((int)a - (int)(16u * lane), 0), 16), qb = min(max((int)b - (int)(16u * lane), 0), 16);
+          g0 |= keep(qb, 0) & ~keep(qa, 0);
+          g1 |= keep(qb, 1) & ~keep(qa, 1);
+          g2 |= keep(qb, 2) & ~keep(qa, 2);
+          g3 |= keep(qb, 3) & ~keep(qa, 3);
+        };
+        for (uint64_t m = evm; m; m &= m - 1) {
+          const uint32_t k = (uint32_t)__builtin_ctzll(m);
+          const uint32_t rel = uni((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wpos - rs), k));
+          if ((ends >> k) & 1u) {
+            lo = rel;
+            open = 1;
+          } else if (open) {
+            zero(lo, rel);
+            open = 0;
+          }
+        }
+        if (open) zero(lo, 1024u);
+        ingap = open;
+        w.x &= ~g0;
+        w.y &= ~g1;
+        w.z &= ~g2;
+        w.w &= ~g3;
+      }
+    }
     c0 = row_step(c0, w.x);
     c1 = row_step(c1, w.y);
     c2 = row_step(c2, w.z);
     c3 = row_step(c3, w.w);
-    const uint64_t evm = __ballot(wpos >= rs && wpos < rs + 1024u);
     asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
-    if (evm) events(w, rs, wpos, evm);
+    if (evh) events(w, rs, wpos, evh);
     __builtin_amdgcn_sched_barrier(0);
     q = buf_load16(rn, no);
     __builtin_amdgcn_sched_barrier(0);
@@ -1964,6 +2014,7 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
       rc = rn;
       g = 0;
       c0 = c1 = c2 = c3 = 0;
+      ingap = gap_at(nf);
       un = unit_of(uni(kv));
       if (lane == 0) kv = atomicAdd(&s_next, 1u);
     } else {
@@ -1983,6 +2034,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
                                                             uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
                                                             const long long *__restrict__ plan_gx,
                                                             const uint32_t *__restrict__ plan_conf, uint32_t plan_wgs,
+                                                            uint32_t allow_grp,
                                                             uint32_t *__restrict__ flag,
                                                             const uint32_t *__restrict__ first_ev,
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
@@ -2028,7 +2080,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   // k_crc_any's alone (the per-record body ran 57-62 % on them)
   const uint32_t mode = !unpacked                   ? kSegPacked
                         : !unsorted && gsum <= 0    ? kSegGapped
-                        : 2 * csum >= n             ? kSegFallbackGrp
+                        : allow_grp && 2 * csum >= n ? kSegFallbackGrp
                                                     : kSegFallback;
   if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
   if (mode == kSegGapped)
@@ -2067,8 +2119,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
                                                       const uint32_t *__restrict__ unit_raw,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken,
-                                                      uint32_t flags, uint32_t grp_lg,
-                                                      const DeviceTables *__restrict__ tables) {
+                                                      uint32_t flags, const DeviceTables *__restrict__ tables) {
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
   constexpr uint32_t kUnitRows = 1u << (kU - 10);
   __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024];
@@ -2092,25 +2143,19 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks)
     *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : 0u;
   __syncthreads();
-  if (mode == kSegFallback || mode == kSegFallbackGrp) {
+  if (mode == kSegFallback) {
     // the stream did not take the batch: k_crc_any's work over every message,
     // in this launch (round 3 launched k_crc_any after the combine, ~5 us a
     // call even when it exits at once).  The tables above are not used: the
-    // bodies fill their own over them, after the barrier.  kSegFallbackGrp:
-    // k_crc_grp's work first (its hand-out counter past its 8 KiB sh512
-    // table), then the k_crc_any sweep over the records it skipped (fast_mask
-    // 4095).  (One call site of crc_any_body: two inlined copies spilled.)
-    static_assert(kFastLdsBytes / 4 + 2048 + 1 <= (kSegRs + kSegIv) * 1024, "k_crc_grp's LDS fits the combine's");
-    const bool grp = mode == kSegFallbackGrp;
-    if (grp) {
-      crc_grp_body<true, false>(tl, tl[kFastLdsBytes / 4 + 2048], base, offs, lens, 0, 0, flags, n, grp_lg, crc_out,
-                                nullptr, nullptr, tables, nullptr, 0);
-      __syncthreads();
-    }
-    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, grp ? 4095u : 0u, 0u, crc_out, nullptr, nullptr, tables,
-                       nullptr, 0);
+    // body fills its own over them, after the barrier.
+    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, 0u, 0u, crc_out, nullptr, nullptr, tables, nullptr, 0);
     return;
   }
+  // kSegFallbackGrp: k_crc_grp and the k_crc_any sweep, launched after this
+  // kernel and gated on the mode word, take the batch.  (Round 5 first ran
+  // k_crc_grp's body here, before the sweep: the combine then faulted on the
+  // plain fallback and took 34 ms for 1M aligned records, profiles/r5/r5d/.)
+  if (mode == kSegFallbackGrp) return;
   const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni(threadIdx.x >> 6);
@@ -2140,22 +2185,29 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
     if (e >> 9) y = seg_lds_tmul(ti + kSegIvD3 * 1024u, y);
     return y ^ 0xFFFFFFFFu;
   };
-  if (mode == kSegGapped) {  // record j = events 2j (s_j) and 2j+1 (e_j), one record a lane
+  if (mode == kSegGapped) {
+    // record j = [s_j, e_j), events 2j and 2j+1, one record a lane.  The
+    // stream zeroed the gap bytes and left H at e_j (2j+1) and s_0 (0): H(s_j)
+    // is H(e_{j-1}) shifted by the rows between them in one unit, else 0
+    // (k_seg_stream's kGap notes)
     for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
-      uint64_t xa[kSub];
-      uint32_t ln[kSub], ha[kSub], hb[kSub];
+      uint64_t xa[kSub], xe[kSub];
+      uint32_t ln[kSub], he[kSub], hb[kSub];
 #pragma unroll
       for (int p = 0; p < kSub; p++) {
-        const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1;
+        const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1, jp = jj ? jj - 1 : 0;
         xa[p] = (uint64_t)base + offs[jj] - geo.a0;
         ln[p] = lens[jj];
-        ha[p] = ev_h[2 * jj];
+        xe[p] = (uint64_t)base + offs[jp] + lens[jp] - geo.a0;
+        he[p] = ev_h[jj ? 2 * jj - 1 : 0];
         hb[p] = ev_h[2 * jj + 1];
       }
 #pragma unroll
       for (int p = 0; p < kSub; p++) {
         const uint64_t j = c + 64u * p + lane;
-        if (j < n) crc_out[j] = rec_crc(xa[p], ha[p], xa[p] + ln[p], hb[p]);
+        uint32_t ha = he[p];  // j == 0: H(s_0) itself
+        if (j) ha = (xe[p] >> kU) == (xa[p] >> kU) ? rsh(he[p], (uint32_t)((xa[p] >> 10) - (xe[p] >> 10))) : 0u;
+        if (j < n) crc_out[j] = rec_crc(xa[p], ha, xa[p] + ln[p], hb[p]);
       }
     }
     return;
@@ -2306,7 +2358,7 @@ uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken, uint32_t lg_chunk) {
+                      uint32_t *taken, uint64_t grp_min, uint32_t lg_chunk) {
   if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
     return hipErrorInvalidValue;
   const uint64_t n = b.nblocks;
@@ -2320,10 +2372,21 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
                      plan_gx, plan_conf, first_ev);
+  // a batch large enough that two gated launches (exiting on their first load
+  // unless the stream chose kSegFallbackGrp, ~2-3 us each) are small against it
+  // (grp_min: HC_SEG_GRP_MIN, default kSegGrpFallbackMin)
+  const uint32_t allow_grp = n >= grp_min ? 1u : 0u;
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
-                     plan_gx, plan_conf, plan_wgs, flag, first_ev, unit_raw, ev_h, b.tables);
+                     plan_gx, plan_conf, plan_wgs, allow_grp, flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
-                     b.crc_out, st, taken, b.flags, grp_lg_chunk(n, grid, 0), b.tables);
+                     b.crc_out, st, taken, b.flags, b.tables);
+  if (allow_grp) {
+    hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
+                       b.flags, n, grp_lg_chunk(n, grid, 0), b.crc_out, nullptr, nullptr, b.tables, nullptr, 0,
+                       flag);
+    hipLaunchKernelGGL(k_crc_any<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
+                       b.flags, n, 4095u, 0u, b.crc_out, nullptr, nullptr, b.tables, nullptr, 0, flag);
+  }
   return hipGetLastError();
 }
 

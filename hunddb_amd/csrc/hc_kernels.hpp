@@ -101,18 +101,23 @@ uint64_t md5_workspace_bytes(uint64_t n);
 hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s);
 hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
-// Packed whole-message batches (off[i+1] = off[i] + len[i], HC_F_MESSAGES) as
-// one stream over their span (k_seg_*, hc_kernels.hip).  max_units bounds the
-// span's 16 KiB units (seg_max_units of a byte bound on the span); ws holds
-// seg_workspace_bytes(n, max_units) bytes.  A batch that is not packed, is
-// larger than the bound, holds records under ~64 B or over 16 MiB raises ws[0]
-// on the device, and k_seg_combine runs k_crc_any's work over the batch instead
-// (the same launch: the dispatch is three kernels whichever path is taken).
+// Whole-message batches (HC_F_MESSAGES) as one stream over their span
+// (k_seg_*, hc_kernels.hip): records back to back (off[i+1] = off[i] +
+// len[i]), or sorted with gaps of at most a quarter of the payload between
+// them.  max_units bounds the span's 16 KiB units (seg_max_units of a byte
+// bound on the span); ws holds seg_workspace_bytes(n, max_units) bytes.  A
+// batch the stream refuses (out of order or overlapping, larger than the
+// bound, records under ~64 B or over 16 MiB) sets ws[0] on the device and
+// k_seg_combine runs k_crc_any's work over it in the same launch; from grp_min
+// records on, a refused batch of mostly aligned 4 KiB-multiple records goes to
+// k_crc_grp + the k_crc_any sweep, two launches after the combine that exit at
+// once unless ws[0] says so.
 uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
-// taken (optional, device word): 1 when the stream took the batch, else 0.
+constexpr uint64_t kSegGrpFallbackMin = 1ull << 18;  // grp_min's default (HC_SEG_GRP_MIN)
+// taken (optional, device word): 1 packed, 2 gapped, 3 k_crc_grp fallback, 0 k_crc_any fallback.
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken = nullptr, uint32_t lg_chunk = 7);
+                      uint32_t *taken = nullptr, uint64_t grp_min = kSegGrpFallbackMin, uint32_t lg_chunk = 7);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
                                  hipStream_t s);
 

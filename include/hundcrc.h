@@ -344,7 +344,7 @@ int hc_debug_seg_taken(void);
  * call that needs one (a getenv racing with a Go os.Setenv would be a data
  * race): HC_DEVICE, HC_SEG_MIN_MSGS, HC_COPY_THREADS, HC_WAL_MIN_RANGE,
  * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
- * HC_FORCE_GPU, HC_INJECT_FAIL.  hc_debug_set changes one of them afterwards
+ * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN.  hc_debug_set changes one of them afterwards
  * (tests and tools); value NULL restores the compiled default.  HC_OK, or
  * HC_E_ARG for an unknown name. */
 int hc_debug_set(const char *name, const char *value);

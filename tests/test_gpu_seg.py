@@ -382,12 +382,15 @@ def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
     check(torch, hc, oracle, host, buf, off[p], lens[p], None)
 
 
-def test_seg_fallback_runs_crc_grp_on_aligned_records(cuda, hc, oracle, seg_all):
+def test_seg_fallback_runs_crc_grp_on_aligned_records(knobs, cuda, hc, oracle, seg_all):
     """a whole-message batch the stream refuses whose
     records are mostly 16-B aligned 4 KiB multiples (out of order, or far
-    apart) runs k_crc_grp's body first inside k_seg_combine, then the k_crc_any
-    sweep over the rest ("fallback_grp"); under half of them: k_crc_any alone.
-    Every word against the oracle."""
+    apart) goes to k_crc_grp and the k_crc_any sweep over the rest, launched
+    after the combine and gated on the stream's mode word ("fallback_grp");
+    under half of them: k_crc_any alone inside the combine.  Batches from
+    HC_SEG_GRP_MIN records (2^18; 1000 here) may take it, smaller ones never
+    do.  Every word against the oracle."""
+    knobs.setenv("HC_SEG_GRP_MIN", "1000")
     torch = cuda
     rng = np.random.default_rng(41)
     n = 6000
@@ -417,4 +420,7 @@ def test_seg_fallback_runs_crc_grp_on_aligned_records(cuda, hc, oracle, seg_all)
     assert hc.seg_path() == "fallback"
     mis = off[p] + np.uint64(4)  # misaligned 4 KiB multiples (sizes stay in the buffer: -4 from each)
     check(torch, hc, oracle, host, buf, mis, lens[p] - np.uint64(4096), None)
+    assert hc.seg_path() == "fallback"
+    knobs.setenv("HC_SEG_GRP_MIN", str(n + 1))  # under the threshold: k_crc_any in the combine
+    check(torch, hc, oracle, host, buf, off[p], lens[p], None)
     assert hc.seg_path() == "fallback"
