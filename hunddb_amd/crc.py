@@ -651,21 +651,23 @@ def debug_set(name: str, value=None) -> None:
 def seg_path():
     """How this thread's last device batch of whole messages was hashed:
     "packed" (the packed-record stream over records back to back), "gapped"
-    (the same stream over sorted records with gaps), "fallback_grp" (the
-    stream's fallback: k_crc_grp, then k_crc_any over what it skipped) or
-    "fallback" (k_crc_any alone, or not offered to the stream).  Synchronizes
-    the device; tests and tools."""
+    (the same stream over sorted records with gaps of at most 64 B, which the
+    combine hashes itself), "gapped_wide" (sorted, wider gaps, zeroed in the
+    stream), "fallback_grp" (the stream's fallback for aligned 4 KiB-multiple
+    records: k_crc_grp) or "fallback" (k_crc_any, or not offered to the
+    stream).  Synchronizes the device; tests and tools."""
     r = int(_lib().hc_debug_seg_taken())
     if r < 0:
         raise HundCRCError(r, "seg_taken")
-    return {1: "packed", 2: "gapped", 3: "fallback_grp"}.get(r, "fallback")
+    return {1: "packed", 2: "gapped_wide", 3: "fallback_grp", 4: "gapped"}.get(r, "fallback")
 
 
 def seg_mode():
-    """"packed" or "gapped" when the packed-record stream took this thread's
-    last device batch of whole messages, else None (synchronizes the device)."""
+    """"packed" or "gapped" (either gap width) when the packed-record stream
+    took this thread's last device batch of whole messages, else None
+    (synchronizes the device)."""
     p = seg_path()
-    return p if p in ("packed", "gapped") else None
+    return {"packed": "packed", "gapped": "gapped", "gapped_wide": "gapped"}.get(p)
 
 
 def seg_taken() -> bool:

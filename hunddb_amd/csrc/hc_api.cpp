@@ -1415,7 +1415,7 @@ int hc_debug_seg_taken(void) {
   if (hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(&v, g_dev[dev].seg_last, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return HC_E_HIP;
-  return v <= 3 ? (int)v : 0;
+  return v <= 4 ? (int)v : 0;
 }
 
 int hc_debug_set(const char *name, const char *value) { return hc::knob_set(name, value) ? HC_OK : HC_E_ARG; }

@@ -183,6 +183,7 @@ struct SegTables {
   uint32_t ones[1024];
   uint32_t rs[kSegRs][4][256];
   uint32_t iv[kSegIv][4][256];
+  uint32_t sh1[256];  // shift(v, 1): the byte-at-a-time (Sarwate) step, k_seg_combine's small gaps
 };
 
 inline void build_seg_tables(SegTables &t) {
@@ -214,6 +215,8 @@ inline void build_seg_tables(SegTables &t) {
     fill(t.iv[kSegIvD2 + v - 1], ip[64 * v]);
   }
   fill(t.iv[kSegIvD3], ip[512]);
+  const Mat32 s1 = shift_mat(g, 1);
+  for (uint32_t v = 0; v < 256; v++) t.sh1[v] = mat_apply(s1, v);
   uint32_t c = 0xFFFFFFFFu;
   for (int d = 1; d <= 1024; d++) {
     c = g.shift_bytes(c, 1);

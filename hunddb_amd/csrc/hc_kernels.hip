@@ -40,10 +40,11 @@ namespace hc {
 namespace {
 
 // The mode word k_seg_stream stores for its batch:
-// kSegFallbackGrp is the fallback for a batch whose records are mostly 16-B
-// aligned 4 KiB multiples (k_crc_grp's blocks): k_crc_grp and the k_crc_any
-// sweep, launched after the combine with this word as their gate.
-constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2, kSegFallbackGrp = 3;
+// kSegFallbackGrp is the fallback for a batch whose records are all 16-B
+// aligned 4 KiB multiples (k_crc_grp's blocks): k_crc_grp, launched after the
+// combine with this word as its gate.
+// kSegGapSmall: sorted records whose gaps are all at most kSegSmallGap bytes.
+constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2, kSegFallbackGrp = 3, kSegGapSmall = 4;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -1095,10 +1096,8 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_any(
     uint64_t stride, uint32_t ulen, uint32_t flags, uint64_t nblocks, uint32_t fast_mask, uint32_t lg_chunk,
     uint32_t *__restrict__ crc_out, uint32_t *__restrict__ bad_bitmap,
     unsigned long long *__restrict__ first_bad, const DeviceTables *__restrict__ tables,
-    const unsigned long long *skip_slot = nullptr, uint64_t skip_tag = 0,
-    const uint32_t *__restrict__ gate = nullptr) {
+    const unsigned long long *skip_slot = nullptr, uint64_t skip_tag = 0) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + 1];
-  if (gate && *gate != kSegFallbackGrp) return;  // the packed-record stream's fallback only (launch_seg)
   crc_any_body<kSmallLanes>(lds, base, offs, lens, stride, ulen, flags, nblocks, fast_mask, lg_chunk, crc_out,
                             bad_bitmap, first_bad, tables, skip_slot, skip_tag);
 }
@@ -1643,6 +1642,8 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 //                  shift by re_b - b (SegTables: 6 table multiplies a record).
 constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups (the kernels take it as kU)
 constexpr uint32_t kSegMaxRecord = 1u << 24;  // longest record the stream takes (16 MiB)
+constexpr uint64_t kSegMaxGap = 1u << 22;     // longest gap between two records it takes (4 MiB)
+constexpr uint64_t kSegSmallGap = 64;         // longest gap k_seg_combine hashes itself (kSegGapSmall)
 constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's largest grid: one "bad" slot per workgroup
 constexpr uint32_t kSegPlanWgs = 2048;       // its default grid cap (grid-stride beyond; r4e: 13.5 vs 16.8 us at 2M events)
 
@@ -1670,8 +1671,8 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 // e_{j-1} and s_j coincide, so its packed number is (first_ev[u] + 1) >> 1.
 // Workgroup w writes plan_bad[w]: bit 0 when its records find the batch not
 // packed or with more than 64 packed events in one 4 KiB group (records under
-// ~64 B), bit 1 when they find records out of order or overlapping, or more
-// than 64 gapped events in a group; both when the span exceeds max_units, a
+// ~64 B), bit 1 when they find records out of order or overlapping, a gap over
+// kSegMaxGap, or more than 64 gapped events in a group; both when the span exceeds max_units, a
 // record exceeds kSegMaxRecord or lies outside [s_0, pend].  plan_gx[w] =
 // sum over its records of 4 * (gap before it) - len: the stream takes a gapped
 // batch only when the grid's sum is <= 0 (gap bytes at most a quarter of the
@@ -1697,21 +1698,34 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
     conf += ((((uintptr_t)base + offs[j]) & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
   }
   const SegGeo g = seg_geo<kU>(base, offs, lens, n);
-  uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 3u : 0u;
+  uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 15u : 0u;
+  const uint64_t s0 = (uint64_t)base + offs[0];
   long long gx = 0;
   auto grp = [&](uint64_t p) { return (p - g.a0) >> 12; };
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n && bad != 3u; j += step) {
+  // bits: 1 not packed (or a packed group of 65 events), 2 not the zeroed-gap
+  // mode (out of order, overlapping, a gap over kSegMaxGap, 65 of the 2n
+  // events in a group), 4 a gap over kSegSmallGap, 8 not the small-gap mode
+  // (out of order, overlapping, 65 of its n + 1 events -- record ends -- in a
+  // group).  A thread stops when no mode is left.
+  auto none_left = [](uint32_t b) { return (b & 1u) && (b & 2u) && (b & 12u); };
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n && !none_left(bad); j += step) {
     const uint64_t s = (uint64_t)base + offs[j], l = lens[j], e = s + l;
     if (l > kSegMaxRecord || s < g.a0 || e > g.pend) {  // k_seg_combine's unit chain stays <= 1025 units
-      bad = 3u;
+      bad = 15u;
       break;
     }
     uint64_t ulo = 0;
     if (j > 0) {
       const uint64_t sp = (uint64_t)base + offs[j - 1], ep = sp + lens[j - 1];
       if (s != ep) bad |= 1u;
-      if (s < ep) bad |= 2u;
+      // a gap over kSegMaxGap also refuses the gapped mode: first_ev is filled
+      // by each record for the units back to its predecessor's end, which a
+      // batch out of order would otherwise make O(n x units) writes (1M
+      // shuffled 4 KiB records: 33 ms, profiles/r5/r5e/)
+      if (s < ep || s - ep > kSegMaxGap) bad |= 2u;
+      if (s < ep) bad |= 8u;
+      if (s > ep + kSegSmallGap) bad |= 4u;
       gx += 4 * (long long)(s >= ep ? s - ep : 0);
       ulo = ((ep - g.a0) >> kU) + 1;
     }
@@ -1722,7 +1736,9 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
       const uint64_t sq = (uint64_t)base + offs[j - 32];
       if (grp(s) == grp(sq) || grp(e) == grp(sq + lens[j - 32])) bad |= 2u;
     }
-    if (bad == 3u) break;
+    if (j >= 64 && grp(e) == grp((uint64_t)base + offs[j - 64] + lens[j - 64])) bad |= 8u;  // e_j vs e_{j-64}
+    if (j == 63 && grp(e) == grp(s0)) bad |= 8u;  // e_63 vs s_0 (event 0)
+    if (none_left(bad)) break;
     const uint64_t us = (s - g.a0) >> kU, ue = (e - g.a0) >> kU;
     for (uint64_t u = ulo; u <= us; u++) first_ev[u] = (uint32_t)(2 * j);
     for (uint64_t u = us + 1; u <= ue; u++) first_ev[u] = (uint32_t)(2 * j + 1);
@@ -1747,7 +1763,7 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
 // batch (off[] only, first_ev converted).  (Its timing-only builds -- rows
 // XOR-folded, or no event work at all -- are in git history:
 // tools/ab_hc_kernels.hip, up to commit 61a2e0e.)
-template <bool kGap, uint32_t kU>
+template <uint32_t kMode, uint32_t kU>
 __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next, const uint32_t (&col)[32],
                                                 const uint8_t *base, const uint64_t *__restrict__ offs,
                                                 const uint32_t *__restrict__ lens, uint64_t n, uint32_t lg_chunk,
@@ -1755,6 +1771,8 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
                                                 uint32_t *__restrict__ ev_h) {
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
+  constexpr bool kGap = kMode == kSegGapped;     // the 2n events s_j, e_j; gap bytes zeroed
+  constexpr bool kEnds = kMode == kSegGapSmall;  // the n + 1 events s_0, e_0 .. e_{n-1}
   const uint32_t r4 = (lane & 31u) << 2;
   const uint32_t B0 = r4, B1 = r4 | 128u, B2 = 65536u | r4, B3 = 65536u | 128u | r4;
   const uint32_t S4base = kLdsMainBytes + ((lane & 3u) << 2);
@@ -1805,8 +1823,10 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   // the first event at or after unit u's start, in this body's numbering
   auto fev = [&](uint64_t u_) -> uint64_t {
-    const uint32_t f = first_ev[u_];
-    return kGap ? (uint64_t)f : (uint64_t)((f + 1u) >> 1);
+    const uint32_t f = first_ev[u_];  // (the plan's numbering is the 2n one)
+    if constexpr (kGap) return f;
+    if constexpr (kEnds) return f ? (uint64_t)(f >> 1) + 1 : 0;
+    return (uint64_t)((f + 1u) >> 1);
   };
   // window: the positions of events f .. f+63, one per lane (a group holds at most 64)
   struct Win {
@@ -1815,7 +1835,16 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
   };
   auto win_issue = [&](uint64_t f) -> Win {
     Win w;
-    if constexpr (!kGap) {
+    if constexpr (kEnds) {  // event k >= 1 is e_{k-1} = off[k-1] + len[k-1]; event 0 is s_0
+      const uint64_t r0 = f ? (f - 1 < n ? f - 1 : n) : 0;
+      const uint64_t cnt = n - r0;
+      const uint32_t rel = f ? lane : (lane ? lane - 1 : 0);
+      const __amdgpu_buffer_rsrc_t ro = buf_range(offs + r0, (uint32_t)(cnt < 64 ? cnt * 8 : 512));
+      const __amdgpu_buffer_rsrc_t rl = buf_range(lens + r0, (uint32_t)(cnt < 64 ? cnt * 4 : 256));
+      w.o = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(ro, rel * 8u, 0, 0));
+      w.l = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, rel * 4u, 0, 0);
+      if (f == 0 && lane == 0) w.l = 0;
+    } else if constexpr (!kGap) {
       const uint64_t fc = f < n ? f : n;
       const uint64_t cnt = n - fc;
       const __amdgpu_buffer_rsrc_t r = buf_range(offs + fc, (uint32_t)(cnt < 64 ? cnt * 8 : 512));
@@ -1835,6 +1864,7 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
   auto win_pos = [&](Win v, uint64_t f) -> uint64_t {
     const uint64_t j = f + lane;
     const uint64_t p = (uint64_t)base + (((uint64_t)v.o.y << 32) | v.o.x);
+    if constexpr (kEnds) return j <= n ? p + v.l : ~0ull;
     if constexpr (!kGap) return j < n ? p : j == n ? geo.pend : ~0ull;
     return j < 2 * n ? p + ((j & 1u) ? v.l : 0u) : ~0ull;
   };
@@ -2068,6 +2098,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   }
   const int unpacked = __syncthreads_or((int)(bad & 1u));
   const int unsorted = __syncthreads_or((int)(bad & 2u));  // (also orders the s_gx / s_conf stores)
+  const int not_small = __syncthreads_or((int)(bad & 12u));
   long long gsum = 0;
   uint64_t csum = 0;
 #pragma unroll
@@ -2075,18 +2106,21 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     gsum += s_gx[w];
     csum += s_conf[w];
   }
-  // the fallback: k_crc_grp's body first when at least half of the records are
-  // its blocks (aligned 4 KiB multiples out of order, or far apart), else
-  // k_crc_any's alone (the per-record body ran 57-62 % on them)
+  // the fallback: k_crc_grp when every record is one of its blocks (16-B
+  // aligned 4 KiB multiples, out of order or far apart; ADVICE r4: the
+  // per-record body ran 57-62 % on them), else k_crc_any's work in the combine
   const uint32_t mode = !unpacked                   ? kSegPacked
+                        : !not_small && gsum <= 0   ? kSegGapSmall
                         : !unsorted && gsum <= 0    ? kSegGapped
-                        : allow_grp && 2 * csum >= n ? kSegFallbackGrp
+                        : allow_grp && csum == n    ? kSegFallbackGrp
                                                     : kSegFallback;
   if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
-  if (mode == kSegGapped)
-    seg_stream_body<true, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
+  if (mode == kSegGapSmall)
+    seg_stream_body<kSegGapSmall, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
+  else if (mode == kSegGapped)
+    seg_stream_body<kSegGapped, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
   else if (mode == kSegPacked)
-    seg_stream_body<false, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
+    seg_stream_body<kSegPacked, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
 }
 
 __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) {
@@ -2122,10 +2156,11 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
                                                       uint32_t flags, const DeviceTables *__restrict__ tables) {
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
   constexpr uint32_t kUnitRows = 1u << (kU - 10);
-  __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024];
-  {  // rs and iv are contiguous in SegTables: every load issued before the first store
+  __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024 + 256];
+  {  // rs, iv and sh1 are contiguous in SegTables: every load issued before the first store
     static_assert(offsetof(SegTables, iv) == offsetof(SegTables, rs) + sizeof(SegTables::rs), "rs, iv adjacent");
-    constexpr uint32_t kQ = (kSegRs + kSegIv) * 256, kPer = (kQ + 1023) / 1024;  // uint4s; per thread
+    static_assert(offsetof(SegTables, sh1) == offsetof(SegTables, iv) + sizeof(SegTables::iv), "iv, sh1 adjacent");
+    constexpr uint32_t kQ = (kSegRs + kSegIv) * 256 + 64, kPer = (kQ + 1023) / 1024;  // uint4s; per thread
     const uint4 *src = reinterpret_cast<const uint4 *>(&st->rs[0][0][0]);
     uint4 t[kPer];
 #pragma unroll
@@ -2141,7 +2176,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   }
   const uint32_t mode = *flag;
   if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks)
-    *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : 0u;
+    *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : mode == kSegGapSmall ? 4u : 0u;
   __syncthreads();
   if (mode == kSegFallback) {
     // the stream did not take the batch: k_crc_any's work over every message,
@@ -2151,8 +2186,8 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
     crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, 0u, 0u, crc_out, nullptr, nullptr, tables, nullptr, 0);
     return;
   }
-  // kSegFallbackGrp: k_crc_grp and the k_crc_any sweep, launched after this
-  // kernel and gated on the mode word, take the batch.  (Round 5 first ran
+  // kSegFallbackGrp: k_crc_grp, launched after this kernel and gated on the
+  // mode word, takes the batch.  (Round 5 first ran
   // k_crc_grp's body here, before the sweep: the combine then faulted on the
   // plain fallback and took 34 ms for 1M aligned records, profiles/r5/r5d/.)
   if (mode == kSegFallbackGrp) return;
@@ -2162,6 +2197,15 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
   auto rsh = [&](uint32_t v, uint32_t rows) {  // rows in [0, 16]
     return rows ? seg_lds_tmul(tl + (rows - 1u) * 1024u, v) : v;
+  };
+  auto inv_shift = [&](uint32_t y, uint32_t d) -> uint32_t {  // shift(y, -d), d in [1, 1024]: octal digits of d - 1
+    const uint32_t e = d - 1u;
+    const uint32_t *ti = tl + kIv0;
+    y = seg_lds_tmul(ti + (e & 7u) * 1024u, y);
+    if ((e >> 3) & 7u) y = seg_lds_tmul(ti + (kSegIvD1 - 1u + ((e >> 3) & 7u)) * 1024u, y);
+    if ((e >> 6) & 7u) y = seg_lds_tmul(ti + (kSegIvD2 - 1u + ((e >> 6) & 7u)) * 1024u, y);
+    if (e >> 9) y = seg_lds_tmul(ti + kSegIvD3 * 1024u, y);
+    return y;
   };
   // the record [a, b), with x = offsets from A0 and H from the stream
   auto rec_crc = [&](uint64_t xa, uint32_t ha, uint64_t xb, uint32_t hb) -> uint32_t {
@@ -2176,15 +2220,57 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
       for (uint64_t u = ua + 1; u < ub; u++) v = seg_lds_tmul(tl + (kUnitRows - 1u) * 1024u, v) ^ unit_raw[u];
       v = rsh(v, rb - (uint32_t)ub * kUnitRows);
     }
-    uint32_t y = hb ^ v;
-    const uint32_t e = db - 1u;  // inverse shift by db = 1 + e: octal digits of e
-    const uint32_t *ti = tl + kIv0;
-    y = seg_lds_tmul(ti + (e & 7u) * 1024u, y);
-    if ((e >> 3) & 7u) y = seg_lds_tmul(ti + (kSegIvD1 - 1u + ((e >> 3) & 7u)) * 1024u, y);
-    if ((e >> 6) & 7u) y = seg_lds_tmul(ti + (kSegIvD2 - 1u + ((e >> 6) & 7u)) * 1024u, y);
-    if (e >> 9) y = seg_lds_tmul(ti + kSegIvD3 * 1024u, y);
-    return y ^ 0xFFFFFFFFu;
+    return inv_shift(hb ^ v, db) ^ 0xFFFFFFFFu;
   };
+  if (mode == kSegGapSmall) {
+    // record j = [s_j, e_j); the stream left H at s_0 (event 0) and at every
+    // record end e_j (event j + 1) over the span's bytes, gaps included.  H(s_j)
+    // from H(e_{j-1}): shifted by the rows between them, plus the gap bytes
+    // [p, s_j) hashed here byte by byte (<= kSegSmallGap) and shifted to s_j's
+    // row end; p = e_{j-1}, or s_j's unit start when the gap crosses into it
+    // (then H(e_{j-1}) belongs to another unit and drops out).
+    const uint32_t *sh1 = tl + (kSegRs + kSegIv) * 1024;
+    for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
+      uint64_t xa[kSub], xe[kSub];
+      uint32_t ln[kSub], he[kSub], hb[kSub];
+#pragma unroll
+      for (int p = 0; p < kSub; p++) {
+        const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1, jp = jj ? jj - 1 : 0;
+        xa[p] = (uint64_t)base + offs[jj] - geo.a0;
+        ln[p] = lens[jj];
+        xe[p] = (uint64_t)base + offs[jp] + lens[jp] - geo.a0;
+        he[p] = ev_h[jj];
+        hb[p] = ev_h[jj + 1];
+      }
+#pragma unroll
+      for (int p = 0; p < kSub; p++) {
+        const uint64_t j = c + 64u * p + lane;
+        if (j >= n) continue;
+        uint32_t ha = he[p];  // j == 0: H(s_0) itself
+        if (j) {
+          const bool same = (xe[p] >> kU) == (xa[p] >> kU);
+          const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
+          uint32_t r = 0;  // raw(gap bytes [gp, s_j)), a byte at a time, from aligned words
+          const uint64_t w0 = gp & ~3ull;
+          const __amdgpu_buffer_rsrc_t rg = buf_range(reinterpret_cast<const void *>(geo.a0 + w0),
+                                                      (uint32_t)(xa[p] - w0));
+          for (uint64_t w = w0; w < xa[p]; w += 4) {
+            const uint32_t v = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rg, (uint32_t)(w - w0), 0, 0);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+              if (w + k >= gp && w + k < xa[p]) r = sh1[(r ^ (v >> (8 * k))) & 255u] ^ (r >> 8);
+          }
+          const uint32_t re = (uint32_t)(xa[p] >> 10) + 1u, d = (uint32_t)(((uint64_t)re << 10) - xa[p]);
+          // shift(r, d) = shift(shift(r, 1024), -(1024 - d))
+          uint32_t pg = seg_lds_tmul(tl, r);
+          if (d < 1024u) pg = inv_shift(pg, 1024u - d);
+          ha = (same ? rsh(he[p], (uint32_t)((xa[p] >> 10) - (xe[p] >> 10))) : 0u) ^ pg;
+        }
+        crc_out[j] = rec_crc(xa[p], ha, xa[p] + ln[p], hb[p]);
+      }
+    }
+    return;
+  }
   if (mode == kSegGapped) {
     // record j = [s_j, e_j), events 2j and 2j+1, one record a lane.  The
     // stream zeroed the gap bytes and left H at e_j (2j+1) and s_0 (0): H(s_j)
@@ -2372,21 +2458,18 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
                      plan_gx, plan_conf, first_ev);
-  // a batch large enough that two gated launches (exiting on their first load
-  // unless the stream chose kSegFallbackGrp, ~2-3 us each) are small against it
+  // a batch large enough that a gated launch (exiting on its first load unless
+  // the stream chose kSegFallbackGrp: 5 us under rocprofv3, r5e) is small against it
   // (grp_min: HC_SEG_GRP_MIN, default kSegGrpFallbackMin)
   const uint32_t allow_grp = n >= grp_min ? 1u : 0u;
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
                      plan_gx, plan_conf, plan_wgs, allow_grp, flag, first_ev, unit_raw, ev_h, b.tables);
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
                      b.crc_out, st, taken, b.flags, b.tables);
-  if (allow_grp) {
+  if (allow_grp)
     hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
                        b.flags, n, grp_lg_chunk(n, grid, 0), b.crc_out, nullptr, nullptr, b.tables, nullptr, 0,
                        flag);
-    hipLaunchKernelGGL(k_crc_any<true>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
-                       b.flags, n, 4095u, 0u, b.crc_out, nullptr, nullptr, b.tables, nullptr, 0, flag);
-  }
   return hipGetLastError();
 }
 

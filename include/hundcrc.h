@@ -333,11 +333,12 @@ int hc_last_launch(hc_launch_info *info);
 int hc_debug_tables(void *out, size_t cap);
 
 /* How this thread's last device batch of whole messages was hashed: 1 by the
- * packed-record stream (k_seg_*) as records back to back, 2 by
- * the same stream as sorted records with gaps between them, 3 by the stream's
- * fallback with k_crc_grp first (mostly aligned 4 KiB-multiple records out of
- * order), 0 by k_crc_any alone on the device or not offered to the stream;
- * synchronizes that device (tests and tools only). */
+ * packed-record stream (k_seg_*) as records back to back, 4 by
+ * the same stream as sorted records with gaps of at most 64 B between them, 2
+ * as sorted records with wider gaps (zeroed in the stream), 3 by k_crc_grp
+ * (the stream's fallback for aligned 4 KiB-multiple records out of order), 0
+ * by k_crc_any on the device or not offered to the stream; synchronizes that
+ * device (tests and tools only). */
 int hc_debug_seg_taken(void);
 
 /* The library reads its HC_* settings from the environment once, at the first

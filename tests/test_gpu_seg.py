@@ -281,9 +281,9 @@ def expected_mode(base, off, lens):
     """The plan's decision (k_seg_plan + k_seg_stream's prologue) restated:
     "packed" when every record starts where the previous one ends and no 4 KiB
     group (from the span's 1 KiB-aligned origin) holds 65 of the n + 1 events;
-    else "gapped" when the records are sorted and do not overlap, no group holds
-    65 of the 2n events s_j, e_j, and the gap bytes are at most a quarter of the
-    payload; else None (k_crc_any)."""
+    else "gapped" when the records are sorted and do not overlap, no gap is over
+    4 MiB, no group holds 65 of the 2n events s_j, e_j, and the gap bytes are at
+    most a quarter of the payload; else None (k_crc_any)."""
     s = np.uint64(base) + off.astype(np.uint64)
     e = s + lens.astype(np.uint64)
     pend = int(e[-1])
@@ -296,13 +296,32 @@ def expected_mode(base, off, lens):
         return len(ev) > 64 and bool((g[64:] == g[:-64]).any())
     if (s[1:] == e[:-1]).all() and not dense(np.r_[s, np.uint64(pend)]):
         return "packed"
-    if (s[1:] >= e[:-1]).all():
+    if (s[1:] >= e[:-1]).all() and (s[1:] - e[:-1] <= (1 << 22)).all():  # gaps up to kSegMaxGap (4 MiB)
         ev = np.empty(2 * len(s), dtype=np.uint64)
         ev[0::2], ev[1::2] = s, e
         gaps = int((s[1:] - e[:-1]).sum()) if len(s) > 1 else 0
         if not dense(ev) and 4 * gaps <= int(lens.astype(np.uint64).sum()):
             return "gapped"
     return None
+
+
+def expected_path(base, off, lens):
+    """seg_path() of a batch: "gapped" (every gap <= 64 B, the combine hashes
+    them, its n + 1 record-end events at most 64 per 4 KiB group) before
+    "gapped_wide" (the zeroed-gap stream over 2n events)."""
+    m = expected_mode(base, off, lens)
+    if m == "packed":
+        return m
+    s = np.uint64(base) + off.astype(np.uint64)
+    e = s + lens.astype(np.uint64)
+    if (s[1:] >= e[:-1]).all() and (s[1:] - e[:-1] <= 64).all() and len(s):
+        ev = np.r_[s[:1], e]
+        g = (ev - np.uint64(int(s[0]) & ~1023)) >> np.uint64(12)
+        dense = len(ev) > 64 and bool((g[64:] == g[:-64]).any())
+        gaps = int((s[1:] - e[:-1]).sum()) if len(s) > 1 else 0
+        if not dense and 4 * gaps <= int(lens.astype(np.uint64).sum()):
+            return "gapped"
+    return "gapped_wide" if m == "gapped" else m
 
 
 def gapped(lens, gaps, start):
@@ -326,8 +345,9 @@ def test_seg_gapped_wal_records(cuda, hc, oracle, seg_all, start):
     total = int(off[-1] + lens[-1]) + 64
     host = rng.integers(0, 256, total, dtype=np.uint8)
     buf = torch.from_numpy(host).cuda()
-    assert expected_mode(buf.data_ptr(), off, lens) == "gapped"
+    assert expected_path(buf.data_ptr(), off, lens) == "gapped"
     check(torch, hc, oracle, host, buf, off, lens, "gapped")
+    assert hc.seg_path() == "gapped"  # 17-B gaps: the combine hashes them
     assert "k_seg_stream" in hc.last_launch()["kernel"]
 
 
@@ -362,17 +382,27 @@ def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
     g2 = g.copy()
     g2[1:1 + (q - int(g.sum())) + 1] += 1           # one byte over a quarter: k_crc_any
     cases.append((L, g2))
+    big = np.full(20, 1 << 20, dtype=np.uint64)      # one 4 MiB gap (kSegMaxGap): gapped; one byte more: k_crc_any
+    bg = np.zeros(20, dtype=np.uint64)
+    bg[7] = 1 << 22
+    cases.append((big, bg))
+    bg2 = bg.copy()
+    bg2[7] += 1
+    cases.append((big, bg2))
     small = np.full(5000, 120, dtype=np.uint64)      # 32 records + 8-B gaps per 4 KiB: 64 events a group
     cases.append((small, np.full(5000, 8, np.uint64)))
     small2 = np.full(5000, 100, dtype=np.uint64)     # 34 records per group: 68 events, k_crc_any
     cases.append((small2, np.full(5000, 20, np.uint64)))
+    paths = set()
     for lens, gaps in cases:
         for start in (0, 3, 1024 - 1):
             off = gapped(lens, gaps, start)
             assert int(off[-1] + lens[-1]) <= total
             check(torch, hc, oracle, host, buf, off, lens, expected_mode(buf.data_ptr(), off, lens))
-    seen = {expected_mode(buf.data_ptr(), gapped(a, b, 0), a) for a, b in cases}
-    assert seen == {"packed", "gapped", None}, seen
+            want = expected_path(buf.data_ptr(), off, lens)
+            assert hc.seg_path() == (want or "fallback"), (want, hc.seg_path())
+            paths.add(want)
+    assert paths == {"packed", "gapped", "gapped_wide", None}, paths
     lens, gaps = cases[0]
     off = gapped(lens, gaps, 1)
     o = lens.copy()
@@ -384,12 +414,11 @@ def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
 
 def test_seg_fallback_runs_crc_grp_on_aligned_records(knobs, cuda, hc, oracle, seg_all):
     """a whole-message batch the stream refuses whose
-    records are mostly 16-B aligned 4 KiB multiples (out of order, or far
-    apart) goes to k_crc_grp and the k_crc_any sweep over the rest, launched
-    after the combine and gated on the stream's mode word ("fallback_grp");
-    under half of them: k_crc_any alone inside the combine.  Batches from
-    HC_SEG_GRP_MIN records (2^18; 1000 here) may take it, smaller ones never
-    do.  Every word against the oracle."""
+    records are all 16-B aligned 4 KiB multiples (out of order, or far apart)
+    goes to k_crc_grp, launched after the combine and gated on the stream's
+    mode word ("fallback_grp"); one record that is not: k_crc_any inside the
+    combine.  Batches from HC_SEG_GRP_MIN records (2^18; 1000 here) may take
+    it, smaller ones never do.  Every word against the oracle."""
     knobs.setenv("HC_SEG_GRP_MIN", "1000")
     torch = cuda
     rng = np.random.default_rng(41)
@@ -411,11 +440,7 @@ def test_seg_fallback_runs_crc_grp_on_aligned_records(knobs, cuda, hc, oracle, s
     check(torch, hc, oracle, bh, big, far, fl, None)
     assert hc.seg_path() == "fallback_grp"
     mixed = lens[p].copy()
-    k = rng.choice(n, int(0.4 * n), replace=False)
-    mixed[k] -= np.uint64(100)  # 40 % not 4 KiB multiples: k_crc_grp first, the sweep after
-    check(torch, hc, oracle, host, buf, off[p], mixed, None)
-    assert hc.seg_path() == "fallback_grp"
-    mixed[rng.choice(n, int(0.7 * n), replace=False)] -= np.uint64(7)  # most not: k_crc_any alone
+    mixed[n // 2] -= np.uint64(100)  # one record not a 4 KiB multiple: k_crc_any
     check(torch, hc, oracle, host, buf, off[p], mixed, None)
     assert hc.seg_path() == "fallback"
     mis = off[p] + np.uint64(4)  # misaligned 4 KiB multiples (sizes stay in the buffer: -4 from each)

@@ -8,7 +8,7 @@ source (CPU: hipcc cross-compiles):
   rows behind it stay in flight);
 * k_seg_stream's row folds and window waits count exactly the VMEM ops issued
   after the load they wait for (vmcnt(6): three rows, the event window, the
-  group's two stores; vmcnt(7) in the gapped loop, whose window is two loads),
+  group's two stores; vmcnt(7) in the two gapped loops, whose window is two loads),
   and no loop-latch register copies wait for refills
   (round 4 found hipcc copying the loop-carried rows at the latch after small
   unrelated edits; that shows as vmcnt(2)/vmcnt(3) waits before the header);
@@ -95,13 +95,14 @@ def _stream_loops(body):
 
 
 def test_seg_stream_waits_are_exact(isa):
-    """Two stream loops (round 5): the gapped one, whose event window is two
-    loads (off[] and len[]), folds at vmcnt(7); the packed one at vmcnt(6)."""
+    """Three stream loops (round 5): the small-gap and the zeroed-gap ones,
+    whose event windows are two loads (off[] and len[]), fold at vmcnt(7); the
+    packed one at vmcnt(6)."""
     _, bodies = isa
     (name,) = _find(bodies, "k_seg_stream")
     loops = _stream_loops(bodies[name])
-    assert len(loops) == 2, len(loops)
-    for (latch, loop), exact in zip(loops, (7, 6)):  # source order: the gapped body is instantiated first
+    assert len(loops) == 3, len(loops)
+    for (latch, loop), exact in zip(loops, (7, 7, 6)):  # source order of the instantiations
         w = _waits(loop)
         assert w.count(exact) >= 4, (exact, w)  # the four row folds
         assert not [x for x in w if x < exact - 1], (exact, w)  # no wait drains a refill or the window
