@@ -87,6 +87,13 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
          __builtin_amdgcn_readlane(v, 32) ^ __builtin_amdgcn_readlane(v, 48);
 }
 
+// max of v over the 64 lanes (wave-uniform result)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
+  return uni(v);
+}
+
 // Lane-0 side effects of a wave (CRC word, crc_out, verify atomics) issued with
 // exec = lane 0 inside one asm statement.  Written as plain `if (lane == 0)`
 // code these become branches around VMEM instructions, and the waitcnt pass
@@ -2250,15 +2257,34 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
         if (j) {
           const bool same = (xe[p] >> kU) == (xa[p] >> kU);
           const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
-          uint32_t r = 0;  // raw(gap bytes [gp, s_j)), a byte at a time, from aligned words
-          const uint64_t w0 = gp & ~3ull;
-          const __amdgpu_buffer_rsrc_t rg = buf_range(reinterpret_cast<const void *>(geo.a0 + w0),
-                                                      (uint32_t)(xa[p] - w0));
-          for (uint64_t w = w0; w < xa[p]; w += 4) {
-            const uint32_t v = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rg, (uint32_t)(w - w0), 0, 0);
+          // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes: as Z leading
+          // zeros and the gap, nw words ending at s_j (raw ignores leading
+          // zeros).  Word 0 is the dword at gp shifted up by Z bytes; word k
+          // the (unaligned) dword at gp + 4k - Z.  Every load is issued before
+          // the first is used (round 5's first build looped load -> hash per
+          // dword: 207 us of combine at 2M records, profiles/r5/r5h/); a dword
+          // that crosses the range's end reads as zero, so the range is the
+          // gap rounded up to a word (the bytes past s_j are the record's).
+          const uint32_t L = (uint32_t)(xa[p] - gp), nw = (L + 3u) >> 2, Z = 4u * nw - L;
+          const __amdgpu_buffer_rsrc_t rg =
+              buf_range(reinterpret_cast<const void *>(geo.a0 + gp), (L + 3u) & ~3u);
+          const uint32_t nwmax = wave_max_u32(nw);
+          uint32_t W[kSegSmallGap / 4];
 #pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-              if (w + k >= gp && w + k < xa[p]) r = sh1[(r ^ (v >> (8 * k))) & 255u] ^ (r >> 8);
+          for (uint32_t k = 0; k < kSegSmallGap / 4; k++)
+            W[k] = k < nwmax ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rg, k ? 4u * k - Z : 0u, 0, 0) : 0u;
+          W[0] <<= 8u * Z;
+          uint32_t r = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < kSegSmallGap / 4; k++) {
+            if (k >= nwmax) break;
+            uint32_t t = r, w = W[k];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              t = sh1[(t ^ w) & 255u] ^ (t >> 8);
+              w >>= 8;
+            }
+            r = k < nw ? t : r;
           }
           const uint32_t re = (uint32_t)(xa[p] >> 10) + 1u, d = (uint32_t)(((uint64_t)re << 10) - xa[p]);
           // shift(r, d) = shift(shift(r, 1024), -(1024 - d))
@@ -2456,16 +2482,22 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   // HC_SEG_PLAN_WGS overrides the plan's grid cap, up to kSegPlanMaxWgs (tuning sweeps)
   static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanWgs)));
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
+  // every launch checked: a later kernel must not run on a failed one's stale
+  // outputs (hipGetLastError reports the latest call, not the first failure)
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
                      plan_gx, plan_conf, first_ev);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   // a batch large enough that a gated launch (exiting on its first load unless
   // the stream chose kSegFallbackGrp: 5 us under rocprofv3, r5e) is small against it
   // (grp_min: HC_SEG_GRP_MIN, default kSegGrpFallbackMin)
   const uint32_t allow_grp = n >= grp_min ? 1u : 0u;
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
                      plan_gx, plan_conf, plan_wgs, allow_grp, flag, first_ev, unit_raw, ev_h, b.tables);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
                      b.crc_out, st, taken, b.flags, b.tables);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   if (allow_grp)
     hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
                        b.flags, n, grp_lg_chunk(n, grid, 0), b.crc_out, nullptr, nullptr, b.tables, nullptr, 0,

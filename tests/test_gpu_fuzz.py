@@ -148,7 +148,8 @@ N_FRAMING = 48 * SCALE
 
 @pytest.mark.parametrize("seed", range(N_FRAMING))
 def test_random_framing_round_trip(cuda, hc, oracle, seed):
-    """AddCRCsToData (host entry: GPU batch from 256 blocks, host below; device
+    """AddCRCsToData (host entry: a GPU batch at or above the GPU tests' 256-block
+    threshold -- conftest.py; production's is 2048 --, the host below it; device
     entry k_frame) on random payload sizes at random alignments, byte-exact vs
     the oracle; then ReadFromDisk over the framed image (host entry and the
     device k_unframe) at random start offsets and sizes, vs the oracle's
