@@ -2257,28 +2257,34 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
         if (j) {
           const bool same = (xe[p] >> kU) == (xa[p] >> kU);
           const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
-          // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes: as Z leading
-          // zeros and the gap, nw words ending at s_j (raw ignores leading
-          // zeros).  Word 0 is the dword at gp shifted up by Z bytes; word k
-          // the (unaligned) dword at gp + 4k - Z.  Every load is issued before
-          // the first is used (round 5's first build looped load -> hash per
-          // dword: 207 us of combine at 2M records, profiles/r5/r5h/); a dword
-          // that crosses the range's end reads as zero, so the range is the
-          // gap rounded up to a word (the bytes past s_j are the record's).
-          const uint32_t L = (uint32_t)(xa[p] - gp), nw = (L + 3u) >> 2, Z = 4u * nw - L;
-          const __amdgpu_buffer_rsrc_t rg =
-              buf_range(reinterpret_cast<const void *>(geo.a0 + gp), (L + 3u) & ~3u);
+          // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes, as nw words
+          // ending at s_j behind 4nw - L leading zeros (raw ignores them).  The
+          // words come from the aligned dwords D[i] at Bq + 4i, Bq = (s_j -
+          // 4nw) & ~3, bytes before gp cleared, by a funnel shift of sa = s_j & 3
+          // bytes.  Plain per-lane loads: a buffer resource is scalar, so one
+          // built from a per-lane address became a 64-pass waterfall loop per
+          // load (r5h/r5i: 233 / 369 us of combine at 2M records).  An aligned
+          // dword holding a span byte never leaves the span's pages; D[nw] is
+          // read only when it holds gap bytes (sa > 0).
+          const uint32_t L = (uint32_t)(xa[p] - gp), nw = (L + 3u) >> 2, sa = (uint32_t)xa[p] & 3u;
+          const uint64_t Bq = (xa[p] - 4u * nw) & ~3ull;
           const uint32_t nwmax = wave_max_u32(nw);
-          uint32_t W[kSegSmallGap / 4];
+          uint32_t D[kSegSmallGap / 4 + 1];
 #pragma unroll
-          for (uint32_t k = 0; k < kSegSmallGap / 4; k++)
-            W[k] = k < nwmax ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rg, k ? 4u * k - Z : 0u, 0, 0) : 0u;
-          W[0] <<= 8u * Z;
+          for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
+            D[i] = 0;
+            if (i > nwmax) continue;
+            const uint64_t ai = Bq + 4u * i;
+            if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
+              D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
+              if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
+            }
+          }
           uint32_t r = 0;
 #pragma unroll
           for (uint32_t k = 0; k < kSegSmallGap / 4; k++) {
             if (k >= nwmax) break;
-            uint32_t t = r, w = W[k];
+            uint32_t t = r, w = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sa);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
               t = sh1[(t ^ w) & 255u] ^ (t >> 8);

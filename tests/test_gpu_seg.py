@@ -391,15 +391,17 @@ def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
     cases.append((big, bg2))
     small = np.full(5000, 120, dtype=np.uint64)      # 32 records + 8-B gaps per 4 KiB: 64 events a group
     cases.append((small, np.full(5000, 8, np.uint64)))
-    small2 = np.full(5000, 100, dtype=np.uint64)     # 34 records per group: 68 events, k_crc_any
-    cases.append((small2, np.full(5000, 20, np.uint64)))
+    small2 = np.full(5000, 100, dtype=np.uint64)     # 34 records per group: 68 of the 2n events, but
+    cases.append((small2, np.full(5000, 20, np.uint64)))  # 34 record ends: the small-gap mode
+    small3 = np.full(5000, 50, dtype=np.uint64)      # 68 record ends per group: k_crc_any
+    cases.append((small3, np.full(5000, 10, np.uint64)))
     paths = set()
     for lens, gaps in cases:
         for start in (0, 3, 1024 - 1):
             off = gapped(lens, gaps, start)
             assert int(off[-1] + lens[-1]) <= total
-            check(torch, hc, oracle, host, buf, off, lens, expected_mode(buf.data_ptr(), off, lens))
             want = expected_path(buf.data_ptr(), off, lens)
+            check(torch, hc, oracle, host, buf, off, lens, "gapped" if want == "gapped_wide" else want)
             assert hc.seg_path() == (want or "fallback"), (want, hc.seg_path())
             paths.add(want)
     assert paths == {"packed", "gapped", "gapped_wide", None}, paths
