@@ -83,11 +83,15 @@ WORKLOADS = {
     # GetCRC of 1M aligned 4 KiB records in shuffled order: the
     # stream refuses them; its fallback runs k_crc_grp's body inside the combine
     "records4k_shuffled": (1_000_000, "records4k_shuffled", "weak"),
+    # 1M uniform 4092-B blocks back to back (config.go:241 allows any BlockSize >= 1024):
+    # not k_crc_grp's shape; their messages block[4:] on the stream's small-gap mode (round 5)
+    "blocks4092": (1_000_000, 4092, "weak"),
 }
 # the dominant kernel per workload (PMC passes)
 KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
              "records": "k_seg_stream", "records_gapped": "k_seg_stream",
-             "records4k_shuffled": "k_seg_combine"}  # else the streaming CRC kernel
+             "records4k_shuffled": "k_seg_combine", "blocks4092": "k_seg_stream"}  # else the streaming CRC kernel
+SEG_WORKLOADS = ("records", "records_gapped", "records4k_shuffled", "blocks4092")  # on k_seg_*: stream_mode
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
 
@@ -157,7 +161,7 @@ def pmc_traffic(args):
     if not exe:
         return None, "rocprofv3 not found"
     out = {}
-    kern = KERNEL_RE.get(WORKLOADS[args.workload][1], "k_crc_(grp|uni|fast)")
+    kern = KERNEL_RE.get(args.workload, "k_crc_(grp|uni|fast)")
     tmp = tempfile.mkdtemp(prefix="hc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
              "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off", "--settle", "0"]
@@ -775,7 +779,7 @@ def main(argv=None):
             raise RuntimeError(f"{world} RCCL ranks ran on {proof['distinct_devices']} distinct GPU(s): "
                                f"{[(i['rank'], i['host'], i['bus_id']) for i in proof['ranks']]}")
     info = crc.last_launch()
-    seg_mode = crc.seg_path() if bsize in ("records", "records_gapped", "records4k_shuffled") else False
+    seg_mode = crc.seg_path() if args.workload in SEG_WORKLOADS else False
     verify_clean = None
     if bsize == "verify":  # every stamped block must have verified clean
         verify_clean = int(first_bad.item()) == 2**63 - 1 and int(bitmap.abs().sum().item()) == 0
@@ -850,7 +854,7 @@ def main(argv=None):
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
                 **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine (the fallback for a "
                                    "batch the stream refuses runs inside the combine); traffic: k_seg_stream"}
-                   if bsize in ("records", "records_gapped", "records4k_shuffled") else {}),
+                   if args.workload in SEG_WORKLOADS else {}),
                 "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
                                  f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
                                  if traffic else f"null: {pmc_note}")}

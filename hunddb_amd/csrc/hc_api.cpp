@@ -229,6 +229,36 @@ uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::uniqu
   return d.seg_ws;
 }
 
+// Uniform device block batches that k_crc_grp cannot take (a length that is
+// not a 4 KiB multiple, e.g. config.go:241's BlockSize, or an address that is
+// not 16-B aligned), from HC_SEG_MIN_BLOCKS blocks: their messages block[4:]
+// lie 4 + stride - ulen bytes apart, which the stream's small-gap mode takes
+// (launch_seg_blocks); k_crc_any ran them at 57-62 % (round 4).
+uint64_t seg_min_blocks() { return (uint64_t)std::max<int64_t>(1, knob(kKnobSegMinBlocks)); }
+
+// The span bound of a batch at `base` (the allocation holding it), as k_seg_*'s unit count; 0 if unknown.
+uint64_t seg_units_for(const uint8_t *base) {
+  hipDeviceptr_t pb = nullptr;
+  size_t ps = 0;
+  if (hipMemGetAddressRange(&pb, &ps, const_cast<uint8_t *>(base)) != hipSuccess || !ps) return 0;
+  const uint64_t lo = reinterpret_cast<uintptr_t>(base) & ~uint64_t(1023);
+  return seg_max_units(reinterpret_cast<uintptr_t>(pb) + ps - lo);
+}
+
+// launch_seg_blocks with a kept or per-call workspace; false: not launched (no workspace)
+bool seg_blocks(DeviceState &d, const Batch &b, hipStream_t s, int grid, hipError_t &e) {
+  const uint64_t mu = seg_units_for(b.base);
+  if (!mu) return false;
+  const uint64_t need = seg_block_workspace_bytes(b.nblocks, mu, !b.crc_out);
+  std::unique_lock<std::mutex> lk;
+  uint32_t *ws = seg_cached_ws(d, s, need, lk), *own = nullptr;
+  if (!ws && hipMallocAsync(reinterpret_cast<void **>(&own), need, s) == hipSuccess) ws = own;
+  if (!ws) return false;
+  e = launch_seg_blocks(b, d.dseg, ws, mu, grid, s, d.seg_last);
+  if (own && hipFreeAsync(own, s) != hipSuccess && e == hipSuccess) e = hipErrorUnknown;
+  return true;
+}
+
 int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
              uint32_t ulen, uint64_t n, uint32_t *crc_out, uint32_t *bitmap, int64_t *first_bad,
              uint32_t flags, hipStream_t s, uint64_t bytes_hint, bool seg_ok = false) {
@@ -246,6 +276,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
   b.first_bad = reinterpret_cast<unsigned long long *>(first_bad);
   b.tables = d.dtab;
   if (n == 0) return HC_OK;
+  t_seg_dev = -1;  // set below when the batch goes to the stream
   const int fast_grid = d.cus;  // one 1024-thread, 144 KiB-LDS workgroup per CU
   const int gen_grid = d.cus;  // k_crc_any: same geometry as the streaming kernel
   hc_launch_info info{"k_crc_fast", 0, 0, bytes_hint, (uint32_t)fast_grid, kFastThreads,
@@ -261,6 +292,11 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
     } else if (fast) {
       e = launch_fast(b, fast_grid, s);
       info.fast_blocks = n;
+    } else if (seg_ok && ulen >= 4 && stride >= ulen && n >= seg_min_blocks() && n < 0x7FFFFFFFull &&
+               seg_blocks(d, b, s, fast_grid, e)) {
+      info.kernel = "k_seg_plan+k_seg_stream+k_seg_combine";
+      info.fast_blocks = n;
+      t_seg_dev = dev;
     } else {
       e = launch_general(b, 0, gen_grid, s);
       info.kernel = "k_crc_any";
@@ -280,11 +316,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
     // the stream's only output is crc_out (k_seg_combine): a batch without it
     // (verify or stamp only) takes k_crc_grp + k_crc_any
     if (seg_ok && (flags & kFlagMessages) && crc_out && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
-      hipDeviceptr_t pb = nullptr;
-      size_t ps = 0;
-      if (hipMemGetAddressRange(&pb, &ps, const_cast<uint8_t *>(base)) == hipSuccess && ps) {
-        const uint64_t lo = reinterpret_cast<uintptr_t>(base) & ~uint64_t(1023);
-        const uint64_t mu = seg_max_units(reinterpret_cast<uintptr_t>(pb) + ps - lo);
+      if (const uint64_t mu = seg_units_for(base)) {
         const uint64_t need = seg_workspace_bytes(n, mu);
         uint32_t *ws = seg_cached_ws(d, s, need, seg_lock);
         if (!ws && hipMallocAsync(reinterpret_cast<void **>(&seg_ws), need, s) == hipSuccess) ws = seg_ws;

@@ -2349,6 +2349,46 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   }
 }
 
+// A uniform block batch k_crc_grp refuses, on the message stream
+// (launch_seg_blocks): its messages block[4:ulen] as off/len arrays ...
+__global__ __launch_bounds__(256) void k_seg_block_msgs(uint64_t n, uint64_t stride, uint32_t ulen,
+                                                        uint64_t *__restrict__ moff, uint32_t *__restrict__ mlen) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    moff[j] = j * stride + 4u;
+    mlen[j] = ulen - 4u;
+  }
+}
+
+// ... and the blocks' outputs from the message CRCs: CheckBlockIntegrity's
+// compare (crc_util.go:88-100) into the bitmap and first_bad, then
+// AddCRCToBlockData's store (:21-33), as k_crc_any does them (the stored word
+// read before the stamp).  A wave takes 64 consecutive blocks: one bitmap
+// atomic per 32 with a bad block, one first_bad lowering per wave.
+__global__ __launch_bounds__(256) void k_seg_block_out(const uint8_t *base, uint64_t n, uint64_t stride,
+                                                       uint32_t flags, const uint32_t *__restrict__ crcs,
+                                                       uint32_t *__restrict__ bad_bitmap,
+                                                       unsigned long long *__restrict__ first_bad) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t c = w0 * 64u; c < n; c += nw * 64u) {
+    const uint64_t j = c + lane;
+    const bool in = j < n;
+    uint32_t *p = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(base) + (in ? j : 0) * stride);
+    const uint32_t crc = in ? crcs[j] : 0u;
+    if (first_bad) {
+      const uint32_t stored = in ? *p : 0u;
+      const uint64_t bad = __ballot(in && stored != crc);
+      if (bad) {  // wave-uniform
+        if (bad_bitmap && lane == 0 && (uint32_t)bad) atomicOr(bad_bitmap + (c >> 5), (uint32_t)bad);
+        if (bad_bitmap && lane == 32 && (bad >> 32)) atomicOr(bad_bitmap + (c >> 5) + 1, (uint32_t)(bad >> 32));
+        if (lane == 0) atomicMin(first_bad, (unsigned long long)(c + (uint64_t)__builtin_ctzll(bad)));
+      }
+    }
+    if (in && (flags & kFlagStamp)) *p = crc;
+  }
+}
+
 }  // namespace
 
 // uniform batches of 16-B aligned 1 KiB-multiple blocks (k_crc_fast)
@@ -2508,6 +2548,37 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
     hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
                        b.flags, n, grp_lg_chunk(n, grid, 0), b.crc_out, nullptr, nullptr, b.tables, nullptr, 0,
                        flag);
+  return hipGetLastError();
+}
+
+uint64_t seg_block_workspace_bytes(uint64_t n, uint64_t max_units, bool crc_words) {
+  return ((seg_workspace_bytes(n, max_units) + 7) & ~7ull) + 12 * n + (crc_words ? 4 * n : 0);
+}
+
+hipError_t launch_seg_blocks(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid,
+                             hipStream_t s, uint32_t *taken) {
+  const uint64_t n = b.nblocks;
+  if (!b.base || b.off || b.len || b.ulen < 4 || b.stride < b.ulen || !st || !ws || n == 0 ||
+      (b.flags & kFlagMessages) || !b.tables)
+    return hipErrorInvalidValue;
+  uint64_t *moff = reinterpret_cast<uint64_t *>(ws + ((seg_workspace_bytes(n, max_units) + 7) & ~7ull) / 4);
+  uint32_t *mlen = reinterpret_cast<uint32_t *>(moff + n), *wcrc = mlen + n;
+  const int mg = (int)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_seg_block_msgs, dim3(mg), dim3(256), 0, s, n, b.stride, b.ulen, moff, mlen);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  Batch mb = b;
+  mb.off = moff;
+  mb.len = mlen;
+  mb.flags = kFlagMessages;
+  mb.crc_out = b.crc_out ? b.crc_out : wcrc;
+  mb.bad_bitmap = nullptr;
+  mb.first_bad = nullptr;
+  // no k_crc_grp fallback: these blocks are not its shape, and its fallback would hash whole messages
+  if ((e = launch_seg(mb, st, ws, max_units, grid, s, taken, ~0ull)) != hipSuccess) return e;
+  if (!b.first_bad && !(b.flags & kFlagStamp)) return hipSuccess;
+  hipLaunchKernelGGL(k_seg_block_out, dim3(mg), dim3(256), 0, s, b.base, n, b.stride, b.flags, mb.crc_out,
+                     b.bad_bitmap, b.first_bad);
   return hipGetLastError();
 }
 

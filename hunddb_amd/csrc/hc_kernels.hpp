@@ -117,6 +117,15 @@ constexpr uint64_t kSegGrpFallbackMin = 1ull << 18;  // grp_min's default (HC_SE
 // taken (optional, device word): 1 packed, 2 gapped, 3 k_crc_grp fallback, 0 k_crc_any fallback.
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
                       uint32_t *taken = nullptr, uint64_t grp_min = kSegGrpFallbackMin, uint32_t lg_chunk = 7);
+// A uniform block batch (no off/len arrays) that k_crc_grp refuses (lengths not
+// a 4 KiB multiple, or not 16-B aligned), ulen >= 4, stride >= ulen: its
+// messages block[4:ulen] written out as off/len arrays, launch_seg over them
+// (they lie stride - ulen + 4 bytes apart: the small-gap mode), then the
+// blocks' verify / stamp outputs from the message CRCs.  ws holds
+// seg_block_workspace_bytes(n, max_units, !b.crc_out) bytes.
+uint64_t seg_block_workspace_bytes(uint64_t n, uint64_t max_units, bool crc_words);
+hipError_t launch_seg_blocks(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid,
+                             hipStream_t s, uint32_t *taken = nullptr);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
                                  hipStream_t s);
 
