@@ -2252,11 +2252,16 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
 #pragma unroll
       for (int p = 0; p < kSub; p++) {
         const uint64_t j = c + 64u * p + lane;
+        const bool same = (xe[p] >> kU) == (xa[p] >> kU);
+        const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
+        const uint32_t L = j < n && j ? (uint32_t)(xa[p] - gp) : 0u, nw = (L + 3u) >> 2;
+        // before any lane leaves: a butterfly over a partial wave reads the
+        // stale values of the lanes that left (r5l: a record after a 38-B gap
+        // in wave 0, whose lane 0 holds record 0, lost its last words)
+        const uint32_t nwmax = wave_max_u32(nw);
         if (j >= n) continue;
         uint32_t ha = he[p];  // j == 0: H(s_0) itself
         if (j) {
-          const bool same = (xe[p] >> kU) == (xa[p] >> kU);
-          const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
           // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes, as nw words
           // ending at s_j behind 4nw - L leading zeros (raw ignores them).  The
           // words come from the aligned dwords D[i] at Bq + 4i, Bq = (s_j -
@@ -2266,9 +2271,8 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
           // load (r5h/r5i: 233 / 369 us of combine at 2M records).  An aligned
           // dword holding a span byte never leaves the span's pages; D[nw] is
           // read only when it holds gap bytes (sa > 0).
-          const uint32_t L = (uint32_t)(xa[p] - gp), nw = (L + 3u) >> 2, sa = (uint32_t)xa[p] & 3u;
+          const uint32_t sa = (uint32_t)xa[p] & 3u;
           const uint64_t Bq = (xa[p] - 4u * nw) & ~3ull;
-          const uint32_t nwmax = wave_max_u32(nw);
           uint32_t D[kSegSmallGap / 4 + 1];
 #pragma unroll
           for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
