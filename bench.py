@@ -83,15 +83,17 @@ WORKLOADS = {
     # GetCRC of 1M aligned 4 KiB records in shuffled order: the
     # stream refuses them; its fallback runs k_crc_grp's body inside the combine
     "records4k_shuffled": (1_000_000, "records4k_shuffled", "weak"),
-    # 1M uniform 4092-B blocks back to back (config.go:241 allows any BlockSize >= 1024):
-    # not k_crc_grp's shape; their messages block[4:] on the stream's small-gap mode (round 5)
+    # uniform blocks k_crc_grp refuses (config.go:241 allows any BlockSize >= 1024): 1M x 4092 B
+    # (k_crc_any: the route it wins, hc_api.cpp seg_blocks_preferred) and 0.5M x 8188 B (their
+    # messages block[4:] on the stream's small-gap mode, launch_seg_blocks; round 5)
     "blocks4092": (1_000_000, 4092, "weak"),
+    "blocks8188": (500_000, 8188, "weak"),
 }
 # the dominant kernel per workload (PMC passes)
 KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
              "records": "k_seg_stream", "records_gapped": "k_seg_stream",
-             "records4k_shuffled": "k_seg_combine", "blocks4092": "k_seg_stream"}  # else the streaming CRC kernel
-SEG_WORKLOADS = ("records", "records_gapped", "records4k_shuffled", "blocks4092")  # on k_seg_*: stream_mode
+             "records4k_shuffled": "k_seg_combine", "blocks4092": "k_crc_any", "blocks8188": "k_seg_stream"}  # else the streaming CRC kernel
+SEG_WORKLOADS = ("records", "records_gapped", "records4k_shuffled", "blocks4092", "blocks8188")  # on k_seg_*: stream_mode
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
 

@@ -235,6 +235,16 @@ uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::uniqu
 // lie 4 + stride - ulen bytes apart, which the stream's small-gap mode takes
 // (launch_seg_blocks); k_crc_any ran them at 57-62 % (round 4).
 uint64_t seg_min_blocks() { return (uint64_t)std::max<int64_t>(1, knob(kKnobSegMinBlocks)); }
+// The stream against k_crc_any over 4 GiB of uniform blocks, same buffers,
+// alternating routes (tools/seg_blocks_sweep.py, profiles/r5/r5m/sweep.jsonl,
+// TB/s): 1020 B 2.5 / 2.8, 2044 3.7 / 4.1, 4092 5.46 / 5.43, 6000 6.15 / 6.01,
+// 8188 5.76 / 6.20, 12000 5.69 / 6.28, 16380 5.18 / 6.34, 65532 6.40 / 6.48;
+// at an address that is not 4-B aligned 4092 5.02 / 5.42, 4096 5.19 / 5.45,
+// 8192 5.00 / 6.05.  k_crc_any keeps 4-B aligned blocks of 2-8 KiB.
+bool seg_blocks_preferred(const uint8_t *base, uint64_t stride, uint32_t ulen) {
+  const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) | stride) & 3u) == 0;
+  return !(aligned4 && ulen > 2048 && ulen < 8000);
+}
 
 // The span bound of a batch at `base` (the allocation holding it), as k_seg_*'s unit count; 0 if unknown.
 uint64_t seg_units_for(const uint8_t *base) {
@@ -293,7 +303,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       e = launch_fast(b, fast_grid, s);
       info.fast_blocks = n;
     } else if (seg_ok && ulen >= 4 && stride >= ulen && n >= seg_min_blocks() && n < 0x7FFFFFFFull &&
-               seg_blocks(d, b, s, fast_grid, e)) {
+               seg_blocks_preferred(base, stride, ulen) && seg_blocks(d, b, s, fast_grid, e)) {
       info.kernel = "k_seg_plan+k_seg_stream+k_seg_combine";
       info.fast_blocks = n;
       t_seg_dev = dev;

@@ -21,6 +21,11 @@ def seg_blocks(knobs):
     knobs.setenv("HC_SEG_MIN_BLOCKS", "1")  # every size below is offered to the stream
 
 
+def preferred(ptr, stride, ulen):
+    """hc_api.cpp seg_blocks_preferred: k_crc_any keeps 4-B aligned 2-8 KiB blocks"""
+    return not ((ptr | stride) & 3 == 0 and 2048 < ulen < 8000)
+
+
 def u32(t):
     return t.cpu().numpy().view(np.uint32)
 
@@ -38,8 +43,8 @@ def run(torch, hc, buf, n, stride, ulen, flags=0, verify=False):
 
 
 CASES = [  # (ulen, stride - ulen, start, path; None: as the plan's restatement says)
-    (4092, 0, 0, "gapped"),       # config.go:241's non-4 KiB BlockSize, back to back: 4-B gaps (the stored words)
-    (4092, 0, 3, "gapped"),
+    (4092, 0, 0, "gapped"),       # config.go:241's non-4 KiB BlockSize, back to back: 4-B gaps (the stored
+    (4092, 0, 3, "gapped"),       # words); aligned, they stay on k_crc_any (seg_blocks_preferred)
     (4096, 0, 1, "gapped"),       # 4 KiB blocks at an odd address (k_crc_grp needs 16-B alignment)
     (1000, 0, 0, "gapped"),
     (5000, 24, 2, "gapped"),      # 28-B gaps
@@ -68,11 +73,13 @@ def test_uniform_blocks_on_the_stream(seg_blocks, cuda, hc, oracle, ulen, extra,
     assert bad.size == 0, (bad[:8], got[bad[:8]], want[bad[:8]])
     moff = np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(4)
     want_path = expected_path(view.data_ptr(), moff, np.full(n, ulen - 4, np.uint64)) or "fallback"
-    assert hc.seg_path() == want_path
     assert path is None or path == want_path
+    if not preferred(view.data_ptr(), stride, ulen):
+        want_path = "fallback"  # not offered to the stream
+    assert hc.seg_path() == want_path
 
 
-@pytest.mark.parametrize("ulen,extra,start", [(4092, 0, 0), (4092, 0, 1), (6000, 100, 2)])
+@pytest.mark.parametrize("ulen,extra,start", [(8188, 0, 0), (4092, 0, 1), (6000, 100, 2), (1020, 0, 0)])
 def test_uniform_blocks_verify_and_stamp(seg_blocks, cuda, hc, oracle, ulen, extra, start):
     torch = cuda
     stride = ulen + extra
@@ -109,7 +116,7 @@ def test_uniform_blocks_verify_and_stamp(seg_blocks, cuda, hc, oracle, ulen, ext
 def test_threshold_keeps_small_batches_on_k_crc_any(cuda, hc, oracle, knobs):
     """Below HC_SEG_MIN_BLOCKS (default 4096) the batch stays on k_crc_any."""
     torch = cuda
-    n, ulen = 1000, 4092
+    n, ulen = 1000, 8188
     rng = np.random.default_rng(5)
     host = rng.integers(0, 256, n * ulen, dtype=np.uint8)
     got, _, _ = run(torch, hc, torch.from_numpy(host).cuda(), n, ulen, ulen)
