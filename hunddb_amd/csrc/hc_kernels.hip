@@ -1651,7 +1651,6 @@ constexpr uint32_t kSegUnitLg = 14;  // unit = 16 KiB = 16 rows = 4 groups (the 
 constexpr uint32_t kSegMaxRecord = 1u << 24;  // longest record the stream takes (16 MiB)
 constexpr uint64_t kSegMaxGap = 1u << 22;     // longest gap between two records it takes (4 MiB)
 constexpr uint64_t kSegSmallGap = 64;         // longest gap k_seg_combine hashes itself (kSegGapSmall)
-constexpr uint32_t kSegGapFastWords = 8;      // gaps of up to 8 words: k_seg_combine's batched loads
 constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's largest grid: one "bad" slot per workgroup
 constexpr uint32_t kSegPlanWgs = 2048;       // its default grid cap (grid-stride beyond; r4e: 13.5 vs 16.8 us at 2M events)
 
@@ -2250,86 +2249,53 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
         he[p] = ev_h[jj];
         hb[p] = ev_h[jj + 1];
       }
-      // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes, as nw words ending
-      // at s_j behind 4nw - L leading zeros (raw ignores them).  The words come
-      // from the aligned dwords D[i] at Bq + 4i, Bq = (s_j - 4nw) & ~3, bytes
-      // before gp cleared, by a funnel shift of sa = s_j & 3 bytes.  Plain
-      // per-lane loads: a buffer resource is scalar, so one built from a
-      // per-lane address became a 64-pass waterfall loop per load (r5h/r5i:
-      // 233 / 369 us of combine at 2M records).  An aligned dword holding a span
-      // byte never leaves the span's pages; D[nw] is read only when it holds gap
-      // bytes (sa > 0).  When every gap of the kSub sub-passes fits
-      // kSegGapFastWords words (WAL headers: 17 B), all their loads are issued
-      // before the first is hashed; else one record at a time.
-      uint64_t gpv[kSub];
-      uint32_t nwv[kSub], nwm[kSub], gr[kSub];
-      bool fast = true;
 #pragma unroll
       for (int p = 0; p < kSub; p++) {
         const uint64_t j = c + 64u * p + lane;
         const bool same = (xe[p] >> kU) == (xa[p] >> kU);
-        gpv[p] = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
-        const uint32_t L = j < n && j ? (uint32_t)(xa[p] - gpv[p]) : 0u;
-        nwv[p] = (L + 3u) >> 2;
-        // every lane: a butterfly over a partial wave reads the stale values
-        // of the lanes that left (r5l: a record after a 38-B gap in wave 0,
-        // whose lane 0 holds record 0, lost its last words)
-        nwm[p] = wave_max_u32(nwv[p]);
-        fast = fast && nwm[p] <= kSegGapFastWords;
-      }
-      auto gap_load = [&](uint32_t *D, int p, uint32_t cap) {
-        const uint32_t nwp = nwv[p], sa = (uint32_t)xa[p] & 3u;
-        const uint64_t Bq = (xa[p] - 4u * nwp) & ~3ull, gp = gpv[p];
-#pragma unroll
-        for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
-          if (i > cap) break;
-          D[i] = 0;
-          if (i > nwm[p]) continue;
-          const uint64_t ai = Bq + 4u * i;
-          if (nwp && i <= nwp && ai + 4u > gp && (i < nwp || sa)) {
-            D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
-            if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
-          }
-        }
-      };
-      auto gap_hash = [&](const uint32_t *D, int p, uint32_t cap) {
-        const uint32_t sa = (uint32_t)xa[p] & 3u;
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kSegSmallGap / 4; k++) {
-          if (k >= cap || k >= nwm[p]) break;
-          uint32_t t = r, w = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sa);
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            t = sh1[(t ^ w) & 255u] ^ (t >> 8);
-            w >>= 8;
-          }
-          r = k < nwv[p] ? t : r;
-        }
-        return r;
-      };
-      if (fast) {  // wave-uniform
-        uint32_t D[kSub][kSegGapFastWords + 1];
-#pragma unroll
-        for (int p = 0; p < kSub; p++) gap_load(D[p], p, kSegGapFastWords);
-#pragma unroll
-        for (int p = 0; p < kSub; p++) gr[p] = gap_hash(D[p], p, kSegGapFastWords);
-      } else {
-#pragma unroll
-        for (int p = 0; p < kSub; p++) {
-          uint32_t D[kSegSmallGap / 4 + 1];
-          gap_load(D, p, kSegSmallGap / 4);
-          gr[p] = gap_hash(D, p, kSegSmallGap / 4);
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < kSub; p++) {
-        const uint64_t j = c + 64u * p + lane;
+        const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
+        const uint32_t L = j < n && j ? (uint32_t)(xa[p] - gp) : 0u, nw = (L + 3u) >> 2;
+        // before any lane leaves: a butterfly over a partial wave reads the
+        // stale values of the lanes that left (r5l: a record after a 38-B gap
+        // in wave 0, whose lane 0 holds record 0, lost its last words)
+        const uint32_t nwmax = wave_max_u32(nw);
         if (j >= n) continue;
         uint32_t ha = he[p];  // j == 0: H(s_0) itself
         if (j) {
-          const bool same = (xe[p] >> kU) == (xa[p] >> kU);
-          const uint32_t r = gr[p];
+          // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes, as nw words
+          // ending at s_j behind 4nw - L leading zeros (raw ignores them).  The
+          // words come from the aligned dwords D[i] at Bq + 4i, Bq = (s_j -
+          // 4nw) & ~3, bytes before gp cleared, by a funnel shift of sa = s_j & 3
+          // bytes.  Plain per-lane loads: a buffer resource is scalar, so one
+          // built from a per-lane address became a 64-pass waterfall loop per
+          // load (r5h/r5i: 233 / 369 us of combine at 2M records).  An aligned
+          // dword holding a span byte never leaves the span's pages; D[nw] is
+          // read only when it holds gap bytes (sa > 0).
+          const uint32_t sa = (uint32_t)xa[p] & 3u;
+          const uint64_t Bq = (xa[p] - 4u * nw) & ~3ull;
+          uint32_t D[kSegSmallGap / 4 + 1];
+#pragma unroll
+          for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
+            D[i] = 0;
+            if (i > nwmax) continue;
+            const uint64_t ai = Bq + 4u * i;
+            if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
+              D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
+              if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
+            }
+          }
+          uint32_t r = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < kSegSmallGap / 4; k++) {
+            if (k >= nwmax) break;
+            uint32_t t = r, w = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sa);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              t = sh1[(t ^ w) & 255u] ^ (t >> 8);
+              w >>= 8;
+            }
+            r = k < nw ? t : r;
+          }
           const uint32_t re = (uint32_t)(xa[p] >> 10) + 1u, d = (uint32_t)(((uint64_t)re << 10) - xa[p]);
           // shift(r, d) = shift(shift(r, 1024), -(1024 - d))
           uint32_t pg = seg_lds_tmul(tl, r);
