@@ -105,7 +105,8 @@ int hc_fix_last_block(uint8_t *p, size_t n);
  * len==NULL -> len[i] = ulen.  Blocks shorter than 4 bytes get crc 0 and, for
  * verify, count as bad ("invalid block data").  Any lengths/alignments are
  * accepted; 16-byte-aligned blocks whose length is a multiple of 1024 take the
- * streaming kernel, all others the general kernel. */
+ * streaming kernel, all others the general kernel (device entries: uniform
+ * batches of other shapes may take the message stream). */
 int hc_crc32_blocks(const uint8_t *base, const uint64_t *off, const uint32_t *len,
                     uint64_t stride, uint32_t ulen, uint64_t nblocks, uint32_t *crc_out);
 /* Batched CheckBlockIntegrity.  bad_bitmap (optional, ceil(n/32) uint32 words,
@@ -345,7 +346,7 @@ int hc_debug_seg_taken(void);
  * call that needs one (a getenv racing with a Go os.Setenv would be a data
  * race): HC_DEVICE, HC_SEG_MIN_MSGS, HC_COPY_THREADS, HC_WAL_MIN_RANGE,
  * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
- * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN.  hc_debug_set changes one of them afterwards
+ * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN, HC_SEG_MIN_BLOCKS.  hc_debug_set changes one of them afterwards
  * (tests and tools); value NULL restores the compiled default.  HC_OK, or
  * HC_E_ARG for an unknown name. */
 int hc_debug_set(const char *name, const char *value);
