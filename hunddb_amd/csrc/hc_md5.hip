@@ -122,7 +122,8 @@ template <bool kOff, bool kLen, int kStage = kMd5StageBlocks, int kDepth = 2, bo
 __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restrict__ base,
                                                         const uint64_t *__restrict__ offs,
                                                         const uint32_t *__restrict__ lens, uint64_t stride,
-                                                        uint32_t ulen, uint64_t n, uint8_t *__restrict__ out16) {
+                                                        uint32_t ulen, uint64_t n, uint8_t *__restrict__ out16,
+                                                        const uint64_t *__restrict__ bounds) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   // stage pieces are addressed as integers: name the global address space, or
   // they become flat loads, which also count on lgkmcnt (the LDS waits of the
@@ -141,7 +142,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   // at chunk e * kPitch + kSlot
   u32x4 *H = L + kSlot;
   const uint64_t gw = (uint64_t)blockIdx.x * kMd5Waves + wave, W = (uint64_t)gridDim.x * kMd5Waves;
-  const uint64_t p0 = n * gw / W, p1 = n * (gw + 1) / W;
+  // the wave's messages: equal counts, or equal blocks (bounds: k_md5_bounds)
+  const uint64_t p0 = bounds ? bounds[gw] : n * gw / W, p1 = bounds ? bounds[gw + 1] : n * (gw + 1) / W;
   if (p0 >= p1) return;
   // metadata windows: lane j holds message wbase + j; the next window of the
   // walk is prefetched into nw_*
@@ -385,6 +387,139 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
 }
 
 // ---------------------------------------------------------------------------
+// Ranges of equal work for k_md5's waves (variable lengths).  Equal message
+// counts left the heaviest of 2048 waves 16.8 % above the mean on 2M
+// log-uniform records (64 B - 64 KiB: a wave's ~1000 records sum to 9.5 MB
+// +- 5 %), and the kernel waits for it.  The work of a message is its
+// compressions, md5_blocks(len).  Three small launches: chunk sums, their
+// scan and each wave's chunk, the split inside that chunk.
+constexpr uint32_t kMd5Chunk = 2048;    // messages per weight chunk
+constexpr uint32_t kMd5MaxWaves = 8192; // k_md5's largest grid (x kMd5Waves)
+constexpr uint32_t kMd5MaxChunks = 16384;  // k_md5_split's prefix in LDS (128 KiB): up to 32M messages
+
+__device__ __forceinline__ uint32_t md5_blocks(uint32_t l) { return (l >> 6) + ((l & 63u) < 56u ? 1u : 2u); }
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d);
+  return v;
+}
+
+// csum[c] = the compressions of chunk c (one workgroup a chunk)
+__global__ __launch_bounds__(256) void k_md5_wsum(const uint32_t *__restrict__ lens, uint64_t n,
+                                                  unsigned long long *__restrict__ csum) {
+  __shared__ unsigned long long part[4];
+  const uint64_t lo = (uint64_t)blockIdx.x * kMd5Chunk, hi = lo + kMd5Chunk < n ? lo + kMd5Chunk : n;
+  uint64_t v = 0;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) v += md5_blocks(lens[i]);
+  v = wave_sum_u64(v);
+  if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) csum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// One workgroup: csum -> exclusive prefix (in place, csum[nch] = total), then
+// for every wave g in 1 .. W-1 its target T_g = total * g / W and the chunk
+// holding it: gch[g] = the last chunk c with csum[c] <= T_g, gt[g] = T_g.
+__global__ __launch_bounds__(1024) void k_md5_split(unsigned long long *__restrict__ csum, uint64_t nch,
+                                                    uint32_t W, unsigned long long *__restrict__ gch,
+                                                    unsigned long long *__restrict__ gt) {
+  __shared__ unsigned long long wsum[16];
+  __shared__ unsigned long long carry;
+  __shared__ unsigned long long pre[kMd5MaxChunks];  // the search reads the prefix here, not
+                                                     // through the vector L1 it was read into
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < nch; base += 1024) {
+    const uint64_t i = base + t;
+    const uint64_t v = i < nch ? csum[i] : 0;
+    uint64_t x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, d);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t off = carry;
+    for (uint32_t k = 0; k < wv; k++) off += wsum[k];
+    if (i < nch) csum[i] = pre[i] = off + x - v;  // exclusive
+    __syncthreads();
+    if (t == 1023) carry = off + x;
+    __syncthreads();
+  }
+  const uint64_t total = carry;
+  if (t == 0) csum[nch] = total;
+  for (uint32_t g = 1 + t; g < W; g += 1024) {
+    const uint64_t T = (total / W) * g + ((total % W) * g) / W;
+    uint64_t lo = 0, hi = nch;  // the last c < nch with csum[c] <= T (csum[0] = 0)
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= T)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    gch[g] = lo;
+    gt[g] = T;
+  }
+}
+
+// One wave per split g: bounds[g] = the first message whose exclusive prefix
+// of compressions is >= T_g (in chunk gch[g], or the next chunk's first);
+// bounds[0] = 0, bounds[W] = n.  Monotone in g, so the ranges tile [0, n).
+__global__ __launch_bounds__(256) void k_md5_bounds(const uint32_t *__restrict__ lens, uint64_t n, uint32_t W,
+                                                    const unsigned long long *__restrict__ csum,
+                                                    const unsigned long long *__restrict__ gch,
+                                                    const unsigned long long *__restrict__ gt,
+                                                    uint64_t *__restrict__ bounds) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (g > W) return;  // whole waves
+  if (g == 0 || g == W) {
+    if (lane == 0) bounds[g] = g ? n : 0;
+    return;
+  }
+  constexpr uint32_t kPer = kMd5Chunk / 64;
+  const uint64_t c = gch[g], T = gt[g], lo = c * kMd5Chunk;
+  uint32_t w[kPer];
+  uint64_t ls = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) {
+    const uint64_t i = lo + lane * kPer + k;
+    w[k] = i < n ? md5_blocks(lens[i]) : 0u;
+    ls += w[k];
+  }
+  uint64_t x = ls;  // inclusive scan of the lane sums
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  // exclusive prefix of this lane's first message; the message of the lane's
+  // range where the running prefix first reaches T
+  uint64_t run = csum[c] + x - ls, idx = ~0ull;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) {
+    const uint64_t i = lo + lane * kPer + k;
+    if (idx == ~0ull && run >= T && i < n) idx = i;
+    run += w[k];
+  }
+  // the lowest lane's hit; none: the next chunk's first message
+  uint64_t best = idx;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)best, d);
+    best = o < best ? o : best;
+  }
+  if (lane == 0) {
+    const uint64_t nx = lo + kMd5Chunk < n ? lo + kMd5Chunk : n;
+    bounds[g] = best != ~0ull ? best : nx;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // One Merkle level: out[i] = md5(in[2i] || in[2i+1]) for i < n_out, with
 // in[n_in] read as the zero padding node when n_in is odd; thread n_out writes
 // that padding node of `in` (it is serialized with the tree).
@@ -411,24 +546,45 @@ __global__ void k_md5_empty(uint8_t *out16) {  // md5.Sum([]byte{}) (merkle_tree
 
 }  // namespace
 
+// messages from which k_md5's waves get ranges of equal work (off/len batches)
+constexpr uint64_t kMd5BalanceMin = 16384;
+
+// workspace: the chunk sums and their prefix (nch + 1), each wave's chunk and
+// target (kMd5MaxWaves + 1 each), the ranges (kMd5MaxWaves + 1); u64 words
 uint64_t md5_workspace_bytes(uint64_t n) {
-  (void)n;
-  return 0;  // the tail blocks are built inside k_md5: no workspace
+  const uint64_t nch = (n + kMd5Chunk - 1) / kMd5Chunk;
+  if (n < kMd5BalanceMin || nch > kMd5MaxChunks) return 0;
+  return 8 * ((nch + 1) + 3 * ((uint64_t)kMd5MaxWaves + 1));
 }
 
 hipError_t launch_md5(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t ulen,
                       uint64_t n, uint8_t *workspace, uint8_t *out16, int cus, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  (void)workspace;  // unused: md5_workspace_bytes() == 0
   // 2 workgroups (8 waves) per CU fit the LDS; a smaller batch gets 4 messages
   // per lane per wave range (256 per wave): with heavy-tailed sizes, fewer and
   // longer ranges balance better than more waves (200k log-uniform records:
   // 1991 GB/s at 196 workgroups against 1284 at 512, profiles/r1/md5/dyn/)
   uint64_t grid = (n + 256 * kMd5Waves - 1) / (256 * kMd5Waves);
   if (grid > (uint64_t)cus * 2) grid = (uint64_t)cus * 2;
+  const uint32_t W = (uint32_t)grid * kMd5Waves;
+  const uint64_t *bounds = nullptr;
+  const uint64_t nch = (n + kMd5Chunk - 1) / kMd5Chunk;
+  if (len && workspace && n >= kMd5BalanceMin && W <= kMd5MaxWaves && nch <= kMd5MaxChunks) {  // equal work
+    auto *csum = reinterpret_cast<unsigned long long *>(workspace);
+    unsigned long long *gch = csum + nch + 1, *gt = gch + kMd5MaxWaves + 1;
+    uint64_t *bnd = reinterpret_cast<uint64_t *>(gt + kMd5MaxWaves + 1);
+    hipLaunchKernelGGL(k_md5_wsum, dim3((unsigned)nch), dim3(256), 0, s, len, n, csum);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_md5_split, dim3(1), dim3(1024), 0, s, csum, nch, W, gch, gt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_md5_bounds, dim3((W + 1 + 3) / 4), dim3(256), 0, s, len, n, W, csum, gch, gt, bnd);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    bounds = bnd;
+  }
   const dim3 g((unsigned)grid), b(64 * kMd5Waves);
 #define HC_MD5_LAUNCH(O, L)                                                                                  \
-  hipLaunchKernelGGL((k_md5<O, L>), g, b, 0, s, base, off, len, stride, ulen, n, out16)
+  hipLaunchKernelGGL((k_md5<O, L>), g, b, 0, s, base, off, len, stride, ulen, n, out16, bounds)
   if (off && len)
     HC_MD5_LAUNCH(true, true);
   else if (off)

@@ -289,7 +289,8 @@ int hc_md5_messages(const uint8_t *base, const uint64_t *off, const uint32_t *le
 /* Device form: message i = base[off(i) .. +len(i)) (off/len arrays or
  * i*stride / ulen, as hc_dev_crc32_blocks), digests into out16 (device,
  * 16-B aligned).  workspace: device memory of hc_md5_workspace_bytes(n)
- * bytes (currently 0: the kernel pads each message's tail itself), or NULL.
+ * bytes (the waves' ranges of equal work for off/len batches of 16384 to 32M
+ * messages; else 0), or NULL (then allocated per call on `stream`).
  * Kernel k_md5 (lane per message). */
 uint64_t hc_md5_workspace_bytes(uint64_t n);
 int hc_dev_md5_messages(int device, const void *base, const uint64_t *off, const uint32_t *len, uint64_t stride,

@@ -88,6 +88,32 @@ def test_md5_records_batch_vs_oracle(cuda, oracle):
     assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}"
 
 
+@pytest.mark.parametrize("case", ["skewed", "all_empty", "one_huge", "threshold"])
+def test_md5_balanced_ranges(cuda, oracle, case):
+    """From 16384 off/len messages k_md5's waves take ranges of equal work
+    (k_md5_wsum / k_md5_split / k_md5_bounds): ranges of very unequal counts,
+    all-equal weights, one wave's range a single 8 MiB record, and the
+    threshold itself.  Every digest vs the oracle."""
+    torch = cuda
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    if case == "skewed":
+        lens = np.zeros(40_000, dtype=np.uint32)
+        lens[20_000:] = rng.integers(0, 200, 20_000)
+        lens[-300:] = 65536
+    elif case == "all_empty":
+        lens = np.zeros(50_000, dtype=np.uint32)
+    elif case == "one_huge":
+        lens = rng.integers(0, 3000, 40_000).astype(np.uint32)
+        lens[12345] = 8 << 20
+    else:
+        lens = rng.integers(0, 9000, 16_384).astype(np.uint32)
+    buf, off, ln = _packed(rng, lens, pad=3)
+    got = _dev_md5(torch, buf, off, ln)
+    want = _oracle_md5(oracle, buf, off, ln)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}"
+
+
 def test_md5_uniform_stride(cuda, oracle, hc):
     torch = cuda
     n, size = 100_000, 4096
