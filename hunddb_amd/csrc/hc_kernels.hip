@@ -2113,13 +2113,17 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     gsum += s_gx[w];
     csum += s_conf[w];
   }
-  // the fallback: k_crc_grp when every record is one of its blocks (16-B
-  // aligned 4 KiB multiples, out of order or far apart; ADVICE r4: the
-  // per-record body ran 57-62 % on them), else k_crc_any's work in the combine
-  const uint32_t mode = !unpacked                   ? kSegPacked
+  // k_crc_grp when every record is one of its blocks (16-B aligned 4 KiB
+  // multiples) in a large batch, whatever their order: ahead of the stream's
+  // own modes, whose event work at 4 KiB records costs more than the hand-out
+  // (1M x 4 KiB, TB/s: packed 4.65 vs 5.73, 16-B gaps 4.37 vs 5.51, 1 KiB gaps
+  // 3.75 vs 6.31, tools/seg_aligned_probe.py, profiles/r5/r5s/; ADVICE r4: the
+  // per-record body ran 57-62 % on them).  Else the stream; else k_crc_any's
+  // work in the combine.
+  const uint32_t mode = allow_grp && csum == n      ? kSegFallbackGrp
+                        : !unpacked                 ? kSegPacked
                         : !not_small && gsum <= 0   ? kSegGapSmall
                         : !unsorted && gsum <= 0    ? kSegGapped
-                        : allow_grp && csum == n    ? kSegFallbackGrp
                                                     : kSegFallback;
   if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
   if (mode == kSegGapSmall)

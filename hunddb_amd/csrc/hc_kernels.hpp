@@ -109,8 +109,8 @@ hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 // batch the stream refuses (out of order or overlapping, larger than the
 // bound, records under ~64 B or over 16 MiB) sets ws[0] on the device and
 // k_seg_combine runs k_crc_any's work over it in the same launch; from grp_min
-// records on, a refused batch of aligned 4 KiB-multiple records only goes to
-// k_crc_grp, launched after the combine, which exits at once unless ws[0] says so.
+// records on, a batch of aligned 4 KiB-multiple records goes to k_crc_grp in
+// any layout, launched after the combine, which exits at once unless ws[0] says so.
 uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
 constexpr uint64_t kSegGrpFallbackMin = 1ull << 18;  // grp_min's default (HC_SEG_GRP_MIN)

@@ -415,11 +415,11 @@ def test_seg_gapped_shapes(cuda, hc, oracle, seg_all):
 
 
 def test_seg_fallback_runs_crc_grp_on_aligned_records(knobs, cuda, hc, oracle, seg_all):
-    """a whole-message batch the stream refuses whose
-    records are all 16-B aligned 4 KiB multiples (out of order, or far apart)
-    goes to k_crc_grp, launched after the combine and gated on the stream's
-    mode word ("fallback_grp"); one record that is not: k_crc_any inside the
-    combine.  Batches from HC_SEG_GRP_MIN records (2^18; 1000 here) may take
+    """a whole-message batch whose records are all 16-B
+    aligned 4 KiB multiples goes to k_crc_grp in any order or layout (since
+    r5s ahead of the stream's own modes), launched after the combine and gated
+    on the stream's mode word ("fallback_grp"); one record that is not:
+    k_crc_any inside the combine, or the stream when it takes the batch.  Batches from HC_SEG_GRP_MIN records (2^18; 1000 here) may take
     it, smaller ones never do.  Every word against the oracle."""
     knobs.setenv("HC_SEG_GRP_MIN", "1000")
     torch = cuda
@@ -433,6 +433,11 @@ def test_seg_fallback_runs_crc_grp_on_aligned_records(knobs, cuda, hc, oracle, s
     assert buf.data_ptr() % 16 == 0
     p = rng.permutation(n)
     check(torch, hc, oracle, host, buf, off[p], lens[p], None)          # out of order: all k_crc_grp's
+    assert hc.seg_path() == "fallback_grp"
+    check(torch, hc, oracle, host, buf, off, lens, None)                # in order: still k_crc_grp's (r5s)
+    assert hc.seg_path() == "fallback_grp"
+    gp = packed(lens + np.uint64(16), 0)                                # 16-B gaps: ditto
+    check(torch, hc, oracle, host, buf, gp[: n // 2], lens[: n // 2], None)
     assert hc.seg_path() == "fallback_grp"
     far = (np.arange(n, dtype=np.uint64) * np.uint64(16384 * 2))[: n // 4]  # gaps over a quarter
     fl = np.full(n // 4, 16384, dtype=np.uint64)
