@@ -447,8 +447,10 @@ def _best_rate(fn, nbytes, reps):
 def h2d_peak(torch, pinned, seconds=1.0):
     """GB/s of pinned host -> device hipMemcpyAsync (torch copies), 256 MiB
     chunks on two streams: the link's practical ceiling on this box."""
-    chunk = 256 << 20
-    n = pinned.numel() // chunk
+    chunk = min(256 << 20, pinned.numel())  # (a small --blocks run: one chunk of the whole buffer)
+    n = pinned.numel() // chunk if chunk else 0
+    if n == 0:
+        return 0.0
     dst = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(3)]
     streams = [torch.cuda.Stream() for _ in range(2)]
     best = 0.0
@@ -491,7 +493,7 @@ def host_inclusive(torch, crc, dev_buf, dev_words, B, reps=3, wal_records=2_000_
                           nbytes, reps)
         words[name] = out["w"]
         res[name] = {"workload": f"hc_crc32_blocks, {n} x {B} B", "gb_s": round(r, 2), "s": round(t, 4),
-                     "frac_h2d_peak": round(r / peak, 3), "frac_pcie_gen5_x16": round(r / 63.0, 3),
+                     "frac_h2d_peak": round(r / peak, 3) if peak else None, "frac_pcie_gen5_x16": round(r / 63.0, 3),
                      "words_match_device": bool(np.array_equal(out["w"], want))}
     leg("crc32_blocks_pinned", pinned.numpy())
     pageable = np.empty(nbytes, dtype=np.uint8)
@@ -512,7 +514,7 @@ def host_inclusive(torch, crc, dev_buf, dev_words, B, reps=3, wal_records=2_000_
     err, bm, fb = got["v"]
     res["wal_verify_pinned"] = {"workload": f"hc_verify_blocks over a config-5 WAL image: {wal_records} records "
                                             f"(64 B - 64 KiB log-uniform) framed into {nb} x 4 KiB blocks",
-                                "gb_s": round(r, 2), "s": round(t, 4), "frac_h2d_peak": round(r / peak, 3),
+                                "gb_s": round(r, 2), "s": round(t, 4), "frac_h2d_peak": round(r / peak, 3) if peak else None,
                                 "frac_pcie_gen5_x16": round(r / 63.0, 3),
                                 "all_blocks_verify": err is None and fb == -1 and not bm.any()}
     del img
@@ -863,7 +865,9 @@ def main(argv=None):
         host_leg = None
         if world == 1 and (args.host_leg == "on" or (args.host_leg == "auto" and args.workload == "northstar")):
             phase("host_leg")
-            host_leg = host_inclusive(torch, crc, buf, out, bsize)
+            # the WAL image scales with a reduced --blocks run (2M records at the full 1M blocks)
+            host_leg = host_inclusive(torch, crc, buf, out, bsize,
+                                      wal_records=max(1000, min(2_000_000, 2 * my)))
         cpu = None
         if not args.cpu_threads:
             args.cpu_threads = cores_available()

@@ -26,6 +26,10 @@ CASES = {
     "unframe8k": (2048, "k_unframe", 2048 * (8192 + 8188)),
     "unframe16k": (1024, "k_unframe", 1024 * (16384 + 16380)),
     "records": (4096, None, None),
+    "records_gapped": (4096, None, None),
+    "records4k_shuffled": (4096, None, None),
+    "blocks4092": (4096, "k_crc_any", 4096 * 4092),           # 4-B aligned 4092-B blocks stay on k_crc_any
+    "blocks8188": (4096, None, 4096 * 8188),                  # the message stream (launch_seg_blocks)
 }
 
 
@@ -34,7 +38,8 @@ CASES = {
 def test_bench_workload_small(workload):
     blocks, kernel, nbytes = CASES[workload]
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--blocks", str(blocks),
-           "--steps", "2", "--warmup", "1", "--cpu-seconds", "0", "--pmc", "off", "--settle", "0"]
+           "--steps", "2", "--warmup", "1", "--cpu-seconds", "0", "--pmc", "off", "--settle", "0",
+           "--host-leg", "off" if workload != "northstar" else "on"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -58,7 +63,7 @@ def test_north_star_meets_its_target():
     CRC32 over 1M x 8 KiB blocks, at full size (bench.py's HIP-event timing of
     k_crc_grp; 85-88 % on the boxes of round 4, profiles/r4/)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "northstar", "--steps", "10",
-           "--warmup", "3", "--cpu-seconds", "0", "--pmc", "off"]
+           "--warmup", "3", "--cpu-seconds", "0", "--pmc", "off", "--host-leg", "off"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
