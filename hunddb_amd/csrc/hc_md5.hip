@@ -130,23 +130,17 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   // compression would wait for the stages in flight: -9 %, tools/kmd5)
   typedef const u32x4 __attribute__((aligned(1), address_space(1))) *gpiece;
   constexpr uint32_t kSlot = 4 * kStage;  // 16-B chunks per stage (<= 16: one 16-lane group per message)
-  // A stage's pieces are the aligned 16-B chunks from the message's stage
-  // start rounded down (round 5: unaligned pieces cost 3.4 % on log-uniform
-  // records and 8 % on 4 KiB records at odd addresses, tools/md5_probe.py,
-  // profiles/r5/r5r/); the message's words are read back at their byte phase
-  // (ds_read_b128 at any byte address, tools/lds_unaligned_probe.hip).  A
-  // phase > 0 needs one chunk more: chunk kSlot, loaded by the slot's own lane.
   // slot m (lane m's stage) at m * kPitch chunks: an odd pitch keeps both the
   // loaders' writes and the per-lane ds_read_b128 conflict-free, and every
   // address is a per-lane base plus an immediate offset
-  constexpr uint32_t kPitch = kSlot + 3;
+  constexpr uint32_t kPitch = kSlot + 1;
   __shared__ u32x4 lds[kMd5Waves][64 * kPitch];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uni_u32(threadIdx.x >> 6);
   u32x4 *L = lds[wave];
   // the hand-off of window entries to free lanes uses the pad column: entry e
-  // at chunk e * kPitch + kSlot + 1
-  u32x4 *H = L + kSlot + 1;
+  // at chunk e * kPitch + kSlot
+  u32x4 *H = L + kSlot;
   const uint64_t gw = (uint64_t)blockIdx.x * kMd5Waves + wave, W = (uint64_t)gridDim.x * kMd5Waves;
   // the wave's messages: equal counts, or equal blocks (bounds: k_md5_bounds)
   const uint64_t p0 = bounds ? bounds[gw] : n * gw / W, p1 = bounds ? bounds[gw + 1] : n * (gw + 1) / W;
@@ -232,13 +226,11 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   struct Stage {
     uint32_t msg;
     uint32_t nb;  // blocks, 0 = none
-    uint32_t ph;  // byte phase of the blocks in the slot (full blocks: the message's address & 15)
     bool first, fin;
     uint32_t tinfo, tlen;  // tail stage: 16-B phase | tail bytes << 4; message length
   };
-  // src / cap: the stage's first (aligned) piece and the offset of its last
-  // valid one (pieces past it re-read it; every piece holds a message byte, so
-  // it stays inside that byte's page)
+  // src / cap: the stage's first piece and the offset of its last valid one
+  // (pieces past it re-read it)
   auto plan = [&](Stage &t, uint64_t &src, uint32_t &cap) {
     assign();
     t.first = fresh;
@@ -247,16 +239,14 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     t.msg = msg;
     t.tinfo = 0;
     t.tlen = 0;
-    t.ph = 0;
     if (!act) {
       src = (uint64_t)(uintptr_t)out16;
       cap = 0;
       t.nb = 0;
     } else if (nfull) {
-      t.ph = (uint32_t)(p & 15u);
-      src = p & ~(uint64_t)15;
+      src = p;
       t.nb = nfull < (uint32_t)kStage ? nfull : (uint32_t)kStage;
-      cap = 16u * ((t.ph + 64u * t.nb - 1u) >> 4);  // the last chunk holding a stage byte (<= 16 * kSlot)
+      cap = 64u * t.nb - 16u;
       p += 64u * t.nb;
       nfull -= t.nb;
     } else {
@@ -277,8 +267,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
   // 16 wave-instructions per stage; each covers 4 messages x kSlot chunks
   // (lanes 16r + j, j < kSlot; with kSlot < 16 the other lanes re-read a piece)
   const uint32_t pj = 16u * (lane & 15u);  // this lane's piece offset in every stage
-  auto issue = [&](u32x4(&R)[16], u32x4 &X, uint64_t src, uint32_t cap) {
-    X = *(gpiece)(src + (16u * kSlot < cap ? 16u * kSlot : cap));  // chunk kSlot of the lane's own slot
+  auto issue = [&](u32x4(&R)[16], uint64_t src, uint32_t cap) {
     if constexpr (kTable) {
       // every lane posts {src, cap} in the pad column of its slot (the
       // hand-off is done by now); a loader reads the 16 entries it serves,
@@ -348,8 +337,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
         uint32_t M[16];
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
-          const u32x4 v = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(L + lane * kPitch) +
-                                                           t.ph + 64u * b + 16u * q);
+          const u32x4 v = L[lane * kPitch + 4u * b + q];
           M[4 * q] = v.x;
           M[4 * q + 1] = v.y;
           M[4 * q + 2] = v.z;
@@ -360,14 +348,14 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
     }
     if (t.fin) *reinterpret_cast<uint4 *>(out16 + (p0 + t.msg) * 16) = make_uint4(st[0], st[1], st[2], st[3]);
   };
-  u32x4 R[kDepth][16], X[kDepth];
+  u32x4 R[kDepth][16];
   Stage T[kDepth];
 #pragma unroll
   for (int d = 0; d < kDepth; d++) {
     uint64_t src;
     uint32_t cap;
     plan(T[d], src, cap);
-    issue(R[d], X[d], src, cap);
+    issue(R[d], src, cap);
   }
   // one step on register set d (a template argument, so R[d] stays in registers)
   auto step = [&](auto dc) -> bool {
@@ -378,13 +366,12 @@ __global__ __launch_bounds__(64 * kMd5Waves) void k_md5(const uint8_t *__restric
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++)
       if ((lane & 15u) < kSlot) L[(4u * q + (lane >> 4)) * kPitch + (lane & 15u)] = R[d][q];
-    L[lane * kPitch + kSlot] = X[d];
     __builtin_amdgcn_wave_barrier();
     const Stage cur = T[d];
     uint64_t src;
     uint32_t cap;
     plan(T[d], src, cap);
-    issue(R[d], X[d], src, cap);  // in flight while the older stages are compressed
+    issue(R[d], src, cap);  // in flight while the older stages are compressed
     compress_stage(cur);
     __builtin_amdgcn_wave_barrier();
     return true;
