@@ -6,8 +6,9 @@ start alignment), off/len blocks (4 KiB multiples mixed with arbitrary
 lengths, gaps, unaligned starts, lengths 0-3, shuffled and overlapping
 entries) and whole messages (packed back to back, or scattered).  Every case
 runs the device entry (hc_dev_crc32_blocks, so k_crc_grp / k_crc_fast /
-k_crc_any routing and, for packed message batches with HC_SEG_MIN_MSGS=1, the
-k_seg_* stream) and the host entry (the pipelined staging path), and compares
+k_crc_any routing; the k_seg_* stream for message batches and, with
+HC_SEG_MIN_BLOCKS=1 on half the uniform cases, for the uniform blocks
+k_crc_grp refuses) and the host entry (the pipelined staging path), and compares
 the words with the oracle.  Non-overlapping block cases are then stamped on
 the device, compared byte for byte, corrupted at random blocks and verified:
 bitmap and first_bad must name exactly the corrupted blocks plus every block
@@ -89,6 +90,8 @@ def test_random_layout(knobs, cuda, hc, oracle, seed, monkeypatch):
         np.all(off[1:] == off[:-1] + lens[:-1].astype(np.uint64)))
     if packed and seed % 2:
         knobs.setenv("HC_SEG_MIN_MSGS", "1")  # the packed-record stream on a small batch
+    if kind == "uniform" and seed % 2:
+        knobs.setenv("HC_SEG_MIN_BLOCKS", "1")  # blocks k_crc_grp refuses: the message stream (round 5)
     want = _words(oracle, kind, buf[lead:], off, lens, stride, ulen, n)
     flags = hc.HC_F_MESSAGES if kind == "messages" else 0
     # device entry
