@@ -39,11 +39,13 @@ namespace hc {
 
 namespace {
 
-// The mode word k_seg_stream stores for its batch:
-// kSegFallbackGrp is the fallback for a batch whose records are all 16-B
-// aligned 4 KiB multiples (k_crc_grp's blocks): k_crc_grp, launched after the
-// combine with this word as its gate.
-// kSegGapSmall: sorted records whose gaps are all at most kSegSmallGap bytes.
+// The mode word k_seg_stream stores for its batch, in the
+// order it is chosen: kSegFallbackGrp, a large batch whose records are all
+// 16-B aligned 4 KiB multiples (k_crc_grp's blocks), in any layout: k_crc_grp,
+// launched after the combine with this word as its gate; kSegPacked, records
+// back to back; kSegGapSmall, sorted records whose gaps are all at most
+// kSegSmallGap bytes; kSegGapped, sorted with gaps up to kSegMaxGap (zeroed in
+// the stream); kSegFallback, k_crc_any's work inside the combine.
 constexpr uint32_t kSegPacked = 0, kSegFallback = 1, kSegGapped = 2, kSegFallbackGrp = 3, kSegGapSmall = 4;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -1634,9 +1636,10 @@ __global__ void k_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad
 // from the span's raw CRCs at a and b relative to any common origin; the stream
 // only has to leave them at the record boundaries ("events"), relative to the
 // 16 KiB unit holding each event.
-//   k_seg_plan     events -> first event of every 16 KiB unit; checks that the
-//                  batch is packed and no record exceeds kSegMaxRecord (else a
-//                  flag, stored by k_seg_stream, sends it to k_crc_any)
+//   k_seg_plan     events -> first event of every 16 KiB unit; per workgroup,
+//                  which modes its records rule out, their gap bytes against
+//                  their payload, and how many are k_crc_grp's blocks (slots
+//                  that k_seg_stream's prologue reduces to the mode word)
 //   k_seg_stream   k_crc_grp's rows, groups and hand-out over the span's units;
 //                  per unit its raw CRC, and at every row holding events
 //                  H(x) = shift(raw(unit .. x), re - x) (re = the row's end):
