@@ -2085,11 +2085,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   __shared__ uint32_t s_conf[kFastWaves];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
-  fill_crc_tables(lds, tables, tid, kFastThreads);
   if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
-  uint32_t col[32];
-#pragma unroll
-  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
   uint32_t bad = 0, conf = 0;
   long long gx = 0;
   for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) {
@@ -2129,6 +2125,14 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
                         : !unsorted && gsum <= 0    ? kSegGapped
                                                     : kSegFallback;
   if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
+  // a fallback has no stream work: no table fill (r5: the fill was 8 of the
+  // 9 us this kernel took when k_crc_grp took the batch)
+  if (mode == kSegFallback || mode == kSegFallbackGrp) return;
+  fill_crc_tables(lds, tables, tid, kFastThreads);
+  uint32_t col[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
+  __syncthreads();
   if (mode == kSegGapSmall)
     seg_stream_body<kSegGapSmall, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
   else if (mode == kSegGapped)
@@ -2171,6 +2175,22 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
   constexpr uint32_t kUnitRows = 1u << (kU - 10);
   __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024 + 256];
+  const uint32_t mode = *flag;
+  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks)
+    *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : mode == kSegGapSmall ? 4u : 0u;
+  // kSegFallbackGrp: k_crc_grp, launched after this kernel and gated on the
+  // mode word, takes the batch.  (Round 5 first ran k_crc_grp's body here,
+  // before the sweep: the combine then faulted on the plain fallback and took
+  // 34 ms for 1M aligned records, profiles/r5/r5d/.)  Neither fallback needs
+  // the SegTables below (r5: their fill was most of this kernel's 5 us then).
+  if (mode == kSegFallbackGrp) return;
+  if (mode == kSegFallback) {
+    // the stream did not take the batch: k_crc_any's work over every message,
+    // in this launch (round 3 launched k_crc_any after the combine, ~5 us a
+    // call even when it exits at once); the body fills its own tables
+    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, 0u, 0u, crc_out, nullptr, nullptr, tables, nullptr, 0);
+    return;
+  }
   {  // rs, iv and sh1 are contiguous in SegTables: every load issued before the first store
     static_assert(offsetof(SegTables, iv) == offsetof(SegTables, rs) + sizeof(SegTables::rs), "rs, iv adjacent");
     static_assert(offsetof(SegTables, sh1) == offsetof(SegTables, iv) + sizeof(SegTables::iv), "iv, sh1 adjacent");
@@ -2188,23 +2208,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
       if (i < kQ) reinterpret_cast<uint4 *>(tl)[i] = t[k];
     }
   }
-  const uint32_t mode = *flag;
-  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks)
-    *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : mode == kSegGapSmall ? 4u : 0u;
   __syncthreads();
-  if (mode == kSegFallback) {
-    // the stream did not take the batch: k_crc_any's work over every message,
-    // in this launch (round 3 launched k_crc_any after the combine, ~5 us a
-    // call even when it exits at once).  The tables above are not used: the
-    // body fills its own over them, after the barrier.
-    crc_any_body<true>(tl, base, offs, lens, 0, 0, flags, n, 0u, 0u, crc_out, nullptr, nullptr, tables, nullptr, 0);
-    return;
-  }
-  // kSegFallbackGrp: k_crc_grp, launched after this kernel and gated on the
-  // mode word, takes the batch.  (Round 5 first ran
-  // k_crc_grp's body here, before the sweep: the combine then faulted on the
-  // plain fallback and took 34 ms for 1M aligned records, profiles/r5/r5d/.)
-  if (mode == kSegFallbackGrp) return;
   const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni(threadIdx.x >> 6);
