@@ -89,10 +89,11 @@ WORKLOADS = {
     "blocks4092": (1_000_000, 4092, "weak"),
     "blocks8188": (500_000, 8188, "weak"),
 }
-# the dominant kernel per workload (PMC passes)
-KERNEL_RE = {"frame": r"k_frame\(", "unframe": "k_unframe", "unframe8k": "k_unframe", "unframe16k": "k_unframe",
-             "records": "k_seg_stream", "records_gapped": "k_seg_stream",
-             "records4k_shuffled": "k_seg_combine", "blocks4092": "k_crc_any", "blocks8188": "k_seg_stream"}  # else the streaming CRC kernel
+# PMC passes count every kernel a dispatch launches (plan, stream, combine, the
+# gated k_crc_grp / k_crc_any fallbacks, the block-route helpers), not one
+# kernel: the traffic of a multi-kernel dispatch is their sum
+PMC_KERNELS = r"k_(crc|seg|frame|unframe)"
+PMC_EXCLUDE = ("k_fill", "k_verify_prepare")
 SEG_WORKLOADS = ("records", "records_gapped", "records4k_shuffled", "blocks4092", "blocks8188")  # on k_seg_*: stream_mode
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
@@ -163,15 +164,15 @@ def pmc_traffic(args):
     if not exe:
         return None, "rocprofv3 not found"
     out = {}
-    kern = KERNEL_RE.get(args.workload, "k_crc_(grp|uni|fast)")
+    steps = 3
     tmp = tempfile.mkdtemp(prefix="hc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-    child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
+    child = [sys.executable, os.path.abspath(__file__), "--child", "--steps", str(steps), "--warmup", "1",
              "--workload", args.workload, "--cpu-seconds", "0", "--pmc", "off", "--settle", "0"]
     if args.blocks:
         child += ["--blocks", str(args.blocks)]
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(tmp, ctr)
-        cmd = [exe, "--pmc", ctr, "--kernel-include-regex", kern, "--output-format", "csv",
+        cmd = [exe, "--pmc", ctr, "--kernel-include-regex", PMC_KERNELS, "--output-format", "csv",
                "-d", d, "-o", "run", "--"] + child
         try:
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=300,
@@ -180,25 +181,48 @@ def pmc_traffic(args):
             return None, f"rocprofv3 {ctr} pass timed out"
         if r.returncode != 0:
             return None, f"rocprofv3 {ctr} pass failed rc={r.returncode}: {r.stdout[-400:].decode(errors='replace')}"
-        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        vals = []
-        for f in files:
+        rows = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    if re.search(kern, row.get("Kernel_Name", "")) and row.get("Counter_Name") == ctr:
-                        vals.append(float(row["Counter_Value"]))
-        if not vals:
+                rows += [row for row in csv.DictReader(fh) if row.get("Counter_Name") == ctr]
+        out[ctr] = dispatch_traffic(rows, steps)
+        if not out[ctr]:
             return None, f"no {ctr} rows"
-        out[ctr] = vals
     shutil.rmtree(tmp, ignore_errors=True)
     # units: KiB; gfx950 FETCH_SIZE reports half the bytes of 16-B/lane streaming
-    # reads (MI355X_MICROARCH.md "HBM") -> x2.  Skip the first (warmup) dispatch.
-    f = out["FETCH_SIZE"][1:] or out["FETCH_SIZE"]
-    w = out["WRITE_SIZE"][1:] or out["WRITE_SIZE"]
-    fetch = 2.0 * 1024.0 * sum(f) / len(f)
-    write = 1024.0 * sum(w) / len(w)
+    # reads (MI355X_MICROARCH.md "HBM") -> x2
+    by_kernel = {k: 2.0 * 1024.0 * out["FETCH_SIZE"].get(k, 0.0) + 1024.0 * out["WRITE_SIZE"].get(k, 0.0)
+                 for k in sorted(set(out["FETCH_SIZE"]) | set(out["WRITE_SIZE"]))}
+    fetch = 2.0 * 1024.0 * sum(out["FETCH_SIZE"].values())
+    write = 1024.0 * sum(out["WRITE_SIZE"].values())
     return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write,
-            "raw_fetch_kib": sum(f) / len(f), "raw_write_kib": sum(w) / len(w)}, None
+            "by_kernel": {k: round(v) for k, v in by_kernel.items()},
+            "raw_fetch_kib": sum(out["FETCH_SIZE"].values()), "raw_write_kib": sum(out["WRITE_SIZE"].values())}, None
+
+
+def dispatch_traffic(rows, steps):
+    """Per-dispatch counter value of every kernel the timed dispatches launch:
+    rows are rocprofv3 counter_collection rows of one counter, in dispatch
+    order.  A kernel belongs to the dispatch when it ran at least `steps` + 1
+    times (warmup + timed); its value is the mean of its last `steps` rows (a
+    kernel the workload's setup also launched -- the stamp before verify --
+    keeps only the timed ones).  Returns {short kernel name: mean value}."""
+    per = {}
+    for row in rows:
+        m = re.search(r"\b(k_[a-z0-9_]+)(<[^>]*>)?", row.get("Kernel_Name", ""))
+        if not m or m.group(1) in PMC_EXCLUDE:
+            continue
+        per.setdefault(m.group(0), []).append(float(row["Counter_Value"]))  # one entry per template instance
+    return {k: sum(v[-steps:]) / steps for k, v in per.items() if len(v) >= steps + 1}
+
+
+def bytes_kernel(dispatch, seg_mode):
+    """The kernel that moved the bytes of a dispatch: the stream's mode word says
+    which of the packed-record path's kernels did the work."""
+    if seg_mode in (False, None) or not dispatch.startswith("k_seg_plan"):
+        return dispatch
+    return {"packed": "k_seg_stream", "gapped": "k_seg_stream", "gapped_wide": "k_seg_stream",
+            "fallback_grp": "k_crc_grp", "fallback": "k_seg_combine"}.get(seg_mode, dispatch)
 
 
 def mixed_sizes(seed, lo, n):
@@ -272,16 +296,27 @@ def cgroup_throttled_us():
     return None
 
 
+WARM_AGREE = 0.05   # warm-up ends when two consecutive warm-up slices agree within 5 %
+WARM_CAP_S = 6.0    # ... or after this long (1.8 s did not reach steady state)
+
+
 def _slices(fn, nbytes, budget_s):
     """N_SLICES timed slices of fn (0.08 of the budget each), separated by idle
     gaps of 0.1 s so that one burst of another tenant on the host lands in one
-    slice rather than in all of them; the median is the reported value.  Also
-    returns how long the cgroup's CPU quota throttled the process in each slice
-    (the quota covers every thread of the container, not only the timed ones)."""
-    out, thr = [], []
-    t_warm = time.perf_counter()  # untimed: the host's cores ramp up (slices rose 110 -> 199 GiB/s without it)
-    while time.perf_counter() - t_warm < 0.15 * budget_s:
-        fn()
+    slice rather than in all of them; the median is the reported value.  Before
+    them an untimed warm-up of slices of the same length, until two consecutive
+    ones agree within WARM_AGREE (at most WARM_CAP_S): the host's cores ramp up
+    over seconds (round 5's first slices read 113-139 GiB/s, the rest 162-169).
+    Also returns how long the cgroup's CPU quota throttled the process in each
+    slice (the quota covers every thread of the container, not only the timed
+    ones), and the warm-up's slices and length."""
+    out, thr, warm = [], [], []
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < WARM_CAP_S:
+        warm.append(_rate(fn, nbytes, 0.08 * budget_s))
+        if len(warm) >= 2 and abs(warm[-1] / warm[-2] - 1.0) <= WARM_AGREE:
+            break
+    warm_s = time.perf_counter() - t_warm
     for k in range(N_SLICES):
         if k:
             time.sleep(0.1)
@@ -289,20 +324,23 @@ def _slices(fn, nbytes, budget_s):
         out.append(_rate(fn, nbytes, 0.08 * budget_s))
         t1 = cgroup_throttled_us()
         thr.append(None if t0 is None or t1 is None else round((t1 - t0) / 1e3, 1))
-    return out, thr
+    return out, thr, {"warmup_s": round(warm_s, 2), "warmup_slices": [round(x, 2) for x in warm],
+                      "warmup_converged": len(warm) >= 2 and abs(warm[-1] / warm[-2] - 1.0) <= WARM_AGREE}
 
 
 def _spread(sl, budget_s, threads):
     import numpy as np
-    slices, thr = sl
+    slices, thr, warm = sl
     med = float(np.median(slices))
     return {"spread": [round(min(slices), 3), round(max(slices), 3)],
             "spread_pct": [round(100.0 * (min(slices) / med - 1.0), 1), round(100.0 * (max(slices) / med - 1.0), 1)],
             "slices": [round(x, 2) for x in slices],
             "slices_throttled_ms": thr,
+            **warm,
             "spread_note": f"min/max of {len(slices)} slices of {0.08 * budget_s:.2f} s on {threads} threads after "
-                           f"{0.15 * budget_s:.1f} s of untimed warm-up, 0.1 s idle between slices, work handed to "
-                           f"the threads in 64-block chunks; "
+                           f"an untimed warm-up of slices of the same length until two consecutive ones agreed "
+                           f"within {100 * WARM_AGREE:.0f} % (cap {WARM_CAP_S:.0f} s; warmup_s, warmup_slices), "
+                           f"0.1 s idle between slices, work handed to the threads in 64-block chunks; "
                            f"slices_throttled_ms: time the cgroup CPU quota (cgroup_cpu_quota CPUs for the "
                            f"whole container) stalled the process during each slice"}
 
@@ -849,19 +887,23 @@ def main(argv=None):
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else round(traffic["bytes"]),
-                "kernel": info["kernel"], "bytes_per_launch": step_bytes,
+                "traffic_ratio": None if traffic is None else round(traffic["bytes"] / step_bytes, 4),
+                "kernel": bytes_kernel(info["kernel"], seg_mode), "dispatch": info["kernel"],
+                "bytes_per_launch": step_bytes,
                 "mean_launch_ms": round(mean_kern_s * 1e3, 4),
                 "launch_timing": ("HIP events on the launch stream around the K timed launches; mean = span / K "
                                   "(includes the gaps between launches)" if args.kernel_events == "bracket"
                                   else "HIP events on the launch stream around every timed launch"),
                 "frac_vs_copy_ceiling": round(achieved / COPY_CEILING_GBS, 4),
                 "copy_ceiling_note": "guide's measured float4 copy, 6.29 TB/s read+write; a read stream can exceed it",
-                **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine (the fallback for a "
-                                   "batch the stream refuses runs inside the combine); traffic: k_seg_stream"}
+                **({"launch_note": "one dispatch = k_seg_plan + k_seg_stream + k_seg_combine (+ the gated "
+                                   "k_crc_grp launch for >= 2^18 records); `kernel` is the one the stream's mode "
+                                   "word gave the bytes to (stream_mode)"}
                    if args.workload in SEG_WORKLOADS else {}),
-                "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch "
-                                 f"(fetch {traffic['fetch_bytes']:.4g} B, write {traffic['write_bytes']:.4g} B)"
-                                 if traffic else f"null: {pmc_note}")}
+                **({"traffic_by_kernel": traffic["by_kernel"]} if traffic else {}),
+                "traffic_note": (f"PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per dispatch, summed over every kernel "
+                                 f"it launches (fetch {traffic['fetch_bytes']:.4g} B, write "
+                                 f"{traffic['write_bytes']:.4g} B)" if traffic else f"null: {pmc_note}")}
         host_leg = None
         if world == 1 and (args.host_leg == "on" or (args.host_leg == "auto" and args.workload == "northstar")):
             phase("host_leg")

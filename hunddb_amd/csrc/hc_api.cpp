@@ -241,9 +241,13 @@ uint64_t seg_min_blocks() { return (uint64_t)std::max<int64_t>(1, knob(kKnobSegM
 // 8188 5.76 / 6.20, 12000 5.69 / 6.28, 16380 5.18 / 6.34, 65532 6.40 / 6.48;
 // at an address that is not 4-B aligned 4092 5.02 / 5.42, 4096 5.19 / 5.45,
 // 8192 5.00 / 6.05.  k_crc_any keeps 4-B aligned blocks of 2-8 KiB.
-bool seg_blocks_preferred(const uint8_t *base, uint64_t stride, uint32_t ulen) {
-  const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) | stride) & 3u) == 0;
-  return !(aligned4 && ulen > 2048 && ulen < 8000);
+// A uniform whole-message batch (HC_F_MESSAGES, messages of ulen at base +
+// j * stride) is the same stream work as blocks of ulen + 4 bytes at base - 4.
+bool seg_blocks_preferred(const uint8_t *base, uint64_t stride, uint32_t ulen, bool msg = false) {
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base) - (msg ? 4u : 0u);
+  const uint64_t l = (uint64_t)ulen + (msg ? 4u : 0u);
+  const bool aligned4 = ((b | stride) & 3u) == 0;
+  return !(aligned4 && l > 2048 && l < 8000);
 }
 
 // The span bound of a batch at `base` (the allocation holding it), as k_seg_*'s unit count; 0 if unknown.
@@ -303,7 +307,9 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       e = launch_fast(b, fast_grid, s);
       info.fast_blocks = n;
     } else if (seg_ok && ulen >= 4 && stride >= ulen && n >= seg_min_blocks() && n < 0x7FFFFFFFull &&
-               seg_blocks_preferred(base, stride, ulen) && seg_blocks(d, b, s, fast_grid, e)) {
+               (!(flags & kFlagMessages) || crc_out) &&
+               seg_blocks_preferred(base, stride, ulen, (flags & kFlagMessages) != 0) &&
+               seg_blocks(d, b, s, fast_grid, e)) {
       info.kernel = "k_seg_plan+k_seg_stream+k_seg_combine";
       info.fast_blocks = n;
       t_seg_dev = dev;

@@ -369,10 +369,14 @@ __global__ __launch_bounds__(kFastThreads) void k_crc_fast(const uint8_t *base, 
 // The variants measured against this one before round 4 (static deal, batched
 // refills, nibble finalise tables, timing-only build) are in git history
 // (tools/ab_hc_kernels.hip, up to commit 61a2e0e).
-// The body, a device function: the k_crc_grp kernel below, and k_seg_combine
-// for a batch of mostly 4 KiB-multiple records the packed-record stream did not
-// take (out of order, overlapping: the fallback in the same launch).  `lds`
-// holds kFastLdsBytes of tables and the 8 KiB sh512 table after them.
+// The body, a device function called by the k_crc_grp kernel below only.  (Round
+// 5 also ran it inside k_seg_combine, ahead of crc_any_body behind a runtime
+// mode: hipcc then left the implicit-argument pointer that gridDim.x is read
+// through written on this body's path only, and the plain fallback read it from
+// a stale SGPR pair -- the r5d illegal address; DESIGN.md 4.2a,
+// tests/test_isa_sgpr_defs.py.  The packed-record stream's k_crc_grp fallback is
+// a separate gated launch.)  `lds` holds kFastLdsBytes of tables and the 8 KiB
+// sh512 table after them.
 template <bool kArrays, bool kXcd>
 __device__ __forceinline__ void crc_grp_body(uint32_t *lds, uint32_t &s_next, const uint8_t *base,
                                              const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
@@ -2180,8 +2184,10 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
     *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : mode == kSegGapSmall ? 4u : 0u;
   // kSegFallbackGrp: k_crc_grp, launched after this kernel and gated on the
   // mode word, takes the batch.  (Round 5 first ran k_crc_grp's body here,
-  // before the sweep: the combine then faulted on the plain fallback and took
-  // 34 ms for 1M aligned records, profiles/r5/r5d/.)  Neither fallback needs
+  // before the sweep: the plain fallback then read gridDim.x through an SGPR
+  // pair hipcc wrote on the k_crc_grp path only -- an illegal address,
+  // profiles/r5/r5d/, r6/fault/; the 34 ms on 1M aligned records was the plan's
+  // O(n x units) fill of that build.)  Neither fallback needs
   // the SegTables below (r5: their fill was most of this kernel's 5 us then).
   if (mode == kSegFallbackGrp) return;
   if (mode == kSegFallback) {
@@ -2365,12 +2371,13 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
 }
 
 // A uniform block batch k_crc_grp refuses, on the message stream
-// (launch_seg_blocks): its messages block[4:ulen] as off/len arrays ...
-__global__ __launch_bounds__(256) void k_seg_block_msgs(uint64_t n, uint64_t stride, uint32_t ulen,
+// (launch_seg_blocks): its messages block[hdr:ulen] as off/len arrays (hdr 4:
+// the payload after the stored word; 0: a uniform whole-message batch) ...
+__global__ __launch_bounds__(256) void k_seg_block_msgs(uint64_t n, uint64_t stride, uint32_t ulen, uint32_t hdr,
                                                         uint64_t *__restrict__ moff, uint32_t *__restrict__ mlen) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    moff[j] = j * stride + 4u;
-    mlen[j] = ulen - 4u;
+    moff[j] = j * stride + hdr;
+    mlen[j] = ulen - hdr;
   }
 }
 
@@ -2386,13 +2393,31 @@ __global__ __launch_bounds__(256) void k_seg_block_out(const uint8_t *base, uint
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  // The route exists for blocks k_crc_grp refuses, often at addresses that are
+  // not 4-B aligned: then the stored word is read and written bytewise (ADVICE
+  // r5: a misaligned u32 access is UB the compiler may lower assuming alignment)
+  const bool al4 = (((uintptr_t)base | stride) & 3u) == 0;  // kernel-uniform
+  auto get32 = [&](const uint8_t *q) -> uint32_t {
+    if (al4) return *reinterpret_cast<const uint32_t *>(q);
+    return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  };
+  auto put32 = [&](uint8_t *q, uint32_t v) {  // PutUint32LE
+    if (al4) {
+      *reinterpret_cast<uint32_t *>(q) = v;
+    } else {
+      q[0] = (uint8_t)v;
+      q[1] = (uint8_t)(v >> 8);
+      q[2] = (uint8_t)(v >> 16);
+      q[3] = (uint8_t)(v >> 24);
+    }
+  };
   for (uint64_t c = w0 * 64u; c < n; c += nw * 64u) {
     const uint64_t j = c + lane;
     const bool in = j < n;
-    uint32_t *p = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(base) + (in ? j : 0) * stride);
+    uint8_t *p = const_cast<uint8_t *>(base) + (in ? j : 0) * stride;
     const uint32_t crc = in ? crcs[j] : 0u;
     if (first_bad) {
-      const uint32_t stored = in ? *p : 0u;
+      const uint32_t stored = in ? get32(p) : 0u;
       const uint64_t bad = __ballot(in && stored != crc);
       if (bad) {  // wave-uniform
         if (bad_bitmap && lane == 0 && (uint32_t)bad) atomicOr(bad_bitmap + (c >> 5), (uint32_t)bad);
@@ -2400,7 +2425,7 @@ __global__ __launch_bounds__(256) void k_seg_block_out(const uint8_t *base, uint
         if (lane == 0) atomicMin(first_bad, (unsigned long long)(c + (uint64_t)__builtin_ctzll(bad)));
       }
     }
-    if (in && (flags & kFlagStamp)) *p = crc;
+    if (in && (flags & kFlagStamp)) put32(p, crc);
   }
 }
 
@@ -2573,13 +2598,17 @@ uint64_t seg_block_workspace_bytes(uint64_t n, uint64_t max_units, bool crc_word
 hipError_t launch_seg_blocks(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid,
                              hipStream_t s, uint32_t *taken) {
   const uint64_t n = b.nblocks;
-  if (!b.base || b.off || b.len || b.ulen < 4 || b.stride < b.ulen || !st || !ws || n == 0 ||
-      (b.flags & kFlagMessages) || !b.tables)
+  // whole-message mode (a uniform HC_F_MESSAGES batch): the messages are the
+  // strided entries themselves, and crc_out is their only output (k_crc_any
+  // neither verifies nor stamps messages)
+  const bool msg = (b.flags & kFlagMessages) != 0;
+  if (!b.base || b.off || b.len || b.ulen < 4 || b.stride < b.ulen || !st || !ws || n == 0 || !b.tables ||
+      (msg && !b.crc_out))
     return hipErrorInvalidValue;
   uint64_t *moff = reinterpret_cast<uint64_t *>(ws + ((seg_workspace_bytes(n, max_units) + 7) & ~7ull) / 4);
   uint32_t *mlen = reinterpret_cast<uint32_t *>(moff + n), *wcrc = mlen + n;
   const int mg = (int)std::min<uint64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_seg_block_msgs, dim3(mg), dim3(256), 0, s, n, b.stride, b.ulen, moff, mlen);
+  hipLaunchKernelGGL(k_seg_block_msgs, dim3(mg), dim3(256), 0, s, n, b.stride, b.ulen, msg ? 0u : 4u, moff, mlen);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   Batch mb = b;
@@ -2591,7 +2620,7 @@ hipError_t launch_seg_blocks(const Batch &b, const SegTables *st, uint32_t *ws, 
   mb.first_bad = nullptr;
   // no k_crc_grp fallback: these blocks are not its shape, and its fallback would hash whole messages
   if ((e = launch_seg(mb, st, ws, max_units, grid, s, taken, ~0ull)) != hipSuccess) return e;
-  if (!b.first_bad && !(b.flags & kFlagStamp)) return hipSuccess;
+  if (msg || (!b.first_bad && !(b.flags & kFlagStamp))) return hipSuccess;
   hipLaunchKernelGGL(k_seg_block_out, dim3(mg), dim3(256), 0, s, b.base, n, b.stride, b.flags, mb.crc_out,
                      b.bad_bitmap, b.first_bad);
   return hipGetLastError();

@@ -9,6 +9,7 @@
 #include <deque>
 #include <mutex>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -71,7 +72,12 @@ inline int64_t parse_inject(const char *v) {
     const size_t n = std::strlen(sites[k]);
     if (std::strncmp(v, sites[k], n) != 0) continue;
     if (v[n] == 0) return k + 1;
-    if (v[n] == ':' && std::strcmp(v + n + 1, "nomem") == 0) return (k + 1) | kInjectNomem;
+    if (v[n] != ':') continue;
+    if (std::strcmp(v + n + 1, "nomem") == 0) return (k + 1) | kInjectNomem;
+    // any other suffix keeps the site's HC_E_HIP failure (round 4's meaning of
+    // "<site>:<anything>"), so a script with a typo still runs the host recovery
+    std::fprintf(stderr, "hundcrc: HC_INJECT_FAIL=%s: unknown suffix, injecting HC_E_HIP at %s\n", v, sites[k]);
+    return k + 1;
   }
   return 0;  // an unknown site injects nothing
 }

@@ -349,7 +349,11 @@ int hc_debug_seg_taken(void);
  * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
  * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN, HC_SEG_MIN_BLOCKS.  hc_debug_set changes one of them afterwards
  * (tests and tools); value NULL restores the compiled default.  HC_OK, or
- * HC_E_ARG for an unknown name. */
+ * HC_E_ARG for an unknown name.
+ * HC_INJECT_FAIL (test hook) accepts "add_crcs", "read_from_disk" or
+ * "wal_replay": that GPU batch reports HC_E_HIP and the host path finishes it;
+ * "<site>:nomem" reports HC_E_NOMEM instead; "<site>:<other>" keeps HC_E_HIP
+ * (with a note on stderr); an unknown site injects nothing. */
 int hc_debug_set(const char *name, const char *value);
 
 /* Number of visible gfx950 devices (0 if none; never initialises a context

@@ -25,9 +25,11 @@ CASES = {
     "unframe": (4096, "k_unframe", 4096 * (4096 + 4092)),
     "unframe8k": (2048, "k_unframe", 2048 * (8192 + 8188)),
     "unframe16k": (1024, "k_unframe", 1024 * (16384 + 16380)),
-    "records": (4096, None, None),
-    "records_gapped": (4096, None, None),
-    "records4k_shuffled": (4096, None, None),
+    "records": (4096, "k_seg_stream", None),                 # packed: the stream did the bytes
+    "records_gapped": (4096, "k_seg_stream", None),
+    # >= HC_SEG_GRP_MIN (2^18) shuffled aligned records: the stream refuses them and the
+    # gated k_crc_grp launch moves the bytes (name that kernel)
+    "records4k_shuffled": (300_000, "k_crc_grp", 300_000 * (4096 + 4)),
     "blocks4092": (4096, "k_crc_any", 4096 * 4092),           # 4-B aligned 4092-B blocks stay on k_crc_any
     "blocks8188": (4096, None, 4096 * 8188),                  # the message stream (launch_seg_blocks)
 }
@@ -55,6 +57,9 @@ def test_bench_workload_small(workload):
         assert roof["bytes_per_launch"] == nbytes
     if workload == "verify":
         assert res["config"]["verify_clean"] is True
+    if workload == "records4k_shuffled":
+        assert res["config"]["stream_mode"] == "fallback_grp"
+        assert roof["dispatch"].startswith("k_seg_plan")
 
 
 @pytest.mark.gpu

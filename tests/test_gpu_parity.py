@@ -469,12 +469,14 @@ def test_default_thresholds_route(knobs, cuda, hc, oracle):
         assert hc.stats()["wal_gpu"] == (1 if gpu else 0), nb
 
 
-@pytest.mark.parametrize("inject", ["", "add_crcs", "add_crcs:nomem"])
+@pytest.mark.parametrize("inject", ["", "add_crcs", "add_crcs:nomem", "add_crcs:typo"])
 def test_add_crcs_gpu_failure_finishes_on_host(knobs, cuda, hc, oracle, monkeypatch, inject):
     """VERDICT r3 weak 3 on the box: with a gfx950 present the multi-block
     AddCRCsToData is one GPU batch (hc_stats add_crcs_gpu); a failing batch
     (HC_INJECT_FAIL: HC_E_HIP / HC_E_NOMEM) is finished on the host path,
-    byte-exact vs the oracle, counted as a fallback; HC_FORCE_GPU returns it."""
+    byte-exact vs the oracle, counted as a fallback; HC_FORCE_GPU returns it.
+    "<site>:<other suffix>" keeps the HC_E_HIP failure (it injected
+    nothing in round 5)."""
     rng = np.random.default_rng(13)
     n = 4092 * 4000 + 333
     src = rng.integers(0, 256, n, dtype=np.uint8).tobytes()

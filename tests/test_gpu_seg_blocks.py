@@ -126,3 +126,41 @@ def test_threshold_keeps_small_batches_on_k_crc_any(cuda, hc, oracle, knobs):
     got, _, _ = run(torch, hc, torch.from_numpy(host).cuda(), n, ulen, ulen)
     assert (got == oracle.crc32_blocks(host, stride=ulen, ulen=ulen, nblocks=n)).all()
     assert hc.seg_path() == "gapped"
+
+
+MSG_CASES = [  # (ulen, stride - ulen, start): uniform HC_F_MESSAGES batches k_crc_grp refuses
+    (100, 0, 0),     # 100-B messages back to back: packed
+    (1000, 3, 1),    # odd address, 3-B gaps
+    (4096, 0, 1),    # 4 KiB messages at an odd address
+    (8190, 2, 2),    # 8 KiB-ish, 2-B gaps
+    (4000, 96, 0),   # 4-B aligned 4004-B equivalent blocks: kept on k_crc_any (seg_blocks_preferred)
+    (5, 11, 3),      # tiny messages
+]
+
+
+@pytest.mark.parametrize("ulen,extra,start", MSG_CASES)
+def test_uniform_messages_route(cuda, hc, oracle, ulen, extra, start):
+    """a uniform whole-message batch (HC_F_MESSAGES with stride/ulen,
+    no off/len) of >= HC_SEG_MIN_BLOCKS entries that k_crc_grp cannot take went to
+    launch_seg_blocks, which refused message mode: HC_E_HIP and no words.  Now the
+    route builds whole-message off/len (j * stride, ulen); every word against the
+    oracle's GetCRC (crc_util.go:15-17), at the default threshold."""
+    torch = cuda
+    stride = ulen + extra
+    n = max(5000, (16 << 20) // stride)
+    rng = np.random.default_rng(ulen * 3 + extra + start)
+    host = rng.integers(0, 256, start + n * stride + 64, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    view = buf[start:]
+    got, _, _ = run(torch, hc, view, n, stride, ulen, flags=hc.HC_F_MESSAGES)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(start)
+    want = oracle.crc32_messages(host, off, np.full(n, ulen, np.uint32))
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:8], got[bad[:8]], want[bad[:8]])
+    ptr = view.data_ptr()
+    if not preferred(ptr - 4, stride, ulen + 4) or ulen < 4:
+        assert hc.last_launch()["kernel"] == "k_crc_any"
+    else:
+        assert hc.last_launch()["kernel"].startswith("k_seg_plan")
+        moff = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        assert hc.seg_path() == (expected_path(ptr, moff, np.full(n, ulen, np.uint64)) or "fallback")

@@ -14,8 +14,9 @@ the blocks starting where the WAL segment files put them.
 - The per-record variant on the device: GetCRC of all 10M records packed back
   to back in HBM (the packed-record stream), every word against the oracle
   (the span copied back in 4 GiB segments); the same records with a 17-B WAL
-  header gap before each (the gapped stream), every word against the packed
-  run; and word for word against k_crc_any (an overlap forces the fallback).
+  header gap before each (the gapped stream), every word against the oracle
+  again (its own copy-back of the gapped span); and word for word against
+  k_crc_any (an overlap forces the fallback).
 
 Host memory: ~108 GB (one image); the box allows ~270 GiB per command.
 

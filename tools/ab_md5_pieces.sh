@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 5: k_md5 with aligned stage pieces (production) against the unaligned pieces of r5p
-# (tools/ab/md5old, built from profiles/r5/variants/hc_md5_unaligned_pieces.hip), alternating
+# round 5: k_md5 with aligned stage pieces (the variant then under test) against the unaligned
+# pieces of r5p (tools/ab/md5old, built from hunddb_amd/csrc/hc_md5.hip: production), alternating
 set -e
 O=gpurun_out/${TAG:-r5w}
 mkdir -p $O

@@ -48,7 +48,8 @@ def main():
             dlen = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).cuda()
             res = {}
             for path, env in (("seg", "1"), ("any", str(1 << 40))):
-                os.environ["HC_SEG_MIN_MSGS"] = env
+                # the library reads HC_* once at first use: hc_debug_set, not os.environ
+                hc.debug_set("HC_SEG_MIN_MSGS", env)
                 out = torch.zeros(n, dtype=torch.int32, device="cuda")
 
                 def call():
@@ -73,7 +74,7 @@ def main():
                               "seg_speedup": round(res["any"][0] / res["seg"][0], 3)}), flush=True)
             if not same:
                 sys.exit(1)
-    os.environ.pop("HC_SEG_MIN_MSGS", None)
+    hc.debug_set("HC_SEG_MIN_MSGS", None)
 
 
 if __name__ == "__main__":
