@@ -83,6 +83,10 @@ WORKLOADS = {
     # GetCRC of 1M aligned 4 KiB records in shuffled order: the
     # stream refuses them; its fallback runs k_crc_grp's body inside the combine
     "records4k_shuffled": (1_000_000, "records4k_shuffled", "weak"),
+    # config 5's records (log-uniform 64 B - 64 KiB, back to back from an odd
+    # address) with their off/len arrays in a permuted order:
+    # the plan finds them unsorted, so the stream refuses them
+    "records_shuffled": (2_000_000, "records_shuffled", "weak"),
     # uniform blocks k_crc_grp refuses (config.go:241 allows any BlockSize >= 1024): 1M x 4092 B
     # (k_crc_any: the route it wins, hc_api.cpp seg_blocks_preferred) and 0.5M x 8188 B (their
     # messages block[4:] on the stream's small-gap mode, launch_seg_blocks; round 5)
@@ -94,7 +98,7 @@ WORKLOADS = {
 # kernel: the traffic of a multi-kernel dispatch is their sum
 PMC_KERNELS = r"k_(crc|seg|frame|unframe)"
 PMC_EXCLUDE = ("k_fill", "k_verify_prepare")
-SEG_WORKLOADS = ("records", "records_gapped", "records4k_shuffled", "blocks4092", "blocks8188")  # on k_seg_*: stream_mode
+SEG_WORKLOADS = ("records", "records_gapped", "records4k_shuffled", "records_shuffled", "blocks4092", "blocks8188")  # on k_seg_*: stream_mode
 UNFRAME_B = {"unframe": 4096, "unframe8k": 8192, "unframe16k": 16384}  # f1 block sizes
 
 
@@ -221,6 +225,8 @@ def bytes_kernel(dispatch, seg_mode):
     which of the packed-record path's kernels did the work."""
     if seg_mode in (False, None) or not dispatch.startswith("k_seg_plan"):
         return dispatch
+    if seg_mode.startswith("sorted_"):  # the sort's phases ran in k_seg_stream too (DESIGN.md 4.2b)
+        return "k_seg_stream"
     return {"packed": "k_seg_stream", "gapped": "k_seg_stream", "gapped_wide": "k_seg_stream",
             "fallback_grp": "k_crc_grp", "fallback": "k_seg_combine"}.get(seg_mode, dispatch)
 
@@ -280,6 +286,74 @@ def cores_available():
 
 
 N_SLICES = 7
+_AFFINITY0 = os.sched_getaffinity(0)  # the process's own set (the baseline pins itself inside it)
+
+
+def _cpu_idle():
+    """Per logical CPU idle + iowait jiffies (/proc/stat), or {} if unreadable."""
+    out = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    v = line.split()
+                    out[int(v[0][3:])] = int(v[4]) + int(v[5])
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
+def quiet_cores(n, sample_s=0.3):
+    """n logical CPUs of this process's affinity set on n distinct physical
+    cores (no two on SMT siblings), the most idle ones over sample_s seconds
+    (both siblings' idle time counted); None when the topology is not readable.
+    The host is shared (16 of 256 logical CPUs by quota): unpinned, the CPU
+    baseline's 16 threads land on busy cores and on each other's siblings, and
+    its slices spread -13 / +25 % (round 6's first run)."""
+    allowed = sorted(os.sched_getaffinity(0))
+    core = {}
+    try:
+        for c in allowed:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "physical_package_id") as f:
+                pk = int(f.read())
+            with open(base + "core_id") as f:
+                core.setdefault((pk, int(f.read())), []).append(c)
+    except (OSError, ValueError):
+        return None
+    if len(core) < n:
+        return None
+    a = _cpu_idle()
+    time.sleep(sample_s)
+    b = _cpu_idle()
+    idle = lambda cpus: sum(b.get(c, 0) - a.get(c, 0) for c in cpus)  # noqa: E731
+    best = sorted(core.values(), key=lambda cpus: (-idle(cpus), cpus[0]))[:n]
+    return sorted(c[0] for c in best)
+
+
+class pinned:
+    """Within the block, this thread (and the threads it starts) run on
+    quiet_cores(n); restores the previous affinity after."""
+
+    def __init__(self, n):
+        self.n, self.cpus, self.prev = n, None, None
+
+    def __enter__(self):
+        self.prev = os.sched_getaffinity(0)
+        self.cpus = quiet_cores(self.n)
+        if self.cpus:
+            os.sched_setaffinity(0, self.cpus)
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.prev)
+        return False
+
+    def info(self):
+        return {"pinned_cpus": self.cpus,
+                "pinning": ("one logical CPU per physical core, the most idle cores of the affinity set over 0.3 s "
+                            "(/proc/stat), for the whole CPU-baseline leg" if self.cpus else
+                            "none (topology not readable or too few cores)")}
 
 
 def cgroup_throttled_us():
@@ -358,7 +432,7 @@ def cpu_host():
     except OSError:
         pass
     q = cgroup_cpu_quota()
-    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "affinity_cpus": len(_AFFINITY0),
             "cgroup_cpu_quota": None if q is None else round(q, 2), "cores_available": cores_available()}
 
 
@@ -647,6 +721,7 @@ def main(argv=None):
     stream = torch.cuda.current_stream()
 
     sample = None  # (host blocks, off, lens) for the CPU baseline
+    out_sel = None  # the sample's entries of the GPU words (a permuted batch), else its first len(off)
     if bsize == "mixed":
         sizes = mixed_sizes(SEED, lo, my)
         off = np.zeros(my, dtype=np.uint64)
@@ -694,13 +769,21 @@ def main(argv=None):
         block_desc = "8192 B, verify mode (stamped; B read + 4 B written per block)"
         k = min(my, (512 << 20) // B)
         sample = (slice(0, k * B), np.arange(k, dtype=np.uint64) * B, np.full(k, B, np.uint32))
-    elif bsize in ("records", "records_gapped"):
+    elif bsize in ("records", "records_gapped", "records_shuffled"):
         lens_h = record_sizes(my) if not args.blocks else record_sizes(nblk)[:my]
         gap = 17 if bsize == "records_gapped" else 0
         off_h = np.zeros(my, dtype=np.uint64)
         off_h[1:] = np.cumsum(lens_h[:-1].astype(np.uint64) + np.uint64(gap), dtype=np.uint64)
         off_h += np.uint64(1 + gap)  # back to back (or 17 B apart) from an odd address
         total = (int(off_h[-1]) + int(lens_h[-1]) + 64 + (1 << 20) - 1) >> 20 << 20
+        k = int(np.searchsorted(off_h, 512 << 20))
+        sample = (slice(0, int(off_h[k - 1]) + int(lens_h[k - 1])), off_h[:k].copy(), lens_h[:k].copy())
+        if bsize == "records_shuffled":  # the same records, listed in a permuted order
+            perm = np.random.default_rng(SEED).permutation(my)
+            off_h, lens_h = off_h[perm], lens_h[perm]
+            sel = np.flatnonzero(off_h < np.uint64(512 << 20))  # the sample: the records of its first 512 MiB
+            sample = (sample[0], off_h[sel].copy(), lens_h[sel].copy())
+            out_sel = sel
         buf = torch.empty(total, dtype=torch.uint8, device=dev)
         crc.dev_fill_range(buf, SEED, lo << 20, total >> 20, stride=1 << 20, ulen=1 << 20)
         doff = torch.from_numpy(off_h.view(np.int64)).to(dev)
@@ -708,9 +791,8 @@ def main(argv=None):
         kw = dict(off=doff, lens=dlen, nblocks=my, flags=crc.HC_F_MESSAGES)
         step_bytes = int(lens_h.sum(dtype=np.uint64)) + 4 * my
         block_desc = ("GetCRC per record: log-uniform 64 B - 64 KiB records " +
-                      ("with a 17-B gap before each" if gap else "back to back") + " (off/len arrays)")
-        k = int(np.searchsorted(off_h, 512 << 20))
-        sample = (slice(0, int(off_h[k - 1]) + int(lens_h[k - 1])), off_h[:k].copy(), lens_h[:k].copy())
+                      ("with a 17-B gap before each" if gap else "back to back") +
+                      (", listed in a permuted order" if bsize == "records_shuffled" else "") + " (off/len arrays)")
     elif bsize == "records4k_shuffled":
         buf = torch.empty(my * 4096, dtype=torch.uint8, device=dev)
         crc.dev_fill_range(buf, SEED, lo, my, stride=4096, ulen=4096)
@@ -914,16 +996,21 @@ def main(argv=None):
         if not args.cpu_threads:
             args.cpu_threads = cores_available()
         if world == 1 and args.cpu_seconds > 0:
-            if bsize == "frame" or bsize in UNFRAME_B:
-                cpu = cpu_baseline_framing("frame" if bsize == "frame" else "unframe", buf, args.cpu_threads,
-                                           args.cpu_seconds, B=UNFRAME_B.get(bsize, 4096))
-            elif sample is not None:
-                sl, soff, slen = sample
-                host = buf[sl].cpu().numpy()
-                cpu = cpu_baseline(host, soff, slen, args.cpu_threads, args.cpu_seconds,
-                                   f"{args.workload} ({block_desc})",
-                                   gpu_words=out[: len(soff)].cpu().numpy().view(np.uint32),
-                                   messages=bsize in ("records", "records_gapped", "records4k_shuffled"))
+            with pinned(args.cpu_threads) as pin:
+                if bsize == "frame" or bsize in UNFRAME_B:
+                    cpu = cpu_baseline_framing("frame" if bsize == "frame" else "unframe", buf, args.cpu_threads,
+                                               args.cpu_seconds, B=UNFRAME_B.get(bsize, 4096))
+                elif sample is not None:
+                    sl, soff, slen = sample
+                    host = buf[sl].cpu().numpy()
+                    gw = out.cpu().numpy().view(np.uint32)
+                    gw = gw[out_sel] if out_sel is not None else gw[: len(soff)]
+                    cpu = cpu_baseline(host, soff, slen, args.cpu_threads, args.cpu_seconds,
+                                       f"{args.workload} ({block_desc})", gpu_words=gw,
+                                       messages=bsize in ("records", "records_gapped", "records4k_shuffled",
+                                                          "records_shuffled"))
+            if cpu is not None:
+                cpu.update(pin.info())
         res = {
             "metric": METRIC,
             "value": round(gib_s, 2),
@@ -943,7 +1030,7 @@ def main(argv=None):
                        "dist_backend": backend if world > 1 else None,
                        "hbm_frac_of_8TBps": round(job_bytes / dt / world / 1e12 / 8.0, 4),
                        **({"verify_clean": verify_clean} if verify_clean is not None else {}),
-                       **({"packed_stream_taken": seg_mode in ("packed", "gapped"), "stream_mode": seg_mode}
+                       **({"packed_stream_taken": seg_mode not in ("fallback", "fallback_grp"), "stream_mode": seg_mode}
                           if seg_mode is not False else {})},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -655,19 +655,25 @@ def seg_path():
     combine hashes itself), "gapped_wide" (sorted, wider gaps, zeroed in the
     stream), "fallback_grp" (the stream's fallback for aligned 4 KiB-multiple
     records: k_crc_grp) or "fallback" (k_crc_any, or not offered to the
-    stream).  Synchronizes the device; tests and tools."""
+    stream); "sorted_packed" / "sorted_gapped" / "sorted_gapped_wide" when the
+    records were listed out of order and the stream ran over their sorted view
+    (from HC_SEG_SORT_MIN records, round 6).  Synchronizes the device; tests
+    and tools."""
     r = int(_lib().hc_debug_seg_taken())
     if r < 0:
         raise HundCRCError(r, "seg_taken")
-    return {1: "packed", 2: "gapped_wide", 3: "fallback_grp", 4: "gapped"}.get(r, "fallback")
+    return {1: "packed", 2: "gapped_wide", 3: "fallback_grp", 4: "gapped",
+            9: "sorted_packed", 10: "sorted_gapped_wide", 12: "sorted_gapped"}.get(r, "fallback")
 
 
 def seg_mode():
     """"packed" or "gapped" (either gap width) when the packed-record stream
-    took this thread's last device batch of whole messages, else None
+    took this thread's last device batch of whole messages in the batch's own
+    order, "sorted_packed" / "sorted_gapped" over its sorted view, else None
     (synchronizes the device)."""
     p = seg_path()
-    return {"packed": "packed", "gapped": "gapped", "gapped_wide": "gapped"}.get(p)
+    return {"packed": "packed", "gapped": "gapped", "gapped_wide": "gapped", "sorted_packed": "sorted_packed",
+            "sorted_gapped": "sorted_gapped", "sorted_gapped_wide": "sorted_gapped"}.get(p)
 
 
 def seg_taken() -> bool:

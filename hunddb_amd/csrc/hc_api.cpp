@@ -204,12 +204,12 @@ uint64_t seg_min_msgs() { return (uint64_t)std::max<int64_t>(0, knob(kKnobSegMin
 // The kept workspace (null stream only), grown to `need` bytes on that stream,
 // so the free is ordered after every earlier use.  The lock is held from here
 // until the caller has enqueued the launches that use it.  nullptr: allocate
-// per call.  Only workspaces up to kSegKeepBytes are kept (about 16M records):
+// per call.  Only workspaces up to kSegKeepBytes are kept:
 // a larger one would stay pinned in the default mempool for the life of the
 // process, and its per-call allocation is small against the batch.
 // Relies on the legacy null stream's ordering across host threads (hundcrc.h;
 // the library is not built with -fgpu-default-stream=per-thread).
-constexpr uint64_t kSegKeepBytes = 64ull << 20;
+constexpr uint64_t kSegKeepBytes = 512ull << 20;  // (round 6: the sort's arrays, 48 B a record: ~8M records)
 uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::unique_lock<std::mutex> &lk) {
   if (s != nullptr || need > kSegKeepBytes) return nullptr;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -333,13 +333,15 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
     // (verify or stamp only) takes k_crc_grp + k_crc_any
     if (seg_ok && (flags & kFlagMessages) && crc_out && n >= seg_min_msgs() && n < 0x7FFFFFFFull) {
       if (const uint64_t mu = seg_units_for(base)) {
-        const uint64_t need = seg_workspace_bytes(n, mu);
+        const uint64_t sort_min = (uint64_t)std::max<int64_t>(0, knob(kKnobSegSortMin));
+        const uint64_t need = seg_workspace_bytes(n, mu, sort_min && n >= sort_min);
         uint32_t *ws = seg_cached_ws(d, s, need, seg_lock);
         if (!ws && hipMallocAsync(reinterpret_cast<void **>(&seg_ws), need, s) == hipSuccess) ws = seg_ws;
         if (ws) {
           // word 0 of ws: raised when the stream did not take the batch; then
           // k_seg_combine runs k_crc_any's work over every message itself
-          e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last, (uint64_t)knob(kKnobSegGrpMin));
+          e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last, (uint64_t)knob(kKnobSegGrpMin), sort_min,
+                         (uint32_t)std::min<int64_t>(std::max<int64_t>(0, knob(kKnobSegSyncSpins)), 0xFFFFFFFF));
           seg = true;
         }
       }

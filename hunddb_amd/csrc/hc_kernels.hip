@@ -57,6 +57,9 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_a
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
+}
 
 // 16-B load from an address computed as an integer, as a GLOBAL load.  Through
 // a generic pointer hipcc emits flat_load, which also counts on lgkmcnt: every
@@ -1693,37 +1696,54 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 // payload, the span-DMA rule of the host pipeline).  Every slot is written, so
 // the dispatch needs no memset: k_seg_stream's workgroups reduce the slots and
 // its workgroup 0 stores the mode the combine reads.
-template <uint32_t kU = kSegUnitLg>
-__global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
-                                                  const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
-                                                  uint32_t *__restrict__ plan_bad, long long *__restrict__ plan_gx,
-                                                  uint32_t *__restrict__ plan_conf, uint32_t *__restrict__ first_ev) {
-  __shared__ uint32_t s_bad, s_conf;
-  __shared__ unsigned long long s_gx;
+// The plan of one batch over workgroup wg of nwg (blockDim.x threads each),
+// with the workgroup's shared words s_*: k_seg_plan's body, and the plan of
+// the sorted view inside k_seg_stream (seg_sort).  plan_min / plan_max
+// (optional): the lowest record start and highest record end of the
+// workgroup's records (the sort's key range).
+struct SegPlanShared {
+  uint32_t bad, conf;
+  unsigned long long gx, smin, emax;
+};
+template <uint32_t kU>
+__device__ __forceinline__ void seg_plan_body(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                              const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
+                                              uint32_t wg, uint32_t nwg, uint32_t *__restrict__ plan_bad,
+                                              long long *__restrict__ plan_gx, uint32_t *__restrict__ plan_conf,
+                                              uint32_t *__restrict__ first_ev,
+                                              unsigned long long *__restrict__ plan_min,
+                                              unsigned long long *__restrict__ plan_max, SegPlanShared &sh) {
   if (threadIdx.x == 0) {
-    s_bad = 0;
-    s_conf = 0;
-    s_gx = 0;
+    sh.bad = 0;
+    sh.conf = 0;
+    sh.gx = 0;
+    sh.smin = ~0ull;
+    sh.emax = 0;
   }
-  // records k_crc_grp would take (the fallback's choice: k_seg_stream prologue)
+  const uint64_t step = (uint64_t)nwg * blockDim.x;
+  // records k_crc_grp would take (the fallback's choice: k_seg_stream prologue),
+  // and the key range of the sort (k_seg_stream's seg_sort)
   uint32_t conf = 0;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+  uint64_t smin = ~0ull, emax = 0;
+  for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < n; j += step) {
     const uint32_t l = lens[j];
-    conf += ((((uintptr_t)base + offs[j]) & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
+    const uint64_t s = (uint64_t)base + offs[j];
+    conf += ((s & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
+    smin = s < smin ? s : smin;
+    emax = s + l > emax ? s + l : emax;
   }
   const SegGeo g = seg_geo<kU>(base, offs, lens, n);
   uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 15u : 0u;
   const uint64_t s0 = (uint64_t)base + offs[0];
   long long gx = 0;
   auto grp = [&](uint64_t p) { return (p - g.a0) >> 12; };
-  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
   // bits: 1 not packed (or a packed group of 65 events), 2 not the zeroed-gap
   // mode (out of order, overlapping, a gap over kSegMaxGap, 65 of the 2n
   // events in a group), 4 a gap over kSegSmallGap, 8 not the small-gap mode
   // (out of order, overlapping, 65 of its n + 1 events -- record ends -- in a
   // group).  A thread stops when no mode is left.
   auto none_left = [](uint32_t b) { return (b & 1u) && (b & 2u) && (b & 12u); };
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n && !none_left(bad); j += step) {
+  for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < n && !none_left(bad); j += step) {
     const uint64_t s = (uint64_t)base + offs[j], l = lens[j], e = s + l;
     if (l > kSegMaxRecord || s < g.a0 || e > g.pend) {  // k_seg_combine's unit chain stays <= 1025 units
       bad = 15u;
@@ -1760,15 +1780,35 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
       for (uint64_t u = ue + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(2 * n + 2);
   }
   __syncthreads();
-  if (bad) atomicOr(&s_bad, bad);
-  if (gx) atomicAdd(&s_gx, (unsigned long long)gx);
-  if (conf) atomicAdd(&s_conf, conf);
+  if (bad) atomicOr(&sh.bad, bad);
+  if (gx) atomicAdd(&sh.gx, (unsigned long long)gx);
+  if (conf) atomicAdd(&sh.conf, conf);
+  if (plan_min && smin != ~0ull) atomicMin(&sh.smin, (unsigned long long)smin);
+  if (plan_max && emax) atomicMax(&sh.emax, (unsigned long long)emax);
   __syncthreads();
   if (threadIdx.x == 0) {  // every slot written: no memset
-    plan_bad[blockIdx.x] = s_bad;
-    plan_gx[blockIdx.x] = (long long)s_gx;
-    plan_conf[blockIdx.x] = s_conf;
+    plan_bad[wg] = sh.bad;
+    plan_gx[wg] = (long long)sh.gx;
+    plan_conf[wg] = sh.conf;
+    if (plan_min) plan_min[wg] = sh.smin;
+    if (plan_max) plan_max[wg] = sh.emax;
   }
+}
+
+// sync (optional): the sort's two barrier words (seg_sort), zeroed here for
+// the k_seg_stream after this launch
+template <uint32_t kU = kSegUnitLg>
+__global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
+                                                  const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
+                                                  uint32_t *__restrict__ plan_bad, long long *__restrict__ plan_gx,
+                                                  uint32_t *__restrict__ plan_conf, uint32_t *__restrict__ first_ev,
+                                                  unsigned long long *__restrict__ plan_min,
+                                                  unsigned long long *__restrict__ plan_max,
+                                                  uint32_t *__restrict__ sync) {
+  __shared__ SegPlanShared sh;
+  if (sync && blockIdx.x == 0 && threadIdx.x < 2) sync[threadIdx.x] = 0;
+  seg_plan_body<kU>(base, offs, lens, n, max_units, blockIdx.x, gridDim.x, plan_bad, plan_gx, plan_conf, first_ev,
+                    plan_min, plan_max, sh);
 }
 
 // The stream over one event numbering (k_seg_plan): kGap, the 2n events of a
@@ -1777,7 +1817,7 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
 // batch (off[] only, first_ev converted).  (Its timing-only builds -- rows
 // XOR-folded, or no event work at all -- are in git history:
 // tools/ab_hc_kernels.hip, up to commit 61a2e0e.)
-template <uint32_t kMode, uint32_t kU>
+template <uint32_t kMode, uint32_t kU, bool kView = false>
 __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next, const uint32_t (&col)[32],
                                                 const uint8_t *base, const uint64_t *__restrict__ offs,
                                                 const uint32_t *__restrict__ lens, uint64_t n, uint32_t lg_chunk,
@@ -1837,7 +1877,17 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   // the first event at or after unit u's start, in this body's numbering
   auto fev = [&](uint64_t u_) -> uint64_t {
-    const uint32_t f = first_ev[u_];  // (the plan's numbering is the 2n one)
+    uint32_t f;  // (the plan's numbering is the 2n one)
+    if constexpr (kView) {
+      // the sorted view's first_ev, written earlier in this kernel (seg_sort):
+      // hipcc makes a plain read of it a vector load whose vmcnt(0) drains the
+      // row refills once a unit; a scalar load, waited for at once (lgkmcnt),
+      // leaves them in flight (glc: past the scalar cache)
+      const uint64_t pa = uni64(reinterpret_cast<uint64_t>(first_ev + u_));  // (SGPRs at every -O level)
+      asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(f) : "s"(pa));
+    } else {
+      f = first_ev[u_];
+    }
     if constexpr (kGap) return f;
     if constexpr (kEnds) return f ? (uint64_t)(f >> 1) + 1 : 0;
     return (uint64_t)((f + 1u) >> 1);
@@ -2067,6 +2117,290 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
   }
 }
 
+// ---------------------------------------------------------------------------
+// The sorted view of an unsorted batch (round 6; DESIGN.md
+// 4.2b).  Records listed out of order (config 5's records in a permuted order:
+// 66 % of 8 TB/s on k_crc_any's work, against 83 % for the same records in
+// order on the stream) are sorted by start offset inside k_seg_stream, whose
+// persistent grid (one workgroup per CU) meets at grid barriers between the
+// phases; the plan of the sorted view is made there too, and the stream then
+// runs over it.  k_seg_combine reads the sorted arrays and writes each word
+// through the permutation.  The sort is a bucket sort by 16 KiB unit (the
+// stream's own unit): count per unit (atomics), scan, scatter by arrival,
+// then each record's rank among its unit's records (a unit holds at most 256
+// records of >= 64 B; more than kSegSortMaxBucket in one unit: no sort).
+// Phases, over the workspace arrays of SegSort (its own first_ev: the batch's
+// stays unwritten in this kernel, so the unsorted stream keeps reading it with
+// scalar loads) and the stream's unit_raw (unit starts; the stream rewrites it).
+struct SegSort {
+  unsigned long long *key;  // n: keys (start - A0) in bucket order
+  uint64_t *off;            // n: the sorted view's offsets
+  uint32_t *idx;            // n: the batch index of each bucket-ordered key
+  uint32_t *arr;            // n: each record's arrival rank in its unit
+  uint32_t *len;            // n: the sorted view's lengths
+  uint32_t *perm;           // n: sorted position -> batch index
+  uint32_t *wsum, *wmax;    // kSegSortMaxWgs: per-workgroup unit-count sums / maxima
+  uint32_t *sync;           // 2 words (zeroed by k_seg_plan): the first barrier, the others' counter
+  uint32_t *fev;            // max_units + 1: the unit counts, then the sorted view's first_ev
+  uint32_t spins;           // the first barrier's bound (kSegSyncSpins; HC_SEG_SYNC_SPINS, a test hook)
+};
+constexpr uint32_t kSegSortedBit = 8;        // the mode word of a sorted view: its mode | 8
+constexpr uint32_t kSegSortMaxBucket = 1024; // most records one 16 KiB unit may start (zero-length ones)
+constexpr uint32_t kSegSortMaxWgs = 1024;    // the stream's largest grid with a sort
+constexpr uint32_t kSegSyncAbort = 1u << 31;
+
+// The first grid barrier, also the check that the whole grid is resident (a
+// grid barrier needs every workgroup on a CU at once: k_seg_stream takes one CU
+// each).  A workgroup that waits `limit` polls (kSegSyncSpinsDefault: s_sleep + an L2
+// round trip each, ~0.1-0.3 s) sets the abort bit by a
+// CAS on the counter word, which fails if the last workgroup arrived meanwhile;
+// so either every workgroup passes or every one sees the abort, and none waits
+// on a later barrier for a workgroup that left.  The later barriers need no
+// bound: every workgroup that passed the first is resident until it exits.
+__device__ __forceinline__ bool seg_sync_first(uint32_t *w, uint32_t G, uint32_t limit, uint32_t &s_ok) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t v = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    uint32_t spins = 0;
+    bool ok;
+    for (;;) {
+      if (v & kSegSyncAbort) {
+        ok = false;
+        break;
+      }
+      if (v >= G) {
+        ok = true;
+        break;
+      }
+      if (++spins > limit) {
+        uint32_t expect = v;
+        if (__hip_atomic_compare_exchange_strong(w, &expect, v | kSegSyncAbort, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          ok = false;
+          break;
+        }
+        v = expect;  // the word moved: an arrival or another workgroup's abort
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_ok = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return s_ok != 0;
+}
+__device__ __forceinline__ void seg_sync(uint32_t *ctr, uint32_t target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// Workgroup reductions / scan over blockDim.x threads (<= 1024), through 16 +
+// 16 shared words; each call ends with a barrier, so calls can follow each other.
+struct SegRed {
+  uint32_t w[kFastWaves];
+  unsigned long long q[kFastWaves];
+};
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63u) == 0) r.w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t += r.w[k];
+  __syncthreads();
+  return t;
+}
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
+  if ((threadIdx.x & 63u) == 0) r.w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t = max(t, r.w[k]);
+  __syncthreads();
+  return t;
+}
+__device__ __forceinline__ uint32_t block_or_u32(uint32_t v, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d);
+  if ((threadIdx.x & 63u) == 0) r.w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t |= r.w[k];
+  __syncthreads();
+  return t;
+}
+__device__ __forceinline__ long long block_sum_i64(long long v, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63u) == 0) r.q[threadIdx.x >> 6] = (unsigned long long)v;
+  __syncthreads();
+  long long t = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t += (long long)r.q[k];
+  __syncthreads();
+  return t;
+}
+__device__ __forceinline__ unsigned long long block_min_u64(unsigned long long v, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long o = __shfl_xor(v, d);
+    v = o < v ? o : v;
+  }
+  if ((threadIdx.x & 63u) == 0) r.q[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long t = ~0ull;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t = r.q[k] < t ? r.q[k] : t;
+  __syncthreads();
+  return t;
+}
+__device__ __forceinline__ unsigned long long block_max_u64(unsigned long long v, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long o = __shfl_xor(v, d);
+    v = o > v ? o : v;
+  }
+  if ((threadIdx.x & 63u) == 0) r.q[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t = r.q[k] > t ? r.q[k] : t;
+  __syncthreads();
+  return t;
+}
+// exclusive prefix of v over the threads in order; *total = the sum
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, SegRed &r, uint32_t &total) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(x, d);
+    if (lane >= d) x += t;
+  }
+  if (lane == 63) r.w[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) {
+    if (k < (threadIdx.x >> 6)) before += r.w[k];
+    tot += r.w[k];
+  }
+  __syncthreads();
+  total = tot;
+  return before + x - v;
+}
+
+// The sort and the plan of the sorted view (every workgroup of the grid; the
+// caller checked that the key range fits max_units units).  Returns the sorted
+// view's stream mode, or kSegFallback (the grid was not resident, a unit held
+// too many records, or the sorted records overlap / are refused by the plan):
+// uniform over the grid.
+template <uint32_t kU>
+__device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ offs,
+                             const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units, uint64_t smin,
+                             uint64_t emax, const SegSort &ss, uint32_t *__restrict__ unit_raw,
+                             uint32_t *__restrict__ plan_bad,
+                             long long *__restrict__ plan_gx, uint32_t *__restrict__ plan_conf, SegPlanShared &psh,
+                             SegRed &red, uint32_t &s_ok) {
+  const uint32_t G = gridDim.x, wg = blockIdx.x, T = blockDim.x, tid = threadIdx.x;
+  const uint64_t A0 = smin & ~1023ull;
+  const uint64_t NB = ((emax - A0) >> kU) + 1;
+  const uint64_t gstep = (uint64_t)G * T, g0 = (uint64_t)wg * T + tid;
+  uint32_t *cnt = ss.fev, *start = unit_raw;
+  // P0: zero the unit counts
+  for (uint64_t b = g0; b < NB; b += gstep) cnt[b] = 0;
+  if (!seg_sync_first(ss.sync, G, ss.spins, s_ok)) return kSegFallback;
+  uint32_t phase = 0;
+  auto sync = [&]() { seg_sync(ss.sync + 1, ++phase * G); };
+  // P1: count records per unit; each record's arrival rank in its unit
+  for (uint64_t j = g0; j < n; j += gstep) {
+    const uint64_t key = (uint64_t)base + offs[j] - A0;
+    ss.arr[j] = __hip_atomic_fetch_add(&cnt[key >> kU], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  sync();
+  // P2: exclusive scan of the counts (workgroup wg: units [wg C, wg C + C))
+  const uint64_t C = (NB + G - 1) / G, per = (C + T - 1) / T;
+  const uint64_t b0 = (uint64_t)wg * C, b1 = b0 + C < NB ? b0 + C : NB;
+  const uint64_t t0 = b0 + (uint64_t)tid * per, t1 = t0 + per < b1 ? t0 + per : b1;
+  uint32_t lsum = 0, lmax = 0;
+  for (uint64_t b = t0; b < t1; b++) {
+    const uint32_t c = cnt[b];
+    lsum += c;
+    lmax = c > lmax ? c : lmax;
+  }
+  uint32_t wtot = 0;
+  const uint32_t texcl = block_excl_scan_u32(lsum, red, wtot);
+  const uint32_t wmx = block_max_u32(lmax, red);
+  if (tid == 0) {
+    ss.wsum[wg] = wtot;
+    ss.wmax[wg] = wmx;
+  }
+  sync();
+  uint32_t pre = 0, gmx = 0;
+  for (uint32_t k = tid; k < G; k += T) {
+    if (k < wg) pre += ss.wsum[k];
+    gmx = ss.wmax[k] > gmx ? ss.wmax[k] : gmx;
+  }
+  pre = block_sum_u32(pre, red);
+  gmx = block_max_u32(gmx, red);
+  if (gmx > kSegSortMaxBucket) return kSegFallback;  // (every workgroup reads the same maxima)
+  uint32_t run = pre + texcl;
+  for (uint64_t b = t0; b < t1; b++) {
+    start[b] = run;
+    run += cnt[b];
+  }
+  sync();
+  // P3: scatter the keys by unit, in arrival order inside a unit
+  for (uint64_t j = g0; j < n; j += gstep) {
+    const uint64_t key = (uint64_t)base + offs[j] - A0;
+    const uint32_t pos = start[key >> kU] + ss.arr[j];
+    ss.key[pos] = key;
+    ss.idx[pos] = (uint32_t)j;
+  }
+  sync();
+  // P4: each record's rank among its unit's records (start offset, then batch
+  // index: zero-length records may share a start) -> the sorted arrays
+  for (uint64_t p = g0; p < n; p += gstep) {
+    const uint64_t key = ss.key[p];
+    const uint32_t j = ss.idx[p];
+    const uint64_t b = key >> kU;
+    const uint32_t s0 = start[b], c = cnt[b];
+    uint32_t rank = 0;
+    for (uint32_t q = s0; q < s0 + c; q++) {
+      const uint64_t kq = ss.key[q];
+      rank += (kq < key || (kq == key && ss.idx[q] < j)) ? 1u : 0u;
+    }
+    const uint32_t pos = s0 + rank;
+    ss.off[pos] = offs[j];
+    ss.len[pos] = lens[j];
+    ss.perm[pos] = j;
+  }
+  sync();
+  // P5: the plan of the sorted view (first_ev, the slots 0 .. G-1)
+  seg_plan_body<kU>(base, ss.off, ss.len, n, max_units, wg, G, plan_bad, plan_gx, plan_conf, ss.fev, nullptr,
+                    nullptr, psh);
+  sync();
+  // P6: its mode, as the prologue chooses one (no k_crc_grp: this batch is not all its blocks)
+  uint32_t bad = 0;
+  long long gx = 0;
+  for (uint32_t k = tid; k < G; k += T) {
+    bad |= plan_bad[k];
+    gx += plan_gx[k];
+  }
+  bad = block_or_u32(bad, red);
+  gx = block_sum_i64(gx, red);
+  return !(bad & 1u)                ? kSegPacked
+         : !(bad & 12u) && gx <= 0  ? kSegGapSmall
+         : !(bad & 2u) && gx <= 0   ? kSegGapped
+                                    : kSegFallback;
+}
+
 // The prologue reduces the plan's slots beside the table fill: packed when no
 // workgroup found the batch unpacked, else gapped when none found it out of
 // order and the gap bytes are at most a quarter of the payload, else the
@@ -2075,47 +2409,46 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint32_t lg_chunk, const uint32_t *__restrict__ plan_bad,
-                                                            const long long *__restrict__ plan_gx,
-                                                            const uint32_t *__restrict__ plan_conf, uint32_t plan_wgs,
+                                                            uint32_t lg_chunk, uint32_t *__restrict__ plan_bad,
+                                                            long long *__restrict__ plan_gx,
+                                                            uint32_t *__restrict__ plan_conf, uint32_t plan_wgs,
                                                             uint32_t allow_grp,
                                                             uint32_t *__restrict__ flag,
                                                             const uint32_t *__restrict__ first_ev,
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
-                                                            const DeviceTables *__restrict__ tables) {
+                                                            const DeviceTables *__restrict__ tables,
+                                                            uint64_t max_units,
+                                                            const unsigned long long *__restrict__ plan_min,
+                                                            const unsigned long long *__restrict__ plan_max,
+                                                            SegSort ss) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
-  __shared__ uint32_t s_next;
-  __shared__ long long s_gx[kFastWaves];
-  __shared__ uint32_t s_conf[kFastWaves];
+  __shared__ uint32_t s_next, s_ok;
+  __shared__ SegRed red;
+  __shared__ SegPlanShared psh;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
   uint32_t bad = 0, conf = 0;
   long long gx = 0;
+  uint64_t smin = ~0ull, emax = 0;
   for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) {
     bad |= plan_bad[i];
     gx += plan_gx[i];
     conf += plan_conf[i];
+    if (ss.sync) {
+      smin = plan_min[i] < smin ? plan_min[i] : smin;
+      emax = plan_max[i] > emax ? plan_max[i] : emax;
+    }
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    gx += __shfl_xor(gx, d);
-    conf += __shfl_xor(conf, d);
-  }
-  if (lane == 0) {
-    s_gx[tid >> 6] = gx;
-    s_conf[tid >> 6] = conf;
-  }
-  const int unpacked = __syncthreads_or((int)(bad & 1u));
-  const int unsorted = __syncthreads_or((int)(bad & 2u));  // (also orders the s_gx / s_conf stores)
-  const int not_small = __syncthreads_or((int)(bad & 12u));
-  long long gsum = 0;
-  uint64_t csum = 0;
-#pragma unroll
-  for (int w = 0; w < kFastWaves; w++) {
-    gsum += s_gx[w];
-    csum += s_conf[w];
-  }
+  // (reductions through LDS: readfirstlane tells hipcc the values are uniform,
+  // else every address the stream body forms from them is a VGPR -- 55 spilled)
+  const uint32_t unpacked = uni(block_or_u32(bad & 1u, red));
+  const uint32_t unsorted = uni(block_or_u32(bad & 2u, red));
+  const uint32_t not_small = uni(block_or_u32(bad & 12u, red));
+  const long long gsum = (long long)uni64((uint64_t)block_sum_i64(gx, red));
+  const uint64_t csum = uni(block_sum_u32(conf, red));
+  smin = uni64(block_min_u64(smin, red));
+  emax = uni64(block_max_u64(emax, red));
   // k_crc_grp when every record is one of its blocks (16-B aligned 4 KiB
   // multiples) in a large batch, whatever their order: ahead of the stream's
   // own modes, whose event work at 4 KiB records costs more than the hand-out
@@ -2123,12 +2456,22 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   // 3.75 vs 6.31, tools/seg_aligned_probe.py, profiles/r5/r5s/; ADVICE r4: the
   // per-record body ran 57-62 % on them).  Else the stream; else k_crc_any's
   // work in the combine.
-  const uint32_t mode = allow_grp && csum == n      ? kSegFallbackGrp
-                        : !unpacked                 ? kSegPacked
-                        : !not_small && gsum <= 0   ? kSegGapSmall
-                        : !unsorted && gsum <= 0    ? kSegGapped
-                                                    : kSegFallback;
+  uint32_t mode = allow_grp && csum == n      ? kSegFallbackGrp
+                  : !unpacked                 ? kSegPacked
+                  : !not_small && gsum <= 0   ? kSegGapSmall
+                  : !unsorted && gsum <= 0    ? kSegGapped
+                                              : kSegFallback;
   if (blockIdx.x == 0 && tid == 0) *flag = mode;  // read by k_seg_combine
+  // a batch the stream refuses, given a sort workspace (launch_seg: from
+  // sort_min records) whose key range fits the unit arrays: its sorted view
+  bool sorted = false;
+  if (mode == kSegFallback && ss.sync && smin <= emax && gridDim.x <= kSegSortMaxWgs &&
+      ((emax - (smin & ~1023ull)) >> kU) + 1 <= max_units) {
+    mode = uni(seg_sort<kU>(base, offs, lens, n, max_units, smin, emax, ss, unit_raw, plan_bad, plan_gx, plan_conf,
+                            psh, red, s_ok));
+    sorted = mode != kSegFallback;
+    if (sorted && blockIdx.x == 0 && tid == 0) *flag = mode | kSegSortedBit;
+  }
   // a fallback has no stream work: no table fill (r5: the fill was 8 of the
   // 9 us this kernel took when k_crc_grp took the batch)
   if (mode == kSegFallback || mode == kSegFallbackGrp) return;
@@ -2137,12 +2480,22 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
 #pragma unroll
   for (int i = 0; i < 32; i++) col[i] = tables->lane[lane][i];
   __syncthreads();
-  if (mode == kSegGapSmall)
-    seg_stream_body<kSegGapSmall, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
-  else if (mode == kSegGapped)
-    seg_stream_body<kSegGapped, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
-  else if (mode == kSegPacked)
-    seg_stream_body<kSegPacked, kU>(lds, s_next, col, base, offs, lens, n, lg_chunk, first_ev, unit_raw, ev_h);
+  // (two call sites, not one over a pointer chosen at run time: through the
+  // chosen pointer hipcc spilled 64 VGPRs of the stream loops)
+  auto run = [&](auto view, const uint64_t *__restrict__ o, const uint32_t *__restrict__ l,
+                 const uint32_t *__restrict__ fe) __attribute__((always_inline)) {
+    constexpr bool kV = decltype(view)::value;
+    if (mode == kSegGapSmall)
+      seg_stream_body<kSegGapSmall, kU, kV>(lds, s_next, col, base, o, l, n, lg_chunk, fe, unit_raw, ev_h);
+    else if (mode == kSegGapped)
+      seg_stream_body<kSegGapped, kU, kV>(lds, s_next, col, base, o, l, n, lg_chunk, fe, unit_raw, ev_h);
+    else if (mode == kSegPacked)
+      seg_stream_body<kSegPacked, kU, kV>(lds, s_next, col, base, o, l, n, lg_chunk, fe, unit_raw, ev_h);
+  };
+  if (sorted)
+    run(std::true_type{}, ss.off, ss.len, ss.fev);
+  else
+    run(std::false_type{}, offs, lens, first_ev);
 }
 
 __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) {
@@ -2175,13 +2528,19 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
                                                       const uint32_t *__restrict__ unit_raw,
                                                       const uint32_t *__restrict__ ev_h, uint32_t *__restrict__ crc_out,
                                                       const SegTables *__restrict__ st, uint32_t *__restrict__ taken,
-                                                      uint32_t flags, const DeviceTables *__restrict__ tables) {
+                                                      uint32_t flags, const DeviceTables *__restrict__ tables,
+                                                      const uint64_t *__restrict__ sorted_off,
+                                                      const uint32_t *__restrict__ sorted_len,
+                                                      const uint32_t *__restrict__ perm) {
   constexpr int kSub = 4, kIv0 = kSegRs * 1024;
   constexpr uint32_t kUnitRows = 1u << (kU - 10);
   __shared__ __attribute__((aligned(16))) uint32_t tl[(kSegRs + kSegIv) * 1024 + 256];
-  const uint32_t mode = *flag;
-  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks)
-    *taken = mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : mode == kSegGapSmall ? 4u : 0u;
+  const uint32_t mword = *flag;
+  const bool sorted = (mword & kSegSortedBit) != 0;  // the stream ran over the sorted view (seg_sort)
+  const uint32_t mode = mword & ~kSegSortedBit;
+  if (taken && blockIdx.x == 0 && threadIdx.x == 0)  // (hc_debug_seg_taken: 1 packed, 2 gapped, 3 / 0 fallbacks; | 8 sorted)
+    *taken = (mode == kSegPacked ? 1u : mode == kSegGapped ? 2u : mode == kSegFallbackGrp ? 3u : mode == kSegGapSmall ? 4u : 0u) |
+             (sorted ? kSegSortedBit : 0u);
   // kSegFallbackGrp: k_crc_grp, launched after this kernel and gated on the
   // mode word, takes the batch.  (Round 5 first ran k_crc_grp's body here,
   // before the sweep: the plain fallback then read gridDim.x through an SGPR
@@ -2215,7 +2574,6 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
     }
   }
   __syncthreads();
-  const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni(threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -2246,128 +2604,142 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
     }
     return inv_shift(hb ^ v, db) ^ 0xFFFFFFFFu;
   };
-  if (mode == kSegGapSmall) {
-    // record j = [s_j, e_j); the stream left H at s_0 (event 0) and at every
-    // record end e_j (event j + 1) over the span's bytes, gaps included.  H(s_j)
-    // from H(e_{j-1}): shifted by the rows between them, plus the gap bytes
-    // [p, s_j) hashed here byte by byte (<= kSegSmallGap) and shifted to s_j's
-    // row end; p = e_{j-1}, or s_j's unit start when the gap crosses into it
-    // (then H(e_{j-1}) belongs to another unit and drops out).
-    const uint32_t *sh1 = tl + (kSegRs + kSegIv) * 1024;
-    for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
-      uint64_t xa[kSub], xe[kSub];
-      uint32_t ln[kSub], he[kSub], hb[kSub];
-#pragma unroll
-      for (int p = 0; p < kSub; p++) {
-        const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1, jp = jj ? jj - 1 : 0;
-        xa[p] = (uint64_t)base + offs[jj] - geo.a0;
-        ln[p] = lens[jj];
-        xe[p] = (uint64_t)base + offs[jp] + lens[jp] - geo.a0;
-        he[p] = ev_h[jj];
-        hb[p] = ev_h[jj + 1];
-      }
-#pragma unroll
-      for (int p = 0; p < kSub; p++) {
-        const uint64_t j = c + 64u * p + lane;
-        const bool same = (xe[p] >> kU) == (xa[p] >> kU);
-        const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
-        const uint32_t L = j < n && j ? (uint32_t)(xa[p] - gp) : 0u, nw = (L + 3u) >> 2;
-        // before any lane leaves: a butterfly over a partial wave reads the
-        // stale values of the lanes that left (r5l: a record after a 38-B gap
-        // in wave 0, whose lane 0 holds record 0, lost its last words)
-        const uint32_t nwmax = wave_max_u32(nw);
-        if (j >= n) continue;
-        uint32_t ha = he[p];  // j == 0: H(s_0) itself
-        if (j) {
-          // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes, as nw words
-          // ending at s_j behind 4nw - L leading zeros (raw ignores them).  The
-          // words come from the aligned dwords D[i] at Bq + 4i, Bq = (s_j -
-          // 4nw) & ~3, bytes before gp cleared, by a funnel shift of sa = s_j & 3
-          // bytes.  Plain per-lane loads: a buffer resource is scalar, so one
-          // built from a per-lane address became a 64-pass waterfall loop per
-          // load (r5h/r5i: 233 / 369 us of combine at 2M records).  An aligned
-          // dword holding a span byte never leaves the span's pages; D[nw] is
-          // read only when it holds gap bytes (sa > 0).
-          const uint32_t sa = (uint32_t)xa[p] & 3u;
-          const uint64_t Bq = (xa[p] - 4u * nw) & ~3ull;
-          uint32_t D[kSegSmallGap / 4 + 1];
-#pragma unroll
-          for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
-            D[i] = 0;
-            if (i > nwmax) continue;
-            const uint64_t ai = Bq + 4u * i;
-            if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
-              D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
-              if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
-            }
-          }
-          uint32_t r = 0;
-#pragma unroll
-          for (uint32_t k = 0; k < kSegSmallGap / 4; k++) {
-            if (k >= nwmax) break;
-            uint32_t t = r, w = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sa);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-              t = sh1[(t ^ w) & 255u] ^ (t >> 8);
-              w >>= 8;
-            }
-            r = k < nw ? t : r;
-          }
-          const uint32_t re = (uint32_t)(xa[p] >> 10) + 1u, d = (uint32_t)(((uint64_t)re << 10) - xa[p]);
-          // shift(r, d) = shift(shift(r, 1024), -(1024 - d))
-          uint32_t pg = seg_lds_tmul(tl, r);
-          if (d < 1024u) pg = inv_shift(pg, 1024u - d);
-          ha = (same ? rsh(he[p], (uint32_t)((xa[p] >> 10) - (xe[p] >> 10))) : 0u) ^ pg;
+  // the records of the stream's view: the batch's own arrays, or (sorted) the
+  // sorted view's, record j's word going to batch entry perm[j].  Two
+  // instantiations, not one with the arrays chosen at run time (whose
+  // per-record perm select spilled VGPRs to scratch).
+  auto records = [&](auto sorted_c, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens)
+                     __attribute__((always_inline)) {
+    constexpr bool kSorted = decltype(sorted_c)::value;
+    const SegGeo geo = seg_geo<kU>(base, offs, lens, n);
+    auto put = [&](uint64_t j, uint32_t v) { crc_out[kSorted ? perm[j] : j] = v; };
+    if (mode == kSegGapSmall) {
+      // record j = [s_j, e_j); the stream left H at s_0 (event 0) and at every
+      // record end e_j (event j + 1) over the span's bytes, gaps included.  H(s_j)
+      // from H(e_{j-1}): shifted by the rows between them, plus the gap bytes
+      // [p, s_j) hashed here byte by byte (<= kSegSmallGap) and shifted to s_j's
+      // row end; p = e_{j-1}, or s_j's unit start when the gap crosses into it
+      // (then H(e_{j-1}) belongs to another unit and drops out).
+      const uint32_t *sh1 = tl + (kSegRs + kSegIv) * 1024;
+      for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
+        uint64_t xa[kSub], xe[kSub];
+        uint32_t ln[kSub], he[kSub], hb[kSub];
+  #pragma unroll
+        for (int p = 0; p < kSub; p++) {
+          const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1, jp = jj ? jj - 1 : 0;
+          xa[p] = (uint64_t)base + offs[jj] - geo.a0;
+          ln[p] = lens[jj];
+          xe[p] = (uint64_t)base + offs[jp] + lens[jp] - geo.a0;
+          he[p] = ev_h[jj];
+          hb[p] = ev_h[jj + 1];
         }
-        crc_out[j] = rec_crc(xa[p], ha, xa[p] + ln[p], hb[p]);
+  #pragma unroll
+        for (int p = 0; p < kSub; p++) {
+          const uint64_t j = c + 64u * p + lane;
+          const bool same = (xe[p] >> kU) == (xa[p] >> kU);
+          const uint64_t gp = same ? xe[p] : (xa[p] >> kU) << kU;  // first gap byte in s_j's unit
+          const uint32_t L = j < n && j ? (uint32_t)(xa[p] - gp) : 0u, nw = (L + 3u) >> 2;
+          // before any lane leaves: a butterfly over a partial wave reads the
+          // stale values of the lanes that left (r5l: a record after a 38-B gap
+          // in wave 0, whose lane 0 holds record 0, lost its last words)
+          const uint32_t nwmax = wave_max_u32(nw);
+          if (j >= n) continue;
+          uint32_t ha = he[p];  // j == 0: H(s_0) itself
+          if (j) {
+            // raw(gap bytes [gp, s_j)), L <= kSegSmallGap bytes, as nw words
+            // ending at s_j behind 4nw - L leading zeros (raw ignores them).  The
+            // words come from the aligned dwords D[i] at Bq + 4i, Bq = (s_j -
+            // 4nw) & ~3, bytes before gp cleared, by a funnel shift of sa = s_j & 3
+            // bytes.  Plain per-lane loads: a buffer resource is scalar, so one
+            // built from a per-lane address became a 64-pass waterfall loop per
+            // load (r5h/r5i: 233 / 369 us of combine at 2M records).  An aligned
+            // dword holding a span byte never leaves the span's pages; D[nw] is
+            // read only when it holds gap bytes (sa > 0).
+            const uint32_t sa = (uint32_t)xa[p] & 3u;
+            const uint64_t Bq = (xa[p] - 4u * nw) & ~3ull;
+            uint32_t D[kSegSmallGap / 4 + 1];
+  #pragma unroll
+            for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
+              D[i] = 0;
+              if (i > nwmax) continue;
+              const uint64_t ai = Bq + 4u * i;
+              if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
+                D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
+                if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
+              }
+            }
+            uint32_t r = 0;
+  #pragma unroll
+            for (uint32_t k = 0; k < kSegSmallGap / 4; k++) {
+              if (k >= nwmax) break;
+              uint32_t t = r, w = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sa);
+  #pragma unroll
+              for (int q = 0; q < 4; q++) {
+                t = sh1[(t ^ w) & 255u] ^ (t >> 8);
+                w >>= 8;
+              }
+              r = k < nw ? t : r;
+            }
+            const uint32_t re = (uint32_t)(xa[p] >> 10) + 1u, d = (uint32_t)(((uint64_t)re << 10) - xa[p]);
+            // shift(r, d) = shift(shift(r, 1024), -(1024 - d))
+            uint32_t pg = seg_lds_tmul(tl, r);
+            if (d < 1024u) pg = inv_shift(pg, 1024u - d);
+            ha = (same ? rsh(he[p], (uint32_t)((xa[p] >> 10) - (xe[p] >> 10))) : 0u) ^ pg;
+          }
+          put(j, rec_crc(xa[p], ha, xa[p] + ln[p], hb[p]));
+        }
       }
+      return;
     }
-    return;
-  }
-  if (mode == kSegGapped) {
-    // record j = [s_j, e_j), events 2j and 2j+1, one record a lane.  The
-    // stream zeroed the gap bytes and left H at e_j (2j+1) and s_0 (0): H(s_j)
-    // is H(e_{j-1}) shifted by the rows between them in one unit, else 0
-    // (k_seg_stream's kGap notes)
-    for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
-      uint64_t xa[kSub], xe[kSub];
-      uint32_t ln[kSub], he[kSub], hb[kSub];
-#pragma unroll
+    if (mode == kSegGapped) {
+      // record j = [s_j, e_j), events 2j and 2j+1, one record a lane.  The
+      // stream zeroed the gap bytes and left H at e_j (2j+1) and s_0 (0): H(s_j)
+      // is H(e_{j-1}) shifted by the rows between them in one unit, else 0
+      // (k_seg_stream's kGap notes)
+      for (uint64_t c = wv * 64u * kSub; c < n; c += nw * 64u * kSub) {
+        uint64_t xa[kSub], xe[kSub];
+        uint32_t ln[kSub], he[kSub], hb[kSub];
+  #pragma unroll
+        for (int p = 0; p < kSub; p++) {
+          const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1, jp = jj ? jj - 1 : 0;
+          xa[p] = (uint64_t)base + offs[jj] - geo.a0;
+          ln[p] = lens[jj];
+          xe[p] = (uint64_t)base + offs[jp] + lens[jp] - geo.a0;
+          he[p] = ev_h[jj ? 2 * jj - 1 : 0];
+          hb[p] = ev_h[2 * jj + 1];
+        }
+  #pragma unroll
+        for (int p = 0; p < kSub; p++) {
+          const uint64_t j = c + 64u * p + lane;
+          uint32_t ha = he[p];  // j == 0: H(s_0) itself
+          if (j) ha = (xe[p] >> kU) == (xa[p] >> kU) ? rsh(he[p], (uint32_t)((xa[p] >> 10) - (xe[p] >> 10))) : 0u;
+          if (j < n) put(j, rec_crc(xa[p], ha, xa[p] + ln[p], hb[p]));
+        }
+      }
+      return;
+    }
+    for (uint64_t c = wv * 63u * kSub; c < n; c += nw * 63u * kSub) {
+      uint64_t x[kSub];
+      uint32_t eh[kSub];
+  #pragma unroll
+      for (int p = 0; p < kSub; p++) {  // event c + 63p + lane (past n: the span's end again)
+        const uint64_t j = c + 63u * p + lane, jj = j < n ? j : n;
+        x[p] = (jj < n ? (uint64_t)base + offs[jj] : geo.pend) - geo.a0;
+        eh[p] = ev_h[jj];
+      }
+  #pragma unroll
       for (int p = 0; p < kSub; p++) {
-        const uint64_t j = c + 64u * p + lane, jj = j < n ? j : n - 1, jp = jj ? jj - 1 : 0;
-        xa[p] = (uint64_t)base + offs[jj] - geo.a0;
-        ln[p] = lens[jj];
-        xe[p] = (uint64_t)base + offs[jp] + lens[jp] - geo.a0;
-        he[p] = ev_h[jj ? 2 * jj - 1 : 0];
-        hb[p] = ev_h[2 * jj + 1];
-      }
-#pragma unroll
-      for (int p = 0; p < kSub; p++) {
-        const uint64_t j = c + 64u * p + lane;
-        uint32_t ha = he[p];  // j == 0: H(s_0) itself
-        if (j) ha = (xe[p] >> kU) == (xa[p] >> kU) ? rsh(he[p], (uint32_t)((xa[p] >> 10) - (xe[p] >> 10))) : 0u;
-        if (j < n) crc_out[j] = rec_crc(xa[p], ha, xa[p] + ln[p], hb[p]);
+        const uint64_t j = c + 63u * p + lane;
+        const uint32_t kb = __shfl_down(eh[p], 1);
+        const uint64_t xb = __shfl_down((unsigned long long)x[p], 1);
+        if (lane < 63 && j < n) put(j, rec_crc(x[p], eh[p], xb, kb));
       }
     }
-    return;
-  }
-  for (uint64_t c = wv * 63u * kSub; c < n; c += nw * 63u * kSub) {
-    uint64_t x[kSub];
-    uint32_t eh[kSub];
-#pragma unroll
-    for (int p = 0; p < kSub; p++) {  // event c + 63p + lane (past n: the span's end again)
-      const uint64_t j = c + 63u * p + lane, jj = j < n ? j : n;
-      x[p] = (jj < n ? (uint64_t)base + offs[jj] : geo.pend) - geo.a0;
-      eh[p] = ev_h[jj];
-    }
-#pragma unroll
-    for (int p = 0; p < kSub; p++) {
-      const uint64_t j = c + 63u * p + lane;
-      const uint32_t kb = __shfl_down(eh[p], 1);
-      const uint64_t xb = __shfl_down((unsigned long long)x[p], 1);
-      if (lane < 63 && j < n) crc_out[j] = rec_crc(x[p], eh[p], xb, kb);
-    }
-  }
+  };
+  if (sorted)
+    records(std::true_type{}, sorted_off, sorted_len);
+  else
+    records(std::false_type{}, offs, lens);
 }
 
 // A uniform block batch k_crc_grp refuses, on the message stream
@@ -2546,48 +2918,94 @@ hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, 
 
 uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
 
-// workspace (u32 words): the mode flag (64 words), plan_bad[kSegPlanMaxWgs],
-// plan_gx[kSegPlanMaxWgs] (int64), plan_conf[kSegPlanMaxWgs],
-// first_ev[max_units + 1], unit_raw[max_units],
-// ev_h[2n + 1] (the gapped numbering's 2n events; a packed batch uses n + 1)
-uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units) {
-  return 4 * (64 + kSegPlanMaxWgs) + 8 * kSegPlanMaxWgs + 4 * kSegPlanMaxWgs +
-         4 * ((max_units + 1) + max_units + 2 * n + 1);
+// workspace (u32 words): the mode flag (64 words: word 0 the mode, words 1-2
+// the sort's barrier words), plan_bad[kSegPlanMaxWgs], plan_gx[kSegPlanMaxWgs]
+// (int64), plan_conf[kSegPlanMaxWgs], first_ev[max_units + 1],
+// unit_raw[max_units], ev_h[2n + 1] (the gapped numbering's 2n events; a
+// packed batch uses n + 1); 8-B aligned after it plan_min / plan_max
+// [kSegPlanMaxWgs] (u64) and, with a sort, SegSort's arrays.
+namespace {
+struct SegWs {
+  uint32_t *flag, *plan_bad, *plan_conf, *first_ev, *unit_raw, *ev_h;
+  long long *plan_gx;
+  unsigned long long *plan_min, *plan_max;
+  SegSort ss;
+  uint64_t bytes;
+};
+SegWs seg_ws_layout(uint32_t *ws, uint64_t n, uint64_t max_units, bool sort) {
+  SegWs w{};
+  uint64_t o = 0;  // bytes
+  auto take = [&](uint64_t bytes, uint64_t align) {
+    o = (o + align - 1) & ~(align - 1);
+    uint8_t *p = ws ? reinterpret_cast<uint8_t *>(ws) + o : nullptr;
+    o += bytes;
+    return p;
+  };
+  w.flag = reinterpret_cast<uint32_t *>(take(4 * 64, 4));
+  w.plan_bad = reinterpret_cast<uint32_t *>(take(4ull * kSegPlanMaxWgs, 4));
+  w.plan_gx = reinterpret_cast<long long *>(take(8ull * kSegPlanMaxWgs, 8));
+  w.plan_conf = reinterpret_cast<uint32_t *>(take(4ull * kSegPlanMaxWgs, 4));
+  w.first_ev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
+  w.unit_raw = reinterpret_cast<uint32_t *>(take(4 * max_units, 4));
+  w.ev_h = reinterpret_cast<uint32_t *>(take(4 * (2 * n + 1), 4));
+  w.plan_min = reinterpret_cast<unsigned long long *>(take(8ull * kSegPlanMaxWgs, 8));
+  w.plan_max = reinterpret_cast<unsigned long long *>(take(8ull * kSegPlanMaxWgs, 8));
+  if (sort) {
+    w.ss.key = reinterpret_cast<unsigned long long *>(take(8 * n, 8));
+    w.ss.off = reinterpret_cast<uint64_t *>(take(8 * n, 8));
+    w.ss.idx = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.arr = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.len = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.perm = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.wsum = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
+    w.ss.wmax = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
+    w.ss.fev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
+    w.ss.sync = w.flag + 1;
+  }
+  w.bytes = (o + 7) & ~7ull;
+  return w;
+}
+}  // namespace
+
+uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units, bool sort) {
+  return seg_ws_layout(nullptr, n, max_units, sort).bytes;
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken, uint64_t grp_min, uint32_t lg_chunk) {
+                      uint32_t *taken, uint64_t grp_min, uint64_t sort_min, uint32_t sync_spins, uint32_t lg_chunk) {
   if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
     return hipErrorInvalidValue;
   const uint64_t n = b.nblocks;
-  uint32_t *flag = ws, *plan_bad = ws + 64;
-  long long *plan_gx = reinterpret_cast<long long *>(plan_bad + kSegPlanMaxWgs);  // (8-B aligned: 64 + 16384 words)
-  uint32_t *plan_conf = reinterpret_cast<uint32_t *>(plan_gx + kSegPlanMaxWgs), *first_ev = plan_conf + kSegPlanMaxWgs,
-           *unit_raw = first_ev + max_units + 1, *ev_h = unit_raw + max_units;
+  // the sorted view (seg_sort): from sort_min records, on a grid it can meet at barriers
+  const bool sort = sort_min && n >= sort_min && grid <= (int)kSegSortMaxWgs;
+  SegWs w = seg_ws_layout(ws, n, max_units, sort);
+  w.ss.spins = sync_spins;
   const uint64_t pg = (n + 256) / 256;
   // HC_SEG_PLAN_WGS overrides the plan's grid cap, up to kSegPlanMaxWgs (tuning sweeps)
   static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanWgs)));
   const uint32_t plan_wgs = (uint32_t)(pg < cap ? pg : cap);
   // every launch checked: a later kernel must not run on a failed one's stale
   // outputs (hipGetLastError reports the latest call, not the first failure)
-  hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, plan_bad,
-                     plan_gx, plan_conf, first_ev);
+  hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, w.plan_bad,
+                     w.plan_gx, w.plan_conf, w.first_ev, sort ? w.plan_min : nullptr, sort ? w.plan_max : nullptr,
+                     w.ss.sync);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // a batch large enough that a gated launch (exiting on its first load unless
   // the stream chose kSegFallbackGrp: 5 us under rocprofv3, r5e) is small against it
   // (grp_min: HC_SEG_GRP_MIN, default kSegGrpFallbackMin)
   const uint32_t allow_grp = n >= grp_min ? 1u : 0u;
-  hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk, plan_bad,
-                     plan_gx, plan_conf, plan_wgs, allow_grp, flag, first_ev, unit_raw, ev_h, b.tables);
+  hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
+                     w.plan_bad, w.plan_gx, w.plan_conf, plan_wgs, allow_grp, w.flag, w.first_ev, w.unit_raw, w.ev_h,
+                     b.tables, max_units, w.plan_min, w.plan_max, w.ss);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, flag, unit_raw, ev_h,
-                     b.crc_out, st, taken, b.flags, b.tables);
+  hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, w.flag, w.unit_raw,
+                     w.ev_h, b.crc_out, st, taken, b.flags, b.tables, w.ss.off, w.ss.len, w.ss.perm);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (allow_grp)
     hipLaunchKernelGGL((k_crc_grp<true>), dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, b.stride, b.ulen,
                        b.flags, n, grp_lg_chunk(n, grid, 0), b.crc_out, nullptr, nullptr, b.tables, nullptr, 0,
-                       flag);
+                       w.flag);
   return hipGetLastError();
 }
 

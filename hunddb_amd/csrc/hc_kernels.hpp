@@ -111,12 +111,23 @@ hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 // k_seg_combine runs k_crc_any's work over it in the same launch; from grp_min
 // records on, a batch of aligned 4 KiB-multiple records goes to k_crc_grp in
 // any layout, launched after the combine, which exits at once unless ws[0] says so.
+// An unsorted batch of at least sort_min records (round 6) is
+// sorted by record offset inside k_seg_stream (grid barriers; its workspace is
+// the sort part of seg_workspace_bytes(n, max_units, true)) and streamed in
+// that order; k_seg_combine writes each word through the permutation.
+// sort_min 0: never (the workspace may then be seg_workspace_bytes(n, mu)).
 uint64_t seg_max_units(uint64_t span_bound);
-uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units);
+uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units, bool sort = false);
 constexpr uint64_t kSegGrpFallbackMin = 1ull << 18;  // grp_min's default (HC_SEG_GRP_MIN)
-// taken (optional, device word): 1 packed, 2 gapped, 3 k_crc_grp fallback, 0 k_crc_any fallback.
+constexpr uint64_t kSegSortMin = 1ull << 14;         // sort_min's default (HC_SEG_SORT_MIN)
+// taken (optional, device word): 1 packed, 2 gapped, 3 k_crc_grp fallback,
+// 4 small gaps, 0 k_crc_any fallback; | 8 when the stream ran on the sorted view.
+// sync_spins bounds the sort's first grid barrier, the check that the grid is
+// resident (polls; a grid that is not: no sort, k_crc_any's work).
+constexpr uint32_t kSegSyncSpinsDefault = 1u << 17;
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken = nullptr, uint64_t grp_min = kSegGrpFallbackMin, uint32_t lg_chunk = 7);
+                      uint32_t *taken = nullptr, uint64_t grp_min = kSegGrpFallbackMin, uint64_t sort_min = 0,
+                      uint32_t sync_spins = kSegSyncSpinsDefault, uint32_t lg_chunk = 7);
 // A uniform block batch (no off/len arrays) that k_crc_grp refuses (lengths not
 // a 4 KiB multiple, or not 16-B aligned), ulen >= 4, stride >= ulen: its
 // messages block[4:ulen] written out as off/len arrays, launch_seg over them

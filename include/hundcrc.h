@@ -339,15 +339,18 @@ int hc_debug_tables(void *out, size_t cap);
  * the same stream as sorted records with gaps of at most 64 B between them, 2
  * as sorted records with wider gaps (zeroed in the stream), 3 by k_crc_grp
  * (the stream's fallback for aligned 4 KiB-multiple records out of order), 0
- * by k_crc_any on the device or not offered to the stream; synchronizes that
- * device (tests and tools only). */
+ * by k_crc_any on the device or not offered to the stream; plus 8 when the
+ * records were listed out of order and the stream ran over their sorted view
+ * (from HC_SEG_SORT_MIN records); synchronizes that device
+ * (tests and tools only). */
 int hc_debug_seg_taken(void);
 
 /* The library reads its HC_* settings from the environment once, at the first
  * call that needs one (a getenv racing with a Go os.Setenv would be a data
  * race): HC_DEVICE, HC_SEG_MIN_MSGS, HC_COPY_THREADS, HC_WAL_MIN_RANGE,
  * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
- * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN, HC_SEG_MIN_BLOCKS.  hc_debug_set changes one of them afterwards
+ * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN, HC_SEG_MIN_BLOCKS, HC_SEG_SORT_MIN,
+ * HC_SEG_SYNC_SPINS.  hc_debug_set changes one of them afterwards
  * (tests and tools); value NULL restores the compiled default.  HC_OK, or
  * HC_E_ARG for an unknown name.
  * HC_INJECT_FAIL (test hook) accepts "add_crcs", "read_from_disk" or

@@ -4,7 +4,8 @@ wave gets one.  Batch sizes around every window size, in block mode (off/len
 blocks k_crc_grp leaves to the sweep: 1 KiB and misaligned 4 KiB blocks, with
 a corrupt block found by verify) and whole-message mode with gaps, out of
 order (the stream takes sorted gapped records since round 5; unsorted ones go
-to k_crc_any on the device flag), every word against the oracle
+to k_crc_any on the device flag, or from 2^14 records to the stream over their
+sorted view since round 6), every word against the oracle
 (crc_util.go:15-17 / :88-100 per block)."""
 import numpy as np
 import pytest
@@ -73,7 +74,13 @@ def test_gapped_messages_all_window_sizes(cuda, hc, oracle, n):
     out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
     hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=n, flags=hc.HC_F_MESSAGES)
     torch.cuda.synchronize()
-    assert hc.seg_taken() == (n == 1)  # one record is packed: the stream takes it
+    # one record is packed: the stream takes it; from HC_SEG_SORT_MIN records the
+    # permuted batch is sorted and the stream takes the sorted view (round 6)
+    if n >= 1 << 14:
+        from test_gpu_seg_sort import sorted_path
+        assert hc.seg_path() == sorted_path(buf.data_ptr(), off, lens)
+    else:
+        assert hc.seg_taken() == (n == 1)
     want = oracle.crc32_messages(host, off, lens, threads=16)
     got = u32(out)
     bad = np.flatnonzero(got != want)
