@@ -141,6 +141,7 @@ def _lib():
             "hc_last_launch": (I, [ctypes.POINTER(LaunchInfo)]),
             "hc_debug_tables": (I, [P, S]),
             "hc_debug_seg_taken": (I, []),
+            "hc_debug_seg_prof": (I, [P]),
             "hc_debug_set": (I, [ctypes.c_char_p, ctypes.c_char_p]),
             "hc_device_count": (I, []),
             "hc_host_pipelines": (I, []),
@@ -664,6 +665,16 @@ def seg_path():
         raise HundCRCError(r, "seg_taken")
     return {1: "packed", 2: "gapped_wide", 3: "fallback_grp", 4: "gapped",
             9: "sorted_packed", 10: "sorted_gapped_wide", 12: "sorted_gapped"}.get(r, "fallback")
+
+
+def seg_prof():
+    """The stream kernel's phase clock for this thread's last stream batch, in
+    microseconds from its start (hc_debug_seg_prof; tools only)."""
+    buf = np.zeros(16, dtype=np.uint64)
+    r = int(_lib().hc_debug_seg_prof(buf.ctypes.data))
+    if r != 0:
+        raise HundCRCError(r, "seg_prof")
+    return [(int(x) - int(buf[0])) / 100.0 for x in buf]
 
 
 def seg_mode():

@@ -2137,6 +2137,7 @@ struct SegSort {
   uint64_t *off;            // n: the sorted view's offsets
   uint32_t *idx;            // n: the batch index of each bucket-ordered key
   uint32_t *arr;            // n: each record's arrival rank in its unit
+  uint32_t *ltmp;           // n: the lengths, in bucket order
   uint32_t *len;            // n: the sorted view's lengths
   uint32_t *perm;           // n: sorted position -> batch index
   uint32_t *wsum, *wmax;    // kSegSortMaxWgs: per-workgroup unit-count sums / maxima
@@ -2145,6 +2146,13 @@ struct SegSort {
   uint32_t spins;           // the first barrier's bound (kSegSyncSpins; HC_SEG_SYNC_SPINS, a test hook)
 };
 constexpr uint32_t kSegSortedBit = 8;        // the mode word of a sorted view: its mode | 8
+// Phase clock of the last sort (hc_debug_seg_prof): workgroup 0's s_memrealtime
+// (100 MHz) at the stream's start and after each sort phase, then when its
+// stream body ends.  One store per phase by one thread.
+__device__ unsigned long long g_seg_prof[16];
+__device__ __forceinline__ void seg_prof(uint32_t k) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && k < 16) g_seg_prof[k] = __builtin_amdgcn_s_memrealtime();
+}
 constexpr uint32_t kSegSortMaxBucket = 1024; // most records one 16 KiB unit may start (zero-length ones)
 constexpr uint32_t kSegSortMaxWgs = 1024;    // the stream's largest grid with a sort
 constexpr uint32_t kSegSyncAbort = 1u << 31;
@@ -2157,10 +2165,15 @@ constexpr uint32_t kSegSyncAbort = 1u << 31;
 // so either every workgroup passes or every one sees the abort, and none waits
 // on a later barrier for a workgroup that left.  The later barriers need no
 // bound: every workgroup that passed the first is resident until it exits.
+// Fences: the workgroup barrier leaves every wave's stores acknowledged by the
+// XCD's L2; ONE agent-scope release (thread 0) then writes that L2 back, and
+// one acquire invalidates the CU's L1 and the L2 before the second barrier
+// releases the waves.  (The first build fenced in every thread: 16 L2
+// writebacks per workgroup per barrier.)
 __device__ __forceinline__ bool seg_sync_first(uint32_t *w, uint32_t G, uint32_t limit, uint32_t &s_ok) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     uint32_t v = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     uint32_t spins = 0;
     bool ok;
@@ -2187,20 +2200,20 @@ __device__ __forceinline__ bool seg_sync_first(uint32_t *w, uint32_t G, uint32_t
       v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     s_ok = ok ? 1u : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return s_ok != 0;
 }
 __device__ __forceinline__ void seg_sync(uint32_t *ctr, uint32_t target) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // Workgroup reductions / scan over blockDim.x threads (<= 1024), through 16 +
@@ -2317,7 +2330,11 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
   for (uint64_t b = g0; b < NB; b += gstep) cnt[b] = 0;
   if (!seg_sync_first(ss.sync, G, ss.spins, s_ok)) return kSegFallback;
   uint32_t phase = 0;
-  auto sync = [&]() { seg_sync(ss.sync + 1, ++phase * G); };
+  auto sync = [&]() {
+    seg_sync(ss.sync + 1, ++phase * G);
+    seg_prof(2 + phase);  // 3: P1 done .. 7: P5 done
+  };
+  seg_prof(2);  // P0 + the residency check
   // P1: count records per unit; each record's arrival rank in its unit
   for (uint64_t j = g0; j < n; j += gstep) {
     const uint64_t key = (uint64_t)base + offs[j] - A0;
@@ -2356,16 +2373,20 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
     run += cnt[b];
   }
   sync();
-  // P3: scatter the keys by unit, in arrival order inside a unit
+  // P3: scatter the keys (and lengths) by unit, in arrival order inside a
+  // unit: the batch arrays read in order, the writes land in its unit's range
   for (uint64_t j = g0; j < n; j += gstep) {
     const uint64_t key = (uint64_t)base + offs[j] - A0;
     const uint32_t pos = start[key >> kU] + ss.arr[j];
     ss.key[pos] = key;
     ss.idx[pos] = (uint32_t)j;
+    ss.ltmp[pos] = lens[j];
   }
   sync();
   // P4: each record's rank among its unit's records (start offset, then batch
-  // index: zero-length records may share a start) -> the sorted arrays
+  // index: zero-length records may share a start) -> the sorted arrays; every
+  // read and write near p (the offset is the key's: no gather from the batch)
+  const uint64_t off0 = A0 - (uint64_t)base;
   for (uint64_t p = g0; p < n; p += gstep) {
     const uint64_t key = ss.key[p];
     const uint32_t j = ss.idx[p];
@@ -2377,8 +2398,8 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
       rank += (kq < key || (kq == key && ss.idx[q] < j)) ? 1u : 0u;
     }
     const uint32_t pos = s0 + rank;
-    ss.off[pos] = offs[j];
-    ss.len[pos] = lens[j];
+    ss.off[pos] = key + off0;
+    ss.len[pos] = ss.ltmp[p];
     ss.perm[pos] = j;
   }
   sync();
@@ -2387,6 +2408,7 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
                     nullptr, psh);
   sync();
   // P6: its mode, as the prologue chooses one (no k_crc_grp: this batch is not all its blocks)
+  seg_prof(8);
   uint32_t bad = 0;
   long long gx = 0;
   for (uint32_t k = tid; k < G; k += T) {
@@ -2428,6 +2450,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   if (tid == 0) s_next = 2 * kFastWaves;  // indices 0 .. 2W-1 are dealt statically below
+  seg_prof(0);
   uint32_t bad = 0, conf = 0;
   long long gx = 0;
   uint64_t smin = ~0ull, emax = 0;
@@ -2465,6 +2488,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   // a batch the stream refuses, given a sort workspace (launch_seg: from
   // sort_min records) whose key range fits the unit arrays: its sorted view
   bool sorted = false;
+  seg_prof(1);  // the prologue's reductions done
   if (mode == kSegFallback && ss.sync && smin <= emax && gridDim.x <= kSegSortMaxWgs &&
       ((emax - (smin & ~1023ull)) >> kU) + 1 <= max_units) {
     mode = uni(seg_sort<kU>(base, offs, lens, n, max_units, smin, emax, ss, unit_raw, plan_bad, plan_gx, plan_conf,
@@ -2492,10 +2516,13 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
     else if (mode == kSegPacked)
       seg_stream_body<kSegPacked, kU, kV>(lds, s_next, col, base, o, l, n, lg_chunk, fe, unit_raw, ev_h);
   };
-  if (sorted)
+  if (sorted) {
+    seg_prof(9);
     run(std::true_type{}, ss.off, ss.len, ss.fev);
-  else
+    seg_prof(10);
+  } else {
     run(std::false_type{}, offs, lens, first_ev);
+  }
 }
 
 __device__ __forceinline__ uint32_t seg_lds_tmul(const uint32_t *t, uint32_t v) {
@@ -2955,6 +2982,7 @@ SegWs seg_ws_layout(uint32_t *ws, uint64_t n, uint64_t max_units, bool sort) {
     w.ss.off = reinterpret_cast<uint64_t *>(take(8 * n, 8));
     w.ss.idx = reinterpret_cast<uint32_t *>(take(4 * n, 4));
     w.ss.arr = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.ltmp = reinterpret_cast<uint32_t *>(take(4 * n, 4));
     w.ss.len = reinterpret_cast<uint32_t *>(take(4 * n, 4));
     w.ss.perm = reinterpret_cast<uint32_t *>(take(4 * n, 4));
     w.ss.wsum = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
@@ -2966,6 +2994,10 @@ SegWs seg_ws_layout(uint32_t *ws, uint64_t n, uint64_t max_units, bool sort) {
   return w;
 }
 }  // namespace
+
+hipError_t seg_prof_read(uint64_t *out16) {
+  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_seg_prof), sizeof(g_seg_prof), 0, hipMemcpyDeviceToHost);
+}
 
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units, bool sort) {
   return seg_ws_layout(nullptr, n, max_units, sort).bytes;

@@ -135,6 +135,8 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
 // blocks' verify / stamp outputs from the message CRCs.  ws holds
 // seg_block_workspace_bytes(n, max_units, !b.crc_out) bytes.
 uint64_t seg_block_workspace_bytes(uint64_t n, uint64_t max_units, bool crc_words);
+// the sort's phase clock (hc_debug_seg_prof): 16 s_memrealtime stamps (100 MHz) of workgroup 0
+hipError_t seg_prof_read(uint64_t *out16);
 hipError_t launch_seg_blocks(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid,
                              hipStream_t s, uint32_t *taken = nullptr);
 hipError_t launch_verify_prepare(uint32_t *bitmap, unsigned long long *first_bad, uint64_t n,
