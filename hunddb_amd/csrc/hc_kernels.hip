@@ -1663,6 +1663,7 @@ constexpr uint64_t kSegMaxGap = 1u << 22;     // longest gap between two records
 constexpr uint64_t kSegSmallGap = 64;         // longest gap k_seg_combine hashes itself (kSegGapSmall)
 constexpr uint32_t kSegPlanMaxWgs = 16384;   // k_seg_plan's largest grid: one "bad" slot per workgroup
 constexpr uint32_t kSegPlanWgs = 2048;       // its default grid cap (grid-stride beyond; r4e: 13.5 vs 16.8 us at 2M events)
+constexpr uint32_t kSegSyncGroups = 16;      // the sort's barrier tree: group counters (seg_sync)
 
 struct SegGeo {
   uint64_t a0, pend, units;
@@ -1697,40 +1698,29 @@ __device__ __forceinline__ SegGeo seg_geo(const uint8_t *base, const uint64_t *o
 // the dispatch needs no memset: k_seg_stream's workgroups reduce the slots and
 // its workgroup 0 stores the mode the combine reads.
 // The plan of one batch over workgroup wg of nwg (blockDim.x threads each),
-// with the workgroup's shared words s_*: k_seg_plan's body, and the plan of
-// the sorted view inside k_seg_stream (seg_sort).  plan_min / plan_max
-// (optional): the lowest record start and highest record end of the
-// workgroup's records (the sort's key range).
+// with the workgroup's shared words: k_seg_plan's body, and the plan of the
+// sorted view inside k_seg_stream (seg_sort).
 struct SegPlanShared {
   uint32_t bad, conf;
-  unsigned long long gx, smin, emax;
+  unsigned long long gx;
 };
 template <uint32_t kU>
 __device__ __forceinline__ void seg_plan_body(const uint8_t *base, const uint64_t *__restrict__ offs,
                                               const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
                                               uint32_t wg, uint32_t nwg, uint32_t *__restrict__ plan_bad,
                                               long long *__restrict__ plan_gx, uint32_t *__restrict__ plan_conf,
-                                              uint32_t *__restrict__ first_ev,
-                                              unsigned long long *__restrict__ plan_min,
-                                              unsigned long long *__restrict__ plan_max, SegPlanShared &sh) {
+                                              uint32_t *__restrict__ first_ev, SegPlanShared &sh) {
   if (threadIdx.x == 0) {
     sh.bad = 0;
     sh.conf = 0;
     sh.gx = 0;
-    sh.smin = ~0ull;
-    sh.emax = 0;
   }
   const uint64_t step = (uint64_t)nwg * blockDim.x;
-  // records k_crc_grp would take (the fallback's choice: k_seg_stream prologue),
-  // and the key range of the sort (k_seg_stream's seg_sort)
+  // records k_crc_grp would take (the fallback's choice: k_seg_stream prologue)
   uint32_t conf = 0;
-  uint64_t smin = ~0ull, emax = 0;
   for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < n; j += step) {
     const uint32_t l = lens[j];
-    const uint64_t s = (uint64_t)base + offs[j];
-    conf += ((s & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
-    smin = s < smin ? s : smin;
-    emax = s + l > emax ? s + l : emax;
+    conf += ((((uintptr_t)base + offs[j]) & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
   }
   const SegGeo g = seg_geo<kU>(base, offs, lens, n);
   uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 15u : 0u;
@@ -1783,32 +1773,25 @@ __device__ __forceinline__ void seg_plan_body(const uint8_t *base, const uint64_
   if (bad) atomicOr(&sh.bad, bad);
   if (gx) atomicAdd(&sh.gx, (unsigned long long)gx);
   if (conf) atomicAdd(&sh.conf, conf);
-  if (plan_min && smin != ~0ull) atomicMin(&sh.smin, (unsigned long long)smin);
-  if (plan_max && emax) atomicMax(&sh.emax, (unsigned long long)emax);
   __syncthreads();
   if (threadIdx.x == 0) {  // every slot written: no memset
     plan_bad[wg] = sh.bad;
     plan_gx[wg] = (long long)sh.gx;
     plan_conf[wg] = sh.conf;
-    if (plan_min) plan_min[wg] = sh.smin;
-    if (plan_max) plan_max[wg] = sh.emax;
   }
 }
 
-// sync (optional): the sort's two barrier words (seg_sort), zeroed here for
-// the k_seg_stream after this launch
+// sync (optional): the sort's barrier words (seg_sort), zeroed here for the
+// k_seg_stream after this launch
 template <uint32_t kU = kSegUnitLg>
 __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uint64_t *__restrict__ offs,
                                                   const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units,
                                                   uint32_t *__restrict__ plan_bad, long long *__restrict__ plan_gx,
                                                   uint32_t *__restrict__ plan_conf, uint32_t *__restrict__ first_ev,
-                                                  unsigned long long *__restrict__ plan_min,
-                                                  unsigned long long *__restrict__ plan_max,
                                                   uint32_t *__restrict__ sync) {
   __shared__ SegPlanShared sh;
-  if (sync && blockIdx.x == 0 && threadIdx.x < 2) sync[threadIdx.x] = 0;
-  seg_plan_body<kU>(base, offs, lens, n, max_units, blockIdx.x, gridDim.x, plan_bad, plan_gx, plan_conf, first_ev,
-                    plan_min, plan_max, sh);
+  if (sync && blockIdx.x == 0 && threadIdx.x < 2 + kSegSyncGroups) sync[threadIdx.x] = 0;
+  seg_plan_body<kU>(base, offs, lens, n, max_units, blockIdx.x, gridDim.x, plan_bad, plan_gx, plan_conf, first_ev, sh);
 }
 
 // The stream over one event numbering (k_seg_plan): kGap, the 2n events of a
@@ -2133,22 +2116,23 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
 // stays unwritten in this kernel, so the unsorted stream keeps reading it with
 // scalar loads) and the stream's unit_raw (unit starts; the stream rewrites it).
 struct SegSort {
-  unsigned long long *key;  // n: keys (start - A0) in bucket order
+  uint4 *rec;               // n: (key = start - A0, batch index, length) in bucket order, one 16-B store
   uint64_t *off;            // n: the sorted view's offsets
-  uint32_t *idx;            // n: the batch index of each bucket-ordered key
   uint32_t *arr;            // n: each record's arrival rank in its unit
-  uint32_t *ltmp;           // n: the lengths, in bucket order
   uint32_t *len;            // n: the sorted view's lengths
   uint32_t *perm;           // n: sorted position -> batch index
   uint32_t *wsum, *wmax;    // kSegSortMaxWgs: per-workgroup unit-count sums / maxima
-  uint32_t *sync;           // 2 words (zeroed by k_seg_plan): the first barrier, the others' counter
+  unsigned long long *wlo, *whi;  // kSegSortMaxWgs: per-workgroup lowest start / highest end
+  uint32_t *sync;           // 18 words (zeroed by k_seg_plan): the first barrier, the others' root and 16 group counters
   uint32_t *fev;            // max_units + 1: the unit counts, then the sorted view's first_ev
   uint32_t spins;           // the first barrier's bound (kSegSyncSpins; HC_SEG_SYNC_SPINS, a test hook)
 };
 constexpr uint32_t kSegSortedBit = 8;        // the mode word of a sorted view: its mode | 8
 // Phase clock of the last sort (hc_debug_seg_prof): workgroup 0's s_memrealtime
-// (100 MHz) at the stream's start and after each sort phase, then when its
-// stream body ends.  One store per phase by one thread.
+// (100 MHz): [0] the stream's start, [1] its prologue, [2] the key range and
+// the residency check, [3..9] the sort's barriers (P0, P1, P2 twice, P3, P4,
+// P5), [10] P6, [14] / [15] the sorted body's start / end.  One store each by
+// one thread.
 __device__ unsigned long long g_seg_prof[16];
 __device__ __forceinline__ void seg_prof(uint32_t k) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && k < 16) g_seg_prof[k] = __builtin_amdgcn_s_memrealtime();
@@ -2156,6 +2140,51 @@ __device__ __forceinline__ void seg_prof(uint32_t k) {
 constexpr uint32_t kSegSortMaxBucket = 1024; // most records one 16 KiB unit may start (zero-length ones)
 constexpr uint32_t kSegSortMaxWgs = 1024;    // the stream's largest grid with a sort
 constexpr uint32_t kSegSyncAbort = 1u << 31;
+
+// workspace (u32 words): the mode flag (64 words: word 0 the mode, words 1-18
+// the sort's barrier words), plan_bad[kSegPlanMaxWgs], plan_gx[kSegPlanMaxWgs]
+// (int64), plan_conf[kSegPlanMaxWgs], first_ev[max_units + 1],
+// unit_raw[max_units], ev_h[2n + 1] (the gapped numbering's 2n events; a
+// packed batch uses n + 1); with a sort, SegSort's arrays after it.
+struct SegWs {
+  uint32_t *flag, *plan_bad, *plan_conf, *first_ev, *unit_raw, *ev_h;
+  long long *plan_gx;
+  SegSort ss;
+  uint64_t bytes;
+};
+__host__ __device__ __forceinline__ SegWs seg_ws_layout(uint32_t *ws, uint64_t n, uint64_t max_units, bool sort) {
+  SegWs w{};
+  uint64_t o = 0;  // bytes
+  auto take = [&](uint64_t bytes, uint64_t align) {
+    o = (o + align - 1) & ~(align - 1);
+    uint8_t *p = ws ? reinterpret_cast<uint8_t *>(ws) + o : nullptr;
+    o += bytes;
+    return p;
+  };
+  w.flag = reinterpret_cast<uint32_t *>(take(4 * 64, 4));
+  w.plan_bad = reinterpret_cast<uint32_t *>(take(4ull * kSegPlanMaxWgs, 4));
+  w.plan_gx = reinterpret_cast<long long *>(take(8ull * kSegPlanMaxWgs, 8));
+  w.plan_conf = reinterpret_cast<uint32_t *>(take(4ull * kSegPlanMaxWgs, 4));
+  w.first_ev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
+  w.unit_raw = reinterpret_cast<uint32_t *>(take(4 * max_units, 4));
+  w.ev_h = reinterpret_cast<uint32_t *>(take(4 * (2 * n + 1), 4));
+  if (sort) {
+    w.ss.rec = reinterpret_cast<uint4 *>(take(16 * n, 16));
+    w.ss.off = reinterpret_cast<uint64_t *>(take(8 * n, 8));
+    w.ss.arr = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.len = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.perm = reinterpret_cast<uint32_t *>(take(4 * n, 4));
+    w.ss.wsum = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
+    w.ss.wmax = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
+    w.ss.wlo = reinterpret_cast<unsigned long long *>(take(8ull * kSegSortMaxWgs, 8));
+    w.ss.whi = reinterpret_cast<unsigned long long *>(take(8ull * kSegSortMaxWgs, 8));
+    w.ss.fev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
+    w.ss.sync = w.flag + 1;
+    w.ss.spins = 0;
+  }
+  w.bytes = (o + 7) & ~7ull;
+  return w;
+}
 
 // The first grid barrier, also the check that the whole grid is resident (a
 // grid barrier needs every workgroup on a CU at once: k_seg_stream takes one CU
@@ -2205,12 +2234,20 @@ __device__ __forceinline__ bool seg_sync_first(uint32_t *w, uint32_t G, uint32_t
   __syncthreads();
   return s_ok != 0;
 }
-__device__ __forceinline__ void seg_sync(uint32_t *ctr, uint32_t target) {
+// The later barriers, k = 1, 2, ...: a two-level counter tree.  Workgroup w
+// arrives on sub[w % 16]; the last arrival of a group raises root; everyone
+// polls root.  (One counter for all 256 workgroups serialised 256 device-scope
+// atomics on one address per barrier, ~15-20 us each.)  Counters only grow: a
+// group of g workgroups has seen k g arrivals after barrier k.
+__device__ __forceinline__ void seg_sync(uint32_t *root, uint32_t *sub, uint32_t k) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+    const uint32_t G = gridDim.x, ng = G < kSegSyncGroups ? G : kSegSyncGroups, grp = blockIdx.x % ng;
+    const uint32_t gsize = (G - grp + ng - 1) / ng;
+    const uint32_t v = __hip_atomic_fetch_add(sub + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (v == k * gsize) __hip_atomic_fetch_add(root, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(root, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k * ng) __builtin_amdgcn_s_sleep(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
@@ -2219,7 +2256,7 @@ __device__ __forceinline__ void seg_sync(uint32_t *ctr, uint32_t target) {
 // Workgroup reductions / scan over blockDim.x threads (<= 1024), through 16 +
 // 16 shared words; each call ends with a barrier, so calls can follow each other.
 struct SegRed {
-  uint32_t w[kFastWaves];
+  uint32_t w[kFastWaves], w2[kFastWaves];
   unsigned long long q[kFastWaves];
 };
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, SegRed &r) {
@@ -2309,6 +2346,34 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, SegRed &r, u
   return before + x - v;
 }
 
+// OR of bad, sums of gx and conf over the workgroup, in one exchange (the
+// stream's prologue: round 6's first build took 10 us there with one
+// reduction per value)
+__device__ __forceinline__ void seg_block_reduce3(uint32_t &bad, long long &gx, uint32_t &conf, SegRed &r) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    bad |= __shfl_xor(bad, d);
+    gx += __shfl_xor(gx, d);
+    conf += __shfl_xor(conf, d);
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 0) {
+    r.w[w] = bad;
+    r.q[w] = (unsigned long long)gx;
+    r.w2[w] = conf;
+  }
+  __syncthreads();
+  bad = 0;
+  gx = 0;
+  conf = 0;
+  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) {
+    bad |= r.w[k];
+    gx += (long long)r.q[k];
+    conf += r.w2[k];
+  }
+  __syncthreads();
+}
+
 // The sort and the plan of the sorted view (every workgroup of the grid; the
 // caller checked that the key range fits max_units units).  Returns the sorted
 // view's stream mode, or kSegFallback (the grid was not resident, a unit held
@@ -2316,29 +2381,63 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, SegRed &r, u
 // uniform over the grid.
 template <uint32_t kU>
 __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ offs,
-                             const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units, uint64_t smin,
-                             uint64_t emax, const SegSort &ss, uint32_t *__restrict__ unit_raw,
-                             uint32_t *__restrict__ plan_bad,
+                             const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units, const SegSort &ss,
+                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ plan_bad,
                              long long *__restrict__ plan_gx, uint32_t *__restrict__ plan_conf, SegPlanShared &psh,
                              SegRed &red, uint32_t &s_ok) {
   const uint32_t G = gridDim.x, wg = blockIdx.x, T = blockDim.x, tid = threadIdx.x;
-  const uint64_t A0 = smin & ~1023ull;
-  const uint64_t NB = ((emax - A0) >> kU) + 1;
   const uint64_t gstep = (uint64_t)G * T, g0 = (uint64_t)wg * T + tid;
-  uint32_t *cnt = ss.fev, *start = unit_raw;
-  // P0: zero the unit counts
-  for (uint64_t b = g0; b < NB; b += gstep) cnt[b] = 0;
+  // P-1: the key range (lowest start, highest end), per workgroup, then over the grid
+  uint64_t lo = ~0ull, hi = 0;
+  for (uint64_t j = g0; j < n; j += gstep) {
+    const uint64_t s = (uint64_t)base + offs[j], e = s + lens[j];
+    lo = s < lo ? s : lo;
+    hi = e > hi ? e : hi;
+  }
+  lo = block_min_u64(lo, red);
+  hi = block_max_u64(hi, red);
+  if (tid == 0) {
+    ss.wlo[wg] = lo;
+    ss.whi[wg] = hi;
+  }
   if (!seg_sync_first(ss.sync, G, ss.spins, s_ok)) return kSegFallback;
   uint32_t phase = 0;
   auto sync = [&]() {
-    seg_sync(ss.sync + 1, ++phase * G);
-    seg_prof(2 + phase);  // 3: P1 done .. 7: P5 done
+    seg_sync(ss.sync + 1, ss.sync + 2, ++phase);
+    seg_prof(2 + phase);  // 3: P0 done, 4: P1, 5-6: P2 (two barriers), 7: P3, 8: P4, 9: P5
   };
-  seg_prof(2);  // P0 + the residency check
-  // P1: count records per unit; each record's arrival rank in its unit
-  for (uint64_t j = g0; j < n; j += gstep) {
-    const uint64_t key = (uint64_t)base + offs[j] - A0;
-    ss.arr[j] = __hip_atomic_fetch_add(&cnt[key >> kU], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  seg_prof(2);  // the key range + the residency check
+  lo = ~0ull;
+  hi = 0;
+  for (uint32_t k = tid; k < G; k += T) {
+    lo = ss.wlo[k] < lo ? ss.wlo[k] : lo;
+    hi = ss.whi[k] > hi ? ss.whi[k] : hi;
+  }
+  const uint64_t smin = uni64(block_min_u64(lo, red)), emax = uni64(block_max_u64(hi, red));
+  const uint64_t A0 = smin & ~1023ull;
+  // (uniform over the grid: every workgroup read the same slots)
+  if (smin > emax || ((emax - A0) >> kU) + 1 > max_units) return kSegFallback;
+  const uint64_t NB = ((emax - A0) >> kU) + 1;
+  uint32_t *cnt = ss.fev, *start = unit_raw;
+  // P0: zero the unit counts
+  for (uint64_t b = g0; b < NB; b += gstep) cnt[b] = 0;
+  sync();
+  // P1: count records per unit; each record's arrival rank in its unit.  kSortBatch
+  // records a thread at a time, every atomic issued before the first result is
+  // stored (random atomics on a permuted batch: latency-bound one at a time)
+  constexpr uint32_t kSortBatch = 4;
+  for (uint64_t j0 = g0; j0 < n; j0 += gstep * kSortBatch) {
+    uint32_t r[kSortBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kSortBatch; k++) {
+      const uint64_t j = j0 + k * gstep;
+      r[k] = j < n ? __hip_atomic_fetch_add(&cnt[((uint64_t)base + offs[j] - A0) >> kU], 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSortBatch; k++)
+      if (j0 + k * gstep < n) ss.arr[j0 + k * gstep] = r[k];
   }
   sync();
   // P2: exclusive scan of the counts (workgroup wg: units [wg C, wg C + C))
@@ -2373,14 +2472,23 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
     run += cnt[b];
   }
   sync();
-  // P3: scatter the keys (and lengths) by unit, in arrival order inside a
-  // unit: the batch arrays read in order, the writes land in its unit's range
-  for (uint64_t j = g0; j < n; j += gstep) {
-    const uint64_t key = (uint64_t)base + offs[j] - A0;
-    const uint32_t pos = start[key >> kU] + ss.arr[j];
-    ss.key[pos] = key;
-    ss.idx[pos] = (uint32_t)j;
-    ss.ltmp[pos] = lens[j];
+  // P3: scatter (key, index, length) by unit, in arrival order inside a unit:
+  // the batch arrays read in order, one 16-B store into its unit's range
+  // (three 4/8-B arrays dirtied three lines a record), kSortBatch at a time
+  for (uint64_t j0 = g0; j0 < n; j0 += gstep * kSortBatch) {
+    uint64_t key[kSortBatch];
+    uint32_t pos[kSortBatch], len[kSortBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kSortBatch; k++) {
+      const uint64_t j = j0 + k * gstep, jj = j < n ? j : 0;
+      key[k] = (uint64_t)base + offs[jj] - A0;
+      len[k] = lens[jj];
+      pos[k] = start[key[k] >> kU] + ss.arr[jj];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSortBatch; k++)
+      if (j0 + k * gstep < n)
+        ss.rec[pos[k]] = make_uint4((uint32_t)key[k], (uint32_t)(key[k] >> 32), (uint32_t)(j0 + k * gstep), len[k]);
   }
   sync();
   // P4: each record's rank among its unit's records (start offset, then batch
@@ -2388,27 +2496,27 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
   // read and write near p (the offset is the key's: no gather from the batch)
   const uint64_t off0 = A0 - (uint64_t)base;
   for (uint64_t p = g0; p < n; p += gstep) {
-    const uint64_t key = ss.key[p];
-    const uint32_t j = ss.idx[p];
+    const uint4 me = ss.rec[p];
+    const uint64_t key = ((uint64_t)me.y << 32) | me.x;
+    const uint32_t j = me.z;
     const uint64_t b = key >> kU;
     const uint32_t s0 = start[b], c = cnt[b];
     uint32_t rank = 0;
     for (uint32_t q = s0; q < s0 + c; q++) {
-      const uint64_t kq = ss.key[q];
-      rank += (kq < key || (kq == key && ss.idx[q] < j)) ? 1u : 0u;
+      const uint4 o = ss.rec[q];
+      const uint64_t kq = ((uint64_t)o.y << 32) | o.x;
+      rank += (kq < key || (kq == key && o.z < j)) ? 1u : 0u;
     }
     const uint32_t pos = s0 + rank;
     ss.off[pos] = key + off0;
-    ss.len[pos] = ss.ltmp[p];
+    ss.len[pos] = me.w;
     ss.perm[pos] = j;
   }
   sync();
   // P5: the plan of the sorted view (first_ev, the slots 0 .. G-1)
-  seg_plan_body<kU>(base, ss.off, ss.len, n, max_units, wg, G, plan_bad, plan_gx, plan_conf, ss.fev, nullptr,
-                    nullptr, psh);
+  seg_plan_body<kU>(base, ss.off, ss.len, n, max_units, wg, G, plan_bad, plan_gx, plan_conf, ss.fev, psh);
   sync();
   // P6: its mode, as the prologue chooses one (no k_crc_grp: this batch is not all its blocks)
-  seg_prof(8);
   uint32_t bad = 0;
   long long gx = 0;
   for (uint32_t k = tid; k < G; k += T) {
@@ -2417,6 +2525,7 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
   }
   bad = block_or_u32(bad, red);
   gx = block_sum_i64(gx, red);
+  seg_prof(10);
   return !(bad & 1u)                ? kSegPacked
          : !(bad & 12u) && gx <= 0  ? kSegGapSmall
          : !(bad & 2u) && gx <= 0   ? kSegGapped
@@ -2439,10 +2548,8 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
                                                             const uint32_t *__restrict__ first_ev,
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
                                                             const DeviceTables *__restrict__ tables,
-                                                            uint64_t max_units,
-                                                            const unsigned long long *__restrict__ plan_min,
-                                                            const unsigned long long *__restrict__ plan_max,
-                                                            SegSort ss) {
+                                                            uint64_t max_units, uint32_t *__restrict__ ws,
+                                                            uint32_t sort_on, uint32_t sync_spins) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
   __shared__ uint32_t s_next, s_ok;
   __shared__ SegRed red;
@@ -2453,25 +2560,17 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   seg_prof(0);
   uint32_t bad = 0, conf = 0;
   long long gx = 0;
-  uint64_t smin = ~0ull, emax = 0;
   for (uint32_t i = tid; i < plan_wgs; i += kFastThreads) {
     bad |= plan_bad[i];
     gx += plan_gx[i];
     conf += plan_conf[i];
-    if (ss.sync) {
-      smin = plan_min[i] < smin ? plan_min[i] : smin;
-      emax = plan_max[i] > emax ? plan_max[i] : emax;
-    }
   }
-  // (reductions through LDS: readfirstlane tells hipcc the values are uniform,
-  // else every address the stream body forms from them is a VGPR -- 55 spilled)
-  const uint32_t unpacked = uni(block_or_u32(bad & 1u, red));
-  const uint32_t unsorted = uni(block_or_u32(bad & 2u, red));
-  const uint32_t not_small = uni(block_or_u32(bad & 12u, red));
-  const long long gsum = (long long)uni64((uint64_t)block_sum_i64(gx, red));
-  const uint64_t csum = uni(block_sum_u32(conf, red));
-  smin = uni64(block_min_u64(smin, red));
-  emax = uni64(block_max_u64(emax, red));
+  // one exchange for the three (readfirstlane: hipcc then knows the results are
+  // uniform; else every address the stream body forms from them is a VGPR)
+  seg_block_reduce3(bad, gx, conf, red);
+  const uint32_t unpacked = uni(bad & 1u), unsorted = uni(bad & 2u), not_small = uni(bad & 12u);
+  const long long gsum = (long long)uni64((uint64_t)gx);
+  const uint64_t csum = uni(conf);
   // k_crc_grp when every record is one of its blocks (16-B aligned 4 KiB
   // multiples) in a large batch, whatever their order: ahead of the stream's
   // own modes, whose event work at 4 KiB records costs more than the hand-out
@@ -2489,10 +2588,15 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   // sort_min records) whose key range fits the unit arrays: its sorted view
   bool sorted = false;
   seg_prof(1);  // the prologue's reductions done
-  if (mode == kSegFallback && ss.sync && smin <= emax && gridDim.x <= kSegSortMaxWgs &&
-      ((emax - (smin & ~1023ull)) >> kU) + 1 <= max_units) {
-    mode = uni(seg_sort<kU>(base, offs, lens, n, max_units, smin, emax, ss, unit_raw, plan_bad, plan_gx, plan_conf,
-                            psh, red, s_ok));
+  // (the sort's pointers come from the workspace base here, not as kernel
+  // arguments: live across the kernel, they pushed the unsorted small-gap
+  // loop's SGPRs into spills -- 16 more reloads a group, -0.75 points)
+  SegSort ss{};
+  if (mode == kSegFallback && sort_on && gridDim.x <= kSegSortMaxWgs) {
+    ss = seg_ws_layout(ws, n, max_units, true).ss;
+    ss.spins = sync_spins;
+    mode = uni(seg_sort<kU>(base, offs, lens, n, max_units, ss, unit_raw, plan_bad, plan_gx, plan_conf, psh, red,
+                            s_ok));
     sorted = mode != kSegFallback;
     if (sorted && blockIdx.x == 0 && tid == 0) *flag = mode | kSegSortedBit;
   }
@@ -2517,9 +2621,9 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
       seg_stream_body<kSegPacked, kU, kV>(lds, s_next, col, base, o, l, n, lg_chunk, fe, unit_raw, ev_h);
   };
   if (sorted) {
-    seg_prof(9);
+    seg_prof(14);
     run(std::true_type{}, ss.off, ss.len, ss.fev);
-    seg_prof(10);
+    seg_prof(15);
   } else {
     run(std::false_type{}, offs, lens, first_ev);
   }
@@ -2945,56 +3049,6 @@ hipError_t launch_fill(uint8_t *base, const uint64_t *off, const uint32_t *len, 
 
 uint64_t seg_max_units(uint64_t span_bound) { return (span_bound >> kSegUnitLg) + 2; }
 
-// workspace (u32 words): the mode flag (64 words: word 0 the mode, words 1-2
-// the sort's barrier words), plan_bad[kSegPlanMaxWgs], plan_gx[kSegPlanMaxWgs]
-// (int64), plan_conf[kSegPlanMaxWgs], first_ev[max_units + 1],
-// unit_raw[max_units], ev_h[2n + 1] (the gapped numbering's 2n events; a
-// packed batch uses n + 1); 8-B aligned after it plan_min / plan_max
-// [kSegPlanMaxWgs] (u64) and, with a sort, SegSort's arrays.
-namespace {
-struct SegWs {
-  uint32_t *flag, *plan_bad, *plan_conf, *first_ev, *unit_raw, *ev_h;
-  long long *plan_gx;
-  unsigned long long *plan_min, *plan_max;
-  SegSort ss;
-  uint64_t bytes;
-};
-SegWs seg_ws_layout(uint32_t *ws, uint64_t n, uint64_t max_units, bool sort) {
-  SegWs w{};
-  uint64_t o = 0;  // bytes
-  auto take = [&](uint64_t bytes, uint64_t align) {
-    o = (o + align - 1) & ~(align - 1);
-    uint8_t *p = ws ? reinterpret_cast<uint8_t *>(ws) + o : nullptr;
-    o += bytes;
-    return p;
-  };
-  w.flag = reinterpret_cast<uint32_t *>(take(4 * 64, 4));
-  w.plan_bad = reinterpret_cast<uint32_t *>(take(4ull * kSegPlanMaxWgs, 4));
-  w.plan_gx = reinterpret_cast<long long *>(take(8ull * kSegPlanMaxWgs, 8));
-  w.plan_conf = reinterpret_cast<uint32_t *>(take(4ull * kSegPlanMaxWgs, 4));
-  w.first_ev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
-  w.unit_raw = reinterpret_cast<uint32_t *>(take(4 * max_units, 4));
-  w.ev_h = reinterpret_cast<uint32_t *>(take(4 * (2 * n + 1), 4));
-  w.plan_min = reinterpret_cast<unsigned long long *>(take(8ull * kSegPlanMaxWgs, 8));
-  w.plan_max = reinterpret_cast<unsigned long long *>(take(8ull * kSegPlanMaxWgs, 8));
-  if (sort) {
-    w.ss.key = reinterpret_cast<unsigned long long *>(take(8 * n, 8));
-    w.ss.off = reinterpret_cast<uint64_t *>(take(8 * n, 8));
-    w.ss.idx = reinterpret_cast<uint32_t *>(take(4 * n, 4));
-    w.ss.arr = reinterpret_cast<uint32_t *>(take(4 * n, 4));
-    w.ss.ltmp = reinterpret_cast<uint32_t *>(take(4 * n, 4));
-    w.ss.len = reinterpret_cast<uint32_t *>(take(4 * n, 4));
-    w.ss.perm = reinterpret_cast<uint32_t *>(take(4 * n, 4));
-    w.ss.wsum = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
-    w.ss.wmax = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
-    w.ss.fev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
-    w.ss.sync = w.flag + 1;
-  }
-  w.bytes = (o + 7) & ~7ull;
-  return w;
-}
-}  // namespace
-
 hipError_t seg_prof_read(uint64_t *out16) {
   return hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_seg_prof), sizeof(g_seg_prof), 0, hipMemcpyDeviceToHost);
 }
@@ -3010,8 +3064,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint64_t n = b.nblocks;
   // the sorted view (seg_sort): from sort_min records, on a grid it can meet at barriers
   const bool sort = sort_min && n >= sort_min && grid <= (int)kSegSortMaxWgs;
-  SegWs w = seg_ws_layout(ws, n, max_units, sort);
-  w.ss.spins = sync_spins;
+  const SegWs w = seg_ws_layout(ws, n, max_units, sort);
   const uint64_t pg = (n + 256) / 256;
   // HC_SEG_PLAN_WGS overrides the plan's grid cap, up to kSegPlanMaxWgs (tuning sweeps)
   static const uint64_t cap = (uint64_t)std::max(1, std::min((int)kSegPlanMaxWgs, env_int("HC_SEG_PLAN_WGS", (int)kSegPlanWgs)));
@@ -3019,8 +3072,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   // every launch checked: a later kernel must not run on a failed one's stale
   // outputs (hipGetLastError reports the latest call, not the first failure)
   hipLaunchKernelGGL(k_seg_plan<>, dim3(plan_wgs), dim3(256), 0, s, b.base, b.off, b.len, n, max_units, w.plan_bad,
-                     w.plan_gx, w.plan_conf, w.first_ev, sort ? w.plan_min : nullptr, sort ? w.plan_max : nullptr,
-                     w.ss.sync);
+                     w.plan_gx, w.plan_conf, w.first_ev, w.ss.sync);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // a batch large enough that a gated launch (exiting on its first load unless
@@ -3029,7 +3081,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint32_t allow_grp = n >= grp_min ? 1u : 0u;
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
                      w.plan_bad, w.plan_gx, w.plan_conf, plan_wgs, allow_grp, w.flag, w.first_ev, w.unit_raw, w.ev_h,
-                     b.tables, max_units, w.plan_min, w.plan_max, w.ss);
+                     b.tables, max_units, ws, sort ? 1u : 0u, sync_spins);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, w.flag, w.unit_raw,
                      w.ev_h, b.crc_out, st, taken, b.flags, b.tables, w.ss.off, w.ss.len, w.ss.perm);

@@ -346,9 +346,10 @@ int hc_debug_tables(void *out, size_t cap);
 int hc_debug_seg_taken(void);
 /* The stream kernel's phase clock for this thread's last batch on the stream
  * (DESIGN.md 4.2b): 16 s_memrealtime stamps (100 MHz) of workgroup 0 -- [0]
- * start, [1] prologue done, [2] the sort's residency check, [3..7] its phases
- * P1..P5, [8] P6, [9] / [10] the sorted view's stream body start / end (stale
- * entries when no sort ran).  Synchronizes that device (tools only). */
+ * start, [1] prologue done, [2] the sort's key range and residency check,
+ * [3..9] its barriers after P0, P1, P2 (two), P3, P4, P5, [10] P6, [14] / [15]
+ * the sorted view's stream body start / end (stale entries when no sort ran).
+ * Synchronizes that device (tools only). */
 int hc_debug_seg_prof(uint64_t *out16);
 
 /* The library reads its HC_* settings from the environment once, at the first

@@ -1,8 +1,9 @@
 """The sorted view's phase clock: config 5's records back to
 back, listed in a permuted order, through dev_crc32_blocks; per call the
 stream kernel's workgroup-0 stamps (hc_debug_seg_prof, microseconds from the
-kernel's start): prologue, residency check, P1 count, P2 scan, P3 scatter, P4
-rank, P5 plan, the sorted stream body; and the words against an in-order run.
+kernel's start, each phase's END): prologue, key range + residency check, P0
+zero, P1 count, P2 scan (two barriers), P3 scatter, P4 rank, P5 plan, P6, the
+sorted stream body; and the words against an in-order run.
 
   python tools/sort_phase_probe.py [--records 2000000] [--calls 3]
 """
@@ -27,8 +28,8 @@ def main():
 
     from hunddb_amd import crc
 
-    names = ["prologue", "resident", "P1_count", "P2_scan", "P3_scatter", "P4_rank", "P5_plan", "P6", "body_start",
-             "body_end"]
+    stamps_at = {"prologue": 1, "range_resident": 2, "P0_zero": 3, "P1_count": 4, "P2a_scan": 5, "P2b_scan": 6,
+                 "P3_scatter": 7, "P4_rank": 8, "P5_plan": 9, "P6_mode": 10, "body_start": 14, "body_end": 15}
     for n in [int(x) for x in a.records.split(",")]:
         lens = record_sizes(n)
         off = np.zeros(n, dtype=np.uint64)
@@ -52,7 +53,7 @@ def main():
             torch.cuda.synchronize()
             path = crc.seg_path()
             prof = crc.seg_prof()
-            stamps = {k: round(prof[i + 1], 1) for i, k in enumerate(names)}
+            stamps = {k: round(prof[i], 1) for k, i in stamps_at.items()}
             same = bool(torch.equal(out.cpu(), ref.cpu()[torch.from_numpy(perm)]))
             print(json.dumps({"records": n, "call": c, "dispatch_ms": round(e0.elapsed_time(e1), 4), "path": path,
                               "stamps_us": stamps, "words_equal": same}), flush=True)
