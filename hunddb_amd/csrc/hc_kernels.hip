@@ -1790,7 +1790,7 @@ __global__ __launch_bounds__(256) void k_seg_plan(const uint8_t *base, const uin
                                                   uint32_t *__restrict__ plan_conf, uint32_t *__restrict__ first_ev,
                                                   uint32_t *__restrict__ sync) {
   __shared__ SegPlanShared sh;
-  if (sync && blockIdx.x == 0 && threadIdx.x < 2 + kSegSyncGroups) sync[threadIdx.x] = 0;
+  if (sync && blockIdx.x == 0 && threadIdx.x < 3 + kSegSyncGroups) sync[threadIdx.x] = 0;
   seg_plan_body<kU>(base, offs, lens, n, max_units, blockIdx.x, gridDim.x, plan_bad, plan_gx, plan_conf, first_ev, sh);
 }
 
@@ -2116,29 +2116,32 @@ __device__ __forceinline__ void seg_stream_body(uint32_t *lds, uint32_t &s_next,
 // stays unwritten in this kernel, so the unsorted stream keeps reading it with
 // scalar loads) and the stream's unit_raw (unit starts; the stream rewrites it).
 struct SegSort {
-  uint4 *rec;               // n: (key = start - A0, batch index, length) in bucket order, one 16-B store
+  uint4 *reca, *recb;       // n each: (key = start - A0, batch index, length) by coarse bucket, then by unit
   uint64_t *off;            // n: the sorted view's offsets
-  uint32_t *arr;            // n: each record's arrival rank in its unit
+  uint32_t *arr;            // n: each record's arrival rank in its unit (recA order)
   uint32_t *len;            // n: the sorted view's lengths
   uint32_t *perm;           // n: sorted position -> batch index
-  uint32_t *wsum, *wmax;    // kSegSortMaxWgs: per-workgroup unit-count sums / maxima
+  uint32_t *hc;             // kSegSortNbcMax x kSegSortMaxWgs: tile counts per coarse bucket, then offsets
+  uint32_t *tc, *tb;        // kSegSortNbcMax each: coarse bucket totals and bases
   unsigned long long *wlo, *whi;  // kSegSortMaxWgs: per-workgroup lowest start / highest end
   uint32_t *sync;           // 18 words (zeroed by k_seg_plan): the first barrier, the others' root and 16 group counters
-  uint32_t *fev;            // max_units + 1: the unit counts, then the sorted view's first_ev
+  uint32_t *fev;            // max_units + 1: the sorted view's first_ev
   uint32_t spins;           // the first barrier's bound (kSegSyncSpins; HC_SEG_SYNC_SPINS, a test hook)
+  uint32_t ucmax;           // units per coarse bucket at most (kSegSortUcMax; HC_SEG_SORT_UC, a test hook)
 };
 constexpr uint32_t kSegSortedBit = 8;        // the mode word of a sorted view: its mode | 8
 // Phase clock of the last sort (hc_debug_seg_prof): workgroup 0's s_memrealtime
 // (100 MHz): [0] the stream's start, [1] its prologue, [2] the key range and
-// the residency check, [3..9] the sort's barriers (P0, P1, P2 twice, P3, P4,
-// P5), [10] P6, [14] / [15] the sorted body's start / end.  One store each by
-// one thread.
+// the residency check, [3..7] the sort's barriers (A1, A2, A3, B, P5), [10] P6,
+// [14] / [15] the sorted body's start / end.  One store each by one thread.
 __device__ unsigned long long g_seg_prof[16];
 __device__ __forceinline__ void seg_prof(uint32_t k) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && k < 16) g_seg_prof[k] = __builtin_amdgcn_s_memrealtime();
 }
 constexpr uint32_t kSegSortMaxBucket = 1024; // most records one 16 KiB unit may start (zero-length ones)
 constexpr uint32_t kSegSortMaxWgs = 1024;    // the stream's largest grid with a sort
+constexpr uint32_t kSegSortUcMax = 32768;    // units per coarse bucket: the LDS counters of phase B (128 KiB)
+constexpr uint32_t kSegSortNbcMax = 4096;    // coarse buckets (2 LDS words each in phase A)
 constexpr uint32_t kSegSyncAbort = 1u << 31;
 
 // workspace (u32 words): the mode flag (64 words: word 0 the mode, words 1-18
@@ -2169,18 +2172,21 @@ __host__ __device__ __forceinline__ SegWs seg_ws_layout(uint32_t *ws, uint64_t n
   w.unit_raw = reinterpret_cast<uint32_t *>(take(4 * max_units, 4));
   w.ev_h = reinterpret_cast<uint32_t *>(take(4 * (2 * n + 1), 4));
   if (sort) {
-    w.ss.rec = reinterpret_cast<uint4 *>(take(16 * n, 16));
+    w.ss.reca = reinterpret_cast<uint4 *>(take(16 * n, 16));
+    w.ss.recb = reinterpret_cast<uint4 *>(take(16 * n, 16));
     w.ss.off = reinterpret_cast<uint64_t *>(take(8 * n, 8));
     w.ss.arr = reinterpret_cast<uint32_t *>(take(4 * n, 4));
     w.ss.len = reinterpret_cast<uint32_t *>(take(4 * n, 4));
     w.ss.perm = reinterpret_cast<uint32_t *>(take(4 * n, 4));
-    w.ss.wsum = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
-    w.ss.wmax = reinterpret_cast<uint32_t *>(take(4ull * kSegSortMaxWgs, 4));
+    w.ss.hc = reinterpret_cast<uint32_t *>(take(4ull * kSegSortNbcMax * kSegSortMaxWgs, 4));
+    w.ss.tc = reinterpret_cast<uint32_t *>(take(4ull * kSegSortNbcMax, 4));
+    w.ss.tb = reinterpret_cast<uint32_t *>(take(4ull * kSegSortNbcMax, 4));
     w.ss.wlo = reinterpret_cast<unsigned long long *>(take(8ull * kSegSortMaxWgs, 8));
     w.ss.whi = reinterpret_cast<unsigned long long *>(take(8ull * kSegSortMaxWgs, 8));
     w.ss.fev = reinterpret_cast<uint32_t *>(take(4 * (max_units + 1), 4));
     w.ss.sync = w.flag + 1;
     w.ss.spins = 0;
+    w.ss.ucmax = 0;
   }
   w.bytes = (o + 7) & ~7ull;
   return w;
@@ -2382,7 +2388,7 @@ __device__ __forceinline__ void seg_block_reduce3(uint32_t &bad, long long &gx, 
 template <uint32_t kU>
 __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ offs,
                              const uint32_t *__restrict__ lens, uint64_t n, uint64_t max_units, const SegSort &ss,
-                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ plan_bad,
+                             uint32_t *scratch, uint32_t *__restrict__ plan_bad,
                              long long *__restrict__ plan_gx, uint32_t *__restrict__ plan_conf, SegPlanShared &psh,
                              SegRed &red, uint32_t &s_ok) {
   const uint32_t G = gridDim.x, wg = blockIdx.x, T = blockDim.x, tid = threadIdx.x;
@@ -2404,7 +2410,7 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
   uint32_t phase = 0;
   auto sync = [&]() {
     seg_sync(ss.sync + 1, ss.sync + 2, ++phase);
-    seg_prof(2 + phase);  // 3: P0 done, 4: P1, 5-6: P2 (two barriers), 7: P3, 8: P4, 9: P5
+    seg_prof(2 + phase);  // 3: A1 done, 4: A2, 5: A3, 6: B, 7: P5
   };
   seg_prof(2);  // the key range + the residency check
   lo = ~0ull;
@@ -2418,101 +2424,128 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
   // (uniform over the grid: every workgroup read the same slots)
   if (smin > emax || ((emax - A0) >> kU) + 1 > max_units) return kSegFallback;
   const uint64_t NB = ((emax - A0) >> kU) + 1;
-  uint32_t *cnt = ss.fev, *start = unit_raw;
-  // P0: zero the unit counts
-  for (uint64_t b = g0; b < NB; b += gstep) cnt[b] = 0;
-  sync();
-  // P1: count records per unit; each record's arrival rank in its unit.  kSortBatch
-  // records a thread at a time, every atomic issued before the first result is
-  // stored (random atomics on a permuted batch: latency-bound one at a time)
-  constexpr uint32_t kSortBatch = 4;
-  for (uint64_t j0 = g0; j0 < n; j0 += gstep * kSortBatch) {
-    uint32_t r[kSortBatch];
-#pragma unroll
-    for (uint32_t k = 0; k < kSortBatch; k++) {
-      const uint64_t j = j0 + k * gstep;
-      r[k] = j < n ? __hip_atomic_fetch_add(&cnt[((uint64_t)base + offs[j] - A0) >> kU], 1u, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT)
-                   : 0u;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kSortBatch; k++)
-      if (j0 + k * gstep < n) ss.arr[j0 + k * gstep] = r[k];
-  }
-  sync();
-  // P2: exclusive scan of the counts (workgroup wg: units [wg C, wg C + C))
-  const uint64_t C = (NB + G - 1) / G, per = (C + T - 1) / T;
-  const uint64_t b0 = (uint64_t)wg * C, b1 = b0 + C < NB ? b0 + C : NB;
-  const uint64_t t0 = b0 + (uint64_t)tid * per, t1 = t0 + per < b1 ? t0 + per : b1;
-  uint32_t lsum = 0, lmax = 0;
-  for (uint64_t b = t0; b < t1; b++) {
-    const uint32_t c = cnt[b];
-    lsum += c;
-    lmax = c > lmax ? c : lmax;
-  }
-  uint32_t wtot = 0;
-  const uint32_t texcl = block_excl_scan_u32(lsum, red, wtot);
-  const uint32_t wmx = block_max_u32(lmax, red);
-  if (tid == 0) {
-    ss.wsum[wg] = wtot;
-    ss.wmax[wg] = wmx;
-  }
-  sync();
-  uint32_t pre = 0, gmx = 0;
-  for (uint32_t k = tid; k < G; k += T) {
-    if (k < wg) pre += ss.wsum[k];
-    gmx = ss.wmax[k] > gmx ? ss.wmax[k] : gmx;
-  }
-  pre = block_sum_u32(pre, red);
-  gmx = block_max_u32(gmx, red);
-  if (gmx > kSegSortMaxBucket) return kSegFallback;  // (every workgroup reads the same maxima)
-  uint32_t run = pre + texcl;
-  for (uint64_t b = t0; b < t1; b++) {
-    start[b] = run;
-    run += cnt[b];
-  }
-  sync();
-  // P3: scatter (key, index, length) by unit, in arrival order inside a unit:
-  // the batch arrays read in order, one 16-B store into its unit's range
-  // (three 4/8-B arrays dirtied three lines a record), kSortBatch at a time
-  for (uint64_t j0 = g0; j0 < n; j0 += gstep * kSortBatch) {
-    uint64_t key[kSortBatch];
-    uint32_t pos[kSortBatch], len[kSortBatch];
-#pragma unroll
-    for (uint32_t k = 0; k < kSortBatch; k++) {
-      const uint64_t j = j0 + k * gstep, jj = j < n ? j : 0;
-      key[k] = (uint64_t)base + offs[jj] - A0;
-      len[k] = lens[jj];
-      pos[k] = start[key[k] >> kU] + ss.arr[jj];
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kSortBatch; k++)
-      if (j0 + k * gstep < n)
-        ss.rec[pos[k]] = make_uint4((uint32_t)key[k], (uint32_t)(key[k] >> 32), (uint32_t)(j0 + k * gstep), len[k]);
-  }
-  sync();
-  // P4: each record's rank among its unit's records (start offset, then batch
-  // index: zero-length records may share a start) -> the sorted arrays; every
-  // read and write near p (the offset is the key's: no gather from the batch)
+  // nbc coarse buckets of UC units each, one owner workgroup a bucket (d % G)
+  const uint64_t ucmax = ss.ucmax ? (ss.ucmax < kSegSortUcMax ? ss.ucmax : kSegSortUcMax) : kSegSortUcMax;
+  const uint64_t m = (NB + (uint64_t)G * ucmax - 1) / ((uint64_t)G * ucmax);
+  if (m * G > kSegSortNbcMax) return kSegFallback;  // (a span of more than 2^40 bytes)
+  const uint32_t nbc = (uint32_t)m * G;
+  const uint64_t UC = (NB + nbc - 1) / nbc;
   const uint64_t off0 = A0 - (uint64_t)base;
-  for (uint64_t p = g0; p < n; p += gstep) {
-    const uint4 me = ss.rec[p];
-    const uint64_t key = ((uint64_t)me.y << 32) | me.x;
-    const uint32_t j = me.z;
-    const uint64_t b = key >> kU;
-    const uint32_t s0 = start[b], c = cnt[b];
-    uint32_t rank = 0;
-    for (uint32_t q = s0; q < s0 + c; q++) {
-      const uint4 o = ss.rec[q];
-      const uint64_t kq = ((uint64_t)o.y << 32) | o.x;
-      rank += (kq < key || (kq == key && o.z < j)) ? 1u : 0u;
-    }
-    const uint32_t pos = s0 + rank;
-    ss.off[pos] = key + off0;
-    ss.len[pos] = me.w;
-    ss.perm[pos] = j;
+  // a record's coarse bucket: its unit / UC in 32 bits (units < 2^32; a 64-bit
+  // division by a run-time value is a long call per record)
+  const uint32_t uc32 = (uint32_t)UC;
+  auto bucket_of = [&](uint64_t key) -> uint32_t { return (uint32_t)(key >> kU) / uc32; };
+  // A: the workgroup's tile of the batch (contiguous: coalesced reads)
+  const uint64_t tile = (n + G - 1) / G;
+  const uint64_t j_lo = (uint64_t)wg * tile < n ? (uint64_t)wg * tile : n, j_hi = j_lo + tile < n ? j_lo + tile : n;
+  uint32_t *hist = scratch, *lbase = scratch + kSegSortNbcMax;  // LDS
+  // A1: histogram of the tile over the coarse buckets (LDS atomics)
+  for (uint32_t d = tid; d < nbc; d += T) hist[d] = 0;
+  __syncthreads();
+  for (uint64_t j = j_lo + tid; j < j_hi; j += T)
+    atomicAdd(&hist[bucket_of((uint64_t)base + offs[j] - A0)], 1u);
+  __syncthreads();
+  for (uint32_t d = tid; d < nbc; d += T) ss.hc[(uint64_t)d * G + wg] = hist[d];
+  sync();  // 3
+  // A2: bucket d's offsets of the workgroups' tiles (exclusive, in place) and its total
+  for (uint32_t d = wg; d < nbc; d += G) {
+    const uint32_t v = tid < G ? ss.hc[(uint64_t)d * G + tid] : 0u;
+    uint32_t tot = 0;
+    const uint32_t ex = block_excl_scan_u32(v, red, tot);
+    if (tid < G) ss.hc[(uint64_t)d * G + tid] = ex;
+    if (tid == 0) ss.tc[d] = tot;
   }
-  sync();
+  sync();  // 4
+  // A3: the buckets' bases (every workgroup: a scan of the nbc totals), then the
+  // tile's records to recA, each at its bucket's base + the tile's offset + its
+  // arrival rank in the tile (LDS atomics)
+  {
+    const uint32_t per = (nbc + T - 1) / T, d0 = tid * per, d1 = d0 + per < nbc ? d0 + per : nbc;
+    uint32_t sum = 0;
+    for (uint32_t d = d0; d < d1; d++) sum += ss.tc[d];
+    uint32_t tot = 0;
+    uint32_t run = block_excl_scan_u32(sum, red, tot);
+    for (uint32_t d = d0; d < d1; d++) {
+      if (wg == 0) ss.tb[d] = run;  // (phase B reads the bases there: its counters reuse this LDS)
+      lbase[d] = run + ss.hc[(uint64_t)d * G + wg];
+      hist[d] = 0;
+      run += ss.tc[d];
+    }
+  }
+  __syncthreads();
+  for (uint64_t j = j_lo + tid; j < j_hi; j += T) {
+    const uint64_t key = (uint64_t)base + offs[j] - A0;
+    const uint32_t d = bucket_of(key);
+    const uint32_t pos = lbase[d] + atomicAdd(&hist[d], 1u);
+    ss.reca[pos] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)j, lens[j]);
+  }
+  sync();  // 5
+  // B: each owned bucket by unit, in LDS counters: count (arrival ranks), scan,
+  // scatter to recb inside the bucket's range, then each record's rank among its
+  // unit's records (start, then batch index: zero-length records may share a
+  // start) -> the sorted arrays.  Every access stays in the bucket's range.
+  uint32_t *ucnt = scratch;  // UC + 1 words (the A arrays are no longer needed)
+  uint32_t too_many = 0;
+  for (uint32_t d = wg; d < nbc; d += G) {
+    const uint64_t p0 = ss.tb[d], pc = ss.tc[d];
+    const uint64_t u0 = (uint64_t)d * UC, nu = u0 < NB ? (NB - u0 < UC ? NB - u0 : UC) : 0;
+    __syncthreads();  // (the previous bucket's readers of ucnt are done)
+    for (uint64_t u = tid; u <= nu; u += T) ucnt[u] = 0;
+    __syncthreads();
+    for (uint64_t p = p0 + tid; p < p0 + pc; p += T) {
+      const uint4 r = ss.reca[p];
+      const uint64_t key = ((uint64_t)r.y << 32) | r.x;
+      ss.arr[p] = atomicAdd(&ucnt[(key >> kU) - u0], 1u);
+    }
+    __syncthreads();
+    {  // exclusive scan of ucnt[0 .. nu) in place; ucnt[nu] = the total
+      const uint32_t per = (uint32_t)((nu + T - 1) / T);
+      const uint64_t a0 = (uint64_t)tid * per, a1 = a0 + per < nu ? a0 + per : nu;
+      uint32_t sum = 0, mx = 0;
+      for (uint64_t u = a0; u < a1; u++) {
+        sum += ucnt[u];
+        mx = ucnt[u] > mx ? ucnt[u] : mx;
+      }
+      uint32_t tot = 0;
+      uint32_t run = block_excl_scan_u32(sum, red, tot);
+      too_many |= block_max_u32(mx, red) > kSegSortMaxBucket ? 1u : 0u;
+      for (uint64_t u = a0; u < a1; u++) {
+        const uint32_t c = ucnt[u];
+        ucnt[u] = run;
+        run += c;
+      }
+      if (tid == 0) ucnt[nu] = tot;
+    }
+    __syncthreads();
+    if (too_many) continue;  // (workgroup-uniform; the grid learns it below)
+    for (uint64_t p = p0 + tid; p < p0 + pc; p += T) {
+      const uint4 r = ss.reca[p];
+      const uint64_t key = ((uint64_t)r.y << 32) | r.x;
+      ss.recb[p0 + ucnt[(key >> kU) - u0] + ss.arr[p]] = r;
+    }
+    __syncthreads();
+    for (uint64_t p = p0 + tid; p < p0 + pc; p += T) {
+      const uint4 me = ss.recb[p];
+      const uint64_t key = ((uint64_t)me.y << 32) | me.x;
+      const uint64_t u = (key >> kU) - u0;
+      const uint32_t s0 = ucnt[u], c = ucnt[u + 1] - s0;
+      uint32_t rank = 0;
+      for (uint32_t q = 0; q < c; q++) {
+        const uint4 o = ss.recb[p0 + s0 + q];
+        const uint64_t kq = ((uint64_t)o.y << 32) | o.x;
+        rank += (kq < key || (kq == key && o.z < me.z)) ? 1u : 0u;
+      }
+      const uint64_t pos = p0 + s0 + rank;
+      ss.off[pos] = key + off0;
+      ss.len[pos] = me.w;
+      ss.perm[pos] = me.z;
+    }
+  }
+  if (too_many && tid == 0) __hip_atomic_fetch_or(ss.sync + 2 + kSegSyncGroups, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+  sync();  // 6
+  if (__hip_atomic_load(ss.sync + 2 + kSegSyncGroups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return kSegFallback;  // a unit starting more than kSegSortMaxBucket records (every workgroup reads the flag)
   // P5: the plan of the sorted view (first_ev, the slots 0 .. G-1)
   seg_plan_body<kU>(base, ss.off, ss.len, n, max_units, wg, G, plan_bad, plan_gx, plan_conf, ss.fev, psh);
   sync();
@@ -2549,7 +2582,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
                                                             uint32_t *__restrict__ unit_raw, uint32_t *__restrict__ ev_h,
                                                             const DeviceTables *__restrict__ tables,
                                                             uint64_t max_units, uint32_t *__restrict__ ws,
-                                                            uint32_t sort_on, uint32_t sync_spins) {
+                                                            uint32_t sort_on, uint32_t sync_spins, uint32_t sort_uc) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
   __shared__ uint32_t s_next, s_ok;
   __shared__ SegRed red;
@@ -2595,8 +2628,8 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
   if (mode == kSegFallback && sort_on && gridDim.x <= kSegSortMaxWgs) {
     ss = seg_ws_layout(ws, n, max_units, true).ss;
     ss.spins = sync_spins;
-    mode = uni(seg_sort<kU>(base, offs, lens, n, max_units, ss, unit_raw, plan_bad, plan_gx, plan_conf, psh, red,
-                            s_ok));
+    ss.ucmax = sort_uc;
+    mode = uni(seg_sort<kU>(base, offs, lens, n, max_units, ss, lds, plan_bad, plan_gx, plan_conf, psh, red, s_ok));
     sorted = mode != kSegFallback;
     if (sorted && blockIdx.x == 0 && tid == 0) *flag = mode | kSegSortedBit;
   }
@@ -3058,7 +3091,8 @@ uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units, bool sort) {
 }
 
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
-                      uint32_t *taken, uint64_t grp_min, uint64_t sort_min, uint32_t sync_spins, uint32_t lg_chunk) {
+                      uint32_t *taken, uint64_t grp_min, uint64_t sort_min, uint32_t sync_spins, uint32_t sort_uc,
+                      uint32_t lg_chunk) {
   if (!b.base || !b.off || !b.len || !b.crc_out || !st || !ws || b.nblocks == 0 || !(b.flags & kFlagMessages))
     return hipErrorInvalidValue;
   const uint64_t n = b.nblocks;
@@ -3081,7 +3115,7 @@ hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_
   const uint32_t allow_grp = n >= grp_min ? 1u : 0u;
   hipLaunchKernelGGL(k_seg_stream<>, dim3(grid), dim3(kFastThreads), 0, s, b.base, b.off, b.len, n, lg_chunk,
                      w.plan_bad, w.plan_gx, w.plan_conf, plan_wgs, allow_grp, w.flag, w.first_ev, w.unit_raw, w.ev_h,
-                     b.tables, max_units, ws, sort ? 1u : 0u, sync_spins);
+                     b.tables, max_units, ws, sort ? 1u : 0u, sync_spins, sort_uc);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_seg_combine<>, dim3(grid), dim3(1024), 0, s, b.base, b.off, b.len, n, w.flag, w.unit_raw,
                      w.ev_h, b.crc_out, st, taken, b.flags, b.tables, w.ss.off, w.ss.len, w.ss.perm);

@@ -347,8 +347,8 @@ int hc_debug_seg_taken(void);
 /* The stream kernel's phase clock for this thread's last batch on the stream
  * (DESIGN.md 4.2b): 16 s_memrealtime stamps (100 MHz) of workgroup 0 -- [0]
  * start, [1] prologue done, [2] the sort's key range and residency check,
- * [3..9] its barriers after P0, P1, P2 (two), P3, P4, P5, [10] P6, [14] / [15]
- * the sorted view's stream body start / end (stale entries when no sort ran).
+ * [3..7] its barriers after A1, A2, A3, B, P5, [10] P6, [14] / [15] the sorted
+ * view's stream body start / end (stale entries when no sort ran).
  * Synchronizes that device (tools only). */
 int hc_debug_seg_prof(uint64_t *out16);
 
@@ -357,7 +357,7 @@ int hc_debug_seg_prof(uint64_t *out16);
  * race): HC_DEVICE, HC_SEG_MIN_MSGS, HC_COPY_THREADS, HC_WAL_MIN_RANGE,
  * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
  * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN, HC_SEG_MIN_BLOCKS, HC_SEG_SORT_MIN,
- * HC_SEG_SYNC_SPINS.  hc_debug_set changes one of them afterwards
+ * HC_SEG_SYNC_SPINS, HC_SEG_SORT_UC.  hc_debug_set changes one of them afterwards
  * (tests and tools); value NULL restores the compiled default.  HC_OK, or
  * HC_E_ARG for an unknown name.
  * HC_INJECT_FAIL (test hook) accepts "add_crcs", "read_from_disk" or

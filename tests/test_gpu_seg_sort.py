@@ -176,3 +176,32 @@ def test_repeated_calls_reuse_the_workspace(cuda, hc, oracle, buf_host):
             off, lens = off[p], lens[p]
         was = check(cuda, hc, oracle, host, buf, off, lens)
         assert was == ("sorted_packed" if perm else "packed"), (n, perm, was)
+
+
+@pytest.mark.parametrize("uc", ["64", "7"])
+def test_several_coarse_buckets_per_workgroup(cuda, hc, oracle, buf_host, knobs, uc):
+    """HC_SEG_SORT_UC (test hook) caps the units of a coarse bucket, so a span of
+    a few hundred MiB runs several buckets a workgroup (the path a span past
+    ~137 GB takes at the default cap): words and path as at the default."""
+    host, buf = buf_host
+    knobs.setenv("HC_SEG_SORT_UC", uc)
+    rng = np.random.default_rng(int(uc))
+    n = 40_000
+    lens = loguniform(rng, n)
+    off = packed(lens, 9)
+    p = rng.permutation(n)
+    check(cuda, hc, oracle, host, buf, off[p], lens[p], "sorted_packed")
+
+
+def test_too_many_records_in_one_unit(cuda, hc, oracle, buf_host):
+    """More than 1024 records starting in one 16 KiB unit (zero-length ones at one
+    start) stop the sort on every workgroup: k_crc_any's work, words exact."""
+    host, buf = buf_host
+    rng = np.random.default_rng(12)
+    n = 30_000
+    lens = loguniform(rng, n)
+    off = packed(lens, 0)
+    off2 = np.concatenate([off, np.full(1500, off[777], np.uint64)])
+    lens2 = np.concatenate([lens, np.zeros(1500, np.uint64)])
+    p = rng.permutation(len(off2))
+    check(cuda, hc, oracle, host, buf, off2[p], lens2[p], "fallback")

@@ -1,9 +1,10 @@
 """The sorted view's phase clock: config 5's records back to
 back, listed in a permuted order, through dev_crc32_blocks; per call the
 stream kernel's workgroup-0 stamps (hc_debug_seg_prof, microseconds from the
-kernel's start, each phase's END): prologue, key range + residency check, P0
-zero, P1 count, P2 scan (two barriers), P3 scatter, P4 rank, P5 plan, P6, the
-sorted stream body; and the words against an in-order run.
+kernel's start, each phase's END): prologue, key range + residency check, A1
+coarse histograms, A2 their scan, A3 the coarse scatter, B the per-bucket unit
+sort, P5 the plan of the sorted view, P6, the sorted stream body; and the words
+against an in-order run.
 
   python tools/sort_phase_probe.py [--records 2000000] [--calls 3]
 """
@@ -28,8 +29,8 @@ def main():
 
     from hunddb_amd import crc
 
-    stamps_at = {"prologue": 1, "range_resident": 2, "P0_zero": 3, "P1_count": 4, "P2a_scan": 5, "P2b_scan": 6,
-                 "P3_scatter": 7, "P4_rank": 8, "P5_plan": 9, "P6_mode": 10, "body_start": 14, "body_end": 15}
+    stamps_at = {"prologue": 1, "range_resident": 2, "A1_hist": 3, "A2_scan": 4, "A3_scatter": 5, "B_buckets": 6,
+                 "P5_plan": 7, "P6_mode": 10, "body_start": 14, "body_end": 15}
     for n in [int(x) for x in a.records.split(",")]:
         lens = record_sizes(n)
         off = np.zeros(n, dtype=np.uint64)
