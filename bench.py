@@ -248,14 +248,26 @@ def mixed_sizes(seed, lo, n):
 # CPU baseline (rank 0, N = 1): the reference's CPU path timed on the host cores
 def _rate(fn, nbytes, seconds):
     """GiB/s of fn() (nbytes per call) run back to back for >= seconds."""
+    return _rate_cpu(fn, nbytes, seconds, 1)[0]
+
+
+def _rate_cpu(fn, nbytes, seconds, threads):
+    """fn() (nbytes per call) run back to back for >= seconds: (wall-clock
+    GiB/s, GiB/s per `threads` CPUs of the process's CPU time, busy = CPU time
+    / (threads x wall)).  The host is shared: a slice's wall time also holds
+    the time other tenants' threads ran on the pinned CPUs (round 6,
+    tools/cpu_spread_probe.py: 16 threads were on a CPU 67-85 % of each slice,
+    and the wall-clock rate followed), which the process's CPU time leaves out."""
     fn()
-    t0, k = time.perf_counter(), 0
+    t0, c0, k = time.perf_counter(), time.process_time(), 0
     while True:
         fn()
         k += 1
         dt = time.perf_counter() - t0
         if dt >= seconds:
-            return k * nbytes / dt / 2**30
+            ct = time.process_time() - c0
+            gib = k * nbytes / 2**30
+            return gib / dt, gib / (ct / threads) if ct > 0 else float("nan"), ct / (threads * dt)
 
 
 def cgroup_cpu_quota():
@@ -370,24 +382,27 @@ def cgroup_throttled_us():
     return None
 
 
+CPU_REGION = 16 << 20  # the CPU baseline's timed set: the sample's first 16 MiB (cpu_baseline)
+CPU_CALL = 1 << 30     # ... listed over and over to 1 GiB a call
 WARM_AGREE = 0.05   # warm-up ends when two consecutive warm-up slices agree within 5 %
 WARM_CAP_S = 6.0    # ... or after this long (1.8 s did not reach steady state)
 
 
-def _slices(fn, nbytes, budget_s):
+def _slices(fn, nbytes, budget_s, threads):
     """N_SLICES timed slices of fn (0.08 of the budget each), separated by idle
     gaps of 0.1 s so that one burst of another tenant on the host lands in one
-    slice rather than in all of them; the median is the reported value.  Before
-    them an untimed warm-up of slices of the same length, until two consecutive
-    ones agree within WARM_AGREE (at most WARM_CAP_S): the host's cores ramp up
-    over seconds (round 5's first slices read 113-139 GiB/s, the rest 162-169).
-    Also returns how long the cgroup's CPU quota throttled the process in each
-    slice (the quota covers every thread of the container, not only the timed
-    ones), and the warm-up's slices and length."""
-    out, thr, warm = [], [], []
+    slice rather than in all of them; the median is the reported value.  Each
+    slice's rate is taken against the process's CPU time (_rate_cpu), its
+    wall-clock rate kept beside it.  Before them an untimed warm-up of slices of
+    the same length, until two consecutive ones agree within WARM_AGREE (at most
+    WARM_CAP_S): the host's cores ramp up over seconds (round 5's first slices
+    read 113-139 GiB/s, the rest 162-169).  Also returns how long the cgroup's
+    CPU quota throttled the process in each slice (the quota covers every thread
+    of the container, not only the timed ones), and the warm-up's slices."""
+    out, wall, busy, thr, warm = [], [], [], [], []
     t_warm = time.perf_counter()
     while time.perf_counter() - t_warm < WARM_CAP_S:
-        warm.append(_rate(fn, nbytes, 0.08 * budget_s))
+        warm.append(_rate_cpu(fn, nbytes, 0.08 * budget_s, threads)[1])
         if len(warm) >= 2 and abs(warm[-1] / warm[-2] - 1.0) <= WARM_AGREE:
             break
     warm_s = time.perf_counter() - t_warm
@@ -395,22 +410,38 @@ def _slices(fn, nbytes, budget_s):
         if k:
             time.sleep(0.1)
         t0 = cgroup_throttled_us()
-        out.append(_rate(fn, nbytes, 0.08 * budget_s))
+        w, c, b = _rate_cpu(fn, nbytes, 0.08 * budget_s, threads)
+        out.append(c)
+        wall.append(w)
+        busy.append(b)
         t1 = cgroup_throttled_us()
         thr.append(None if t0 is None or t1 is None else round((t1 - t0) / 1e3, 1))
     return out, thr, {"warmup_s": round(warm_s, 2), "warmup_slices": [round(x, 2) for x in warm],
-                      "warmup_converged": len(warm) >= 2 and abs(warm[-1] / warm[-2] - 1.0) <= WARM_AGREE}
+                      "warmup_converged": len(warm) >= 2 and abs(warm[-1] / warm[-2] - 1.0) <= WARM_AGREE,
+                      "wall": wall, "busy": busy}
 
 
 def _spread(sl, budget_s, threads):
     import numpy as np
-    slices, thr, warm = sl
-    med = float(np.median(slices))
+    slices, thr, info = sl
+    info = dict(info)
+    wall, busy = info.pop("wall"), info.pop("busy")
+    med, wmed = float(np.median(slices)), float(np.median(wall))
     return {"spread": [round(min(slices), 3), round(max(slices), 3)],
             "spread_pct": [round(100.0 * (min(slices) / med - 1.0), 1), round(100.0 * (max(slices) / med - 1.0), 1)],
             "slices": [round(x, 2) for x in slices],
+            "slices_busy": [round(x, 3) for x in busy],
+            "wall_clock": {"value": round(wmed, 3),
+                           "spread_pct": [round(100.0 * (min(wall) / wmed - 1.0), 1),
+                                          round(100.0 * (max(wall) / wmed - 1.0), 1)],
+                           "slices": [round(x, 2) for x in wall]},
             "slices_throttled_ms": thr,
-            **warm,
+            **info,
+            "rate_note": f"value and slices: GiB per {threads} CPUs of the process's CPU time (bytes / (CPU s / "
+                         f"{threads})), what {threads} cores of its own would do; the host is shared and "
+                         f"slices_busy (CPU time / ({threads} x wall)) shows the share of each slice the pinned "
+                         f"threads were on a CPU (round 6: 0.67-0.85, tools/cpu_spread_probe.py); wall_clock: the "
+                         f"same slices by the wall clock",
             "spread_note": f"min/max of {len(slices)} slices of {0.08 * budget_s:.2f} s on {threads} threads after "
                            f"an untimed warm-up of slices of the same length until two consecutive ones agreed "
                            f"within {100 * WARM_AGREE:.0f} % (cap {WARM_CAP_S:.0f} s; warmup_s, warmup_slices), "
@@ -463,32 +494,49 @@ def cpu_baseline(sample, off, lens, threads, budget_s, what, gpu_words=None, mes
     import numpy as np
 
     from oracle import oracle as O
-    nbytes = int(lens.sum(dtype=np.uint64))
-    if messages:
-        port = lambda t: O.crc32_messages(sample, off, lens, threads=t)  # noqa: E731
-    else:
-        port = lambda t: O.crc32_blocks(sample, off=off, lens=lens, threads=t)  # noqa: E731
-    words = port(threads)
+
+    def runner(o, ln):
+        if messages:
+            return lambda t: O.crc32_messages(sample, o, ln, threads=t)
+        return lambda t: O.crc32_blocks(sample, off=o, lens=ln, threads=t)
+    words = runner(off, lens)(threads)  # every word of the sample, against the GPU's
+    # The timed set: the sample's blocks (records) inside its first CPU_REGION
+    # bytes, listed over and over to CPU_CALL bytes a call -- cache-resident, as
+    # the reference's CRC runs on a block it has just read into a fresh buffer
+    # (block_manager.go:203-235) or just serialized (wal.go:261) -- and long
+    # enough a call to bury the port's per-call thread start.
+    o0 = int(off.min()) if len(off) else 0
+    inr = np.nonzero(off.astype(np.uint64) + lens.astype(np.uint64) <= np.uint64(o0 + CPU_REGION))[0]
+    rb = int(lens[inr].sum(dtype=np.uint64))
+    reps = max(1, -(-CPU_CALL // max(rb, 1)))
+    toff, tlen = np.tile(off[inr], reps), np.tile(lens[inr], reps)
+    nbytes = rb * reps
+    port = runner(toff, tlen)
     mv = memoryview(sample)
     skip = 0 if messages else 4
-    pairs = list(zip(off.tolist(), lens.tolist()))
+    pairs = list(zip(off[inr].tolist(), lens[inr].tolist()))
 
     def zl():
         for o, n_ in pairs:
             zlib.crc32(mv[o + skip:o + n_])
-    zl_ok = all(zlib.crc32(mv[o + skip:o + n_]) == int(words[k]) for k, (o, n_) in enumerate(pairs[:200]))
-    slices = _slices(lambda: port(threads), nbytes, budget_s)
-    one = _rate(lambda: port(1), nbytes, 0.2 * budget_s)
-    zrate = _rate(zl, nbytes, 0.2 * budget_s)
+    zl_ok = all(zlib.crc32(mv[o + skip:o + n_]) == int(words[inr[k]]) for k, (o, n_) in enumerate(pairs[:200]))
+    slices = _slices(lambda: port(threads), nbytes, budget_s, threads)
+    one = _rate_cpu(lambda: port(1), nbytes, 0.2 * budget_s, 1)[1]
+    zrate = _rate_cpu(zl, rb, 0.2 * budget_s, 1)[1]
+    nsb = int(lens.sum(dtype=np.uint64))
+    unit = "records" if messages else "blocks"
     res = {"value": round(float(np.median(slices[0])), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-           "sample": f"{what}: {len(pairs)} {'records' if messages else 'blocks'}, {nbytes / 2**20:.0f} MiB copied from the GPU batch; "
+           "sample": f"{what}: {len(off)} {unit}, {nsb / 2**20:.0f} MiB copied from the GPU batch (every word "
+                     f"checked against the GPU's); timed: its {len(inr)} {unit} in the first "
+                     f"{CPU_REGION >> 20} MiB ({rb / 2**20:.1f} MiB, cache-resident) listed {reps} times a call; "
                      f"oracle/hc_oracle.c oc_crc32_go_amd64 restates Go 1.23 hash/crc32 amd64 "
                      f"(PCLMULQDQ fold + slicing-by-8), pclmul={O.lib().oc_have_pclmul()}",
            **_spread(slices, budget_s, threads),
            "single_thread": round(one, 3),
            "zlib_single_thread": round(zrate, 3),
-           "zlib_note": f"system zlib {zlib.ZLIB_RUNTIME_VERSION} crc32 via Python, 1 thread; "
-                        f"same words as the oracle on the first 200 blocks: {zl_ok}"}
+           "zlib_note": f"system zlib {zlib.ZLIB_RUNTIME_VERSION} crc32 via Python, 1 thread, the timed region once "
+                        f"a call (both single-thread rates per CPU second); same words as the oracle on the "
+                        f"first 200 {unit}: {zl_ok}"}
     if gpu_words is not None:
         res["matches_gpu"] = bool(np.array_equal(words, gpu_words))
     res.update(cpu_host())
@@ -531,8 +579,8 @@ def cpu_baseline_framing(kind, dev_src, threads, budget_s, B=4096):
 
     def par():  # ctypes releases the GIL for the call
         list(pool.map(lambda t: run(t * per_t, (t + 1) * per_t), range(threads)))
-    slices = _slices(par, per_t * threads * (P + B), budget_s)
-    one = _rate(lambda: run(0, nblk), nbytes, 0.3 * budget_s)
+    slices = _slices(par, per_t * threads * (P + B), budget_s, threads)
+    one = _rate_cpu(lambda: run(0, nblk), nbytes, 0.3 * budget_s, 1)[1]
     pool.shutdown()
     return {"value": round(float(np.median(slices[0])), 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{what}, read+written bytes",

@@ -1716,12 +1716,12 @@ __device__ __forceinline__ void seg_plan_body(const uint8_t *base, const uint64_
     sh.gx = 0;
   }
   const uint64_t step = (uint64_t)nwg * blockDim.x;
-  // records k_crc_grp would take (the fallback's choice: k_seg_stream prologue)
+  // records k_crc_grp would take (the fallback's choice: k_seg_stream
+  // prologue), counted in the checking loop below and, past a thread's early
+  // stop, in a loop of their own (round 5 counted them in a first pass over
+  // the arrays: one more dependent round trip per record a thread)
   uint32_t conf = 0;
-  for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < n; j += step) {
-    const uint32_t l = lens[j];
-    conf += ((((uintptr_t)base + offs[j]) & 15u) == 0 && l && (l & 4095u) == 0) ? 1u : 0u;
-  }
+  auto grp_rec = [&](uint64_t s, uint32_t l) -> uint32_t { return (s & 15u) == 0 && l && (l & 4095u) == 0 ? 1u : 0u; };
   const SegGeo g = seg_geo<kU>(base, offs, lens, n);
   uint32_t bad = g.units > max_units || n >= 0x7FFFFFFFull || g.pend < g.a0 ? 15u : 0u;
   const uint64_t s0 = (uint64_t)base + offs[0];
@@ -1733,10 +1733,13 @@ __device__ __forceinline__ void seg_plan_body(const uint8_t *base, const uint64_
   // (out of order, overlapping, 65 of its n + 1 events -- record ends -- in a
   // group).  A thread stops when no mode is left.
   auto none_left = [](uint32_t b) { return (b & 1u) && (b & 2u) && (b & 12u); };
-  for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < n && !none_left(bad); j += step) {
+  uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x;
+  for (; j < n && !none_left(bad); j += step) {
     const uint64_t s = (uint64_t)base + offs[j], l = lens[j], e = s + l;
+    conf += grp_rec(s, (uint32_t)l);
     if (l > kSegMaxRecord || s < g.a0 || e > g.pend) {  // k_seg_combine's unit chain stays <= 1025 units
       bad = 15u;
+      j += step;
       break;
     }
     uint64_t ulo = 0;
@@ -1762,13 +1765,17 @@ __device__ __forceinline__ void seg_plan_body(const uint8_t *base, const uint64_
     }
     if (j >= 64 && grp(e) == grp((uint64_t)base + offs[j - 64] + lens[j - 64])) bad |= 8u;  // e_j vs e_{j-64}
     if (j == 63 && grp(e) == grp(s0)) bad |= 8u;  // e_63 vs s_0 (event 0)
-    if (none_left(bad)) break;
+    if (none_left(bad)) {
+      j += step;
+      break;
+    }
     const uint64_t us = (s - g.a0) >> kU, ue = (e - g.a0) >> kU;
     for (uint64_t u = ulo; u <= us; u++) first_ev[u] = (uint32_t)(2 * j);
     for (uint64_t u = us + 1; u <= ue; u++) first_ev[u] = (uint32_t)(2 * j + 1);
     if (j + 1 == n)
       for (uint64_t u = ue + 1; u <= g.units; u++) first_ev[u] = (uint32_t)(2 * n + 2);
   }
+  for (; j < n; j += step) conf += grp_rec((uint64_t)base + offs[j], lens[j]);  // past an early stop
   __syncthreads();
   if (bad) atomicOr(&sh.bad, bad);
   if (gx) atomicAdd(&sh.gx, (unsigned long long)gx);

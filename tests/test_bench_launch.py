@@ -88,6 +88,12 @@ def test_cpu_baseline_reports_cores_it_used(oracle):
     lo, hi = res["spread_pct"]
     assert lo <= 0.0 <= hi and res["matches_gpu"] is True
     assert "nproc" not in res
+    # rates per CPU second of the pinned threads, the wall clock beside them
+    assert len(res["slices"]) == len(res["slices_busy"]) == len(res["wall_clock"]["slices"]) == bench.N_SLICES
+    assert all(0.0 < b <= 1.5 for b in res["slices_busy"])
+    wlo, whi = res["wall_clock"]["spread_pct"]
+    assert wlo <= 0.0 <= whi and res["wall_clock"]["value"] > 0
+    assert "cache-resident" in res["sample"] and "listed" in res["sample"]
 
 
 def test_self_launch_parent_never_imports_torch_cuda():
