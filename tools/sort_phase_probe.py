@@ -29,7 +29,8 @@ def main():
 
     from hunddb_amd import crc
 
-    stamps_at = {"prologue": 1, "range_resident": 2, "A1_hist": 3, "A2_scan": 4, "A3_scatter": 5, "B_buckets": 6,
+    stamps_at = {"prologue": 1, "range_resident": 2, "A1_hist": 3, "A2_scan": 4, "A3_scatter": 5,
+                 "B1_count_wg0": 8, "B2_scan_wg0": 9, "B3_scatter_wg0": 11, "B4_rank_wg0": 12, "B_buckets": 6,
                  "P5_plan": 7, "P6_mode": 10, "body_start": 14, "body_end": 15}
     for n in [int(x) for x in a.records.split(",")]:
         lens = record_sizes(n)
