@@ -2140,7 +2140,8 @@ constexpr uint32_t kSegSortedBit = 8;        // the mode word of a sorted view: 
 // Phase clock of the last sort (hc_debug_seg_prof): workgroup 0's s_memrealtime
 // (100 MHz): [0] the stream's start, [1] its prologue, [2] the key range and
 // the residency check, [3..7] the sort's barriers (A1, A2, A3, B, P5), [10] P6,
-// [14] / [15] the sorted body's start / end.  One store each by one thread.
+// [14] / [15] the sorted body's start / end; inside B, workgroup 0's own bucket:
+// [8] counted, [9] scanned, [11] scattered, [12] ranked.  One store each by one thread.
 __device__ unsigned long long g_seg_prof[16];
 __device__ __forceinline__ void seg_prof(uint32_t k) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && k < 16) g_seg_prof[k] = __builtin_amdgcn_s_memrealtime();
@@ -2150,6 +2151,8 @@ constexpr uint32_t kSegSortMaxWgs = 1024;    // the stream's largest grid with a
 constexpr uint32_t kSegSortUcMax = 32768;    // units per coarse bucket: the LDS counters of phase B (128 KiB)
 constexpr uint32_t kSegSortNbcMax = 4096;    // coarse buckets (2 LDS words each in phase A)
 constexpr uint32_t kSegSyncAbort = 1u << 31;
+constexpr uint64_t kSegSortLdsWords = kFastLdsBytes / 4 + kFastWaves * 64;  // the stream's LDS, the sort's scratch
+static_assert(kSegSortUcMax + 1 <= kSegSortLdsWords, "phase B's unit counters fit the sort's LDS");
 
 // workspace (u32 words): the mode flag (64 words: word 0 the mode, words 1-18
 // the sort's barrier words), plan_bad[kSegPlanMaxWgs], plan_gx[kSegPlanMaxWgs]
@@ -2505,6 +2508,7 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
       ss.arr[p] = atomicAdd(&ucnt[(key >> kU) - u0], 1u);
     }
     __syncthreads();
+    seg_prof(8);
     {  // exclusive scan of ucnt[0 .. nu) in place; ucnt[nu] = the total
       const uint32_t per = (uint32_t)((nu + T - 1) / T);
       const uint64_t a0 = (uint64_t)tid * per, a1 = a0 + per < nu ? a0 + per : nu;
@@ -2524,6 +2528,7 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
       if (tid == 0) ucnt[nu] = tot;
     }
     __syncthreads();
+    seg_prof(9);
     if (too_many) continue;  // (workgroup-uniform; the grid learns it below)
     for (uint64_t p = p0 + tid; p < p0 + pc; p += T) {
       const uint4 r = ss.reca[p];
@@ -2531,22 +2536,47 @@ __device__ uint32_t seg_sort(const uint8_t *base, const uint64_t *__restrict__ o
       ss.recb[p0 + ucnt[(key >> kU) - u0] + ss.arr[p]] = r;
     }
     __syncthreads();
+    seg_prof(11);
+    // ranks: against LDS copies of the bucket's keys (from the bucket's first
+    // unit, 32 bits) and batch indices when they fit beside the unit counts,
+    // else against recb itself (one L2 round trip per record of the unit)
+    const uint64_t ub = u0 << kU;
+    uint32_t *kk = ucnt + nu + 1, *ii = kk + pc;
+    const bool in_lds = nu + 1 + 2 * pc <= kSegSortLdsWords;
+    if (in_lds) {
+      for (uint64_t p = tid; p < pc; p += T) {
+        const uint4 r = ss.recb[p0 + p];
+        kk[p] = (uint32_t)((((uint64_t)r.y << 32) | r.x) - ub);
+        ii[p] = r.z;
+      }
+      __syncthreads();
+    }
     for (uint64_t p = p0 + tid; p < p0 + pc; p += T) {
       const uint4 me = ss.recb[p];
       const uint64_t key = ((uint64_t)me.y << 32) | me.x;
       const uint64_t u = (key >> kU) - u0;
       const uint32_t s0 = ucnt[u], c = ucnt[u + 1] - s0;
       uint32_t rank = 0;
-      for (uint32_t q = 0; q < c; q++) {
-        const uint4 o = ss.recb[p0 + s0 + q];
-        const uint64_t kq = ((uint64_t)o.y << 32) | o.x;
-        rank += (kq < key || (kq == key && o.z < me.z)) ? 1u : 0u;
+      if (in_lds) {
+        const uint32_t mk = (uint32_t)(key - ub);
+        for (uint32_t q = 0; q < c; q++) {
+          const uint32_t kq = kk[s0 + q];
+          rank += (kq < mk || (kq == mk && ii[s0 + q] < me.z)) ? 1u : 0u;
+        }
+      } else {
+        for (uint32_t q = 0; q < c; q++) {
+          const uint4 o = ss.recb[p0 + s0 + q];
+          const uint64_t kq = ((uint64_t)o.y << 32) | o.x;
+          rank += (kq < key || (kq == key && o.z < me.z)) ? 1u : 0u;
+        }
       }
       const uint64_t pos = p0 + s0 + rank;
       ss.off[pos] = key + off0;
       ss.len[pos] = me.w;
       ss.perm[pos] = me.z;
     }
+    __syncthreads();
+    seg_prof(12);
   }
   if (too_many && tid == 0) __hip_atomic_fetch_or(ss.sync + 2 + kSegSyncGroups, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -2590,7 +2620,7 @@ __global__ __launch_bounds__(kFastThreads) void k_seg_stream(const uint8_t *base
                                                             const DeviceTables *__restrict__ tables,
                                                             uint64_t max_units, uint32_t *__restrict__ ws,
                                                             uint32_t sort_on, uint32_t sync_spins, uint32_t sort_uc) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kFastLdsBytes / 4 + kFastWaves * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kSegSortLdsWords];  // (the tables + the event slots)
   __shared__ uint32_t s_next, s_ok;
   __shared__ SegRed red;
   __shared__ SegPlanShared psh;
