@@ -342,7 +342,8 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
           // k_seg_combine runs k_crc_any's work over every message itself
           e = launch_seg(b, d.dseg, ws, mu, fast_grid, s, d.seg_last, (uint64_t)knob(kKnobSegGrpMin), sort_min,
                          (uint32_t)std::min<int64_t>(std::max<int64_t>(0, knob(kKnobSegSyncSpins)), 0xFFFFFFFF),
-                         (uint32_t)std::min<int64_t>(std::max<int64_t>(0, knob(kKnobSegSortUc)), 0xFFFFFFFF));
+                         (uint32_t)std::min<int64_t>(std::max<int64_t>(0, knob(kKnobSegSortUc)), 0xFFFFFFFF),
+                         (uint32_t)std::min<int64_t>(std::max<int64_t>(0, knob(kKnobSegLgChunk)), 12));
           seg = true;
         }
       }

@@ -127,9 +127,11 @@ constexpr uint64_t kSegSortMin = 1ull << 14;         // sort_min's default (HC_S
 constexpr uint32_t kSegSyncSpinsDefault = 1u << 17;
 // sort_uc (test hook; 0 = the default, 32768) bounds the units of one coarse
 // bucket of the sort, so that small spans can run several buckets a workgroup.
+// the stream's chunk slot: 2^3 units of 16 KiB (HC_SEG_LG_CHUNK; round 6 sweep)
+constexpr uint32_t kSegLgChunk = 3;
 hipError_t launch_seg(const Batch &b, const SegTables *st, uint32_t *ws, uint64_t max_units, int grid, hipStream_t s,
                       uint32_t *taken = nullptr, uint64_t grp_min = kSegGrpFallbackMin, uint64_t sort_min = 0,
-                      uint32_t sync_spins = kSegSyncSpinsDefault, uint32_t sort_uc = 0, uint32_t lg_chunk = 7);
+                      uint32_t sync_spins = kSegSyncSpinsDefault, uint32_t sort_uc = 0, uint32_t lg_chunk = kSegLgChunk);
 // A uniform block batch (no off/len arrays) that k_crc_grp refuses (lengths not
 // a 4 KiB multiple, or not 16-B aligned), ulen >= 4, stride >= ulen: its
 // messages block[4:ulen] written out as off/len arrays, launch_seg over them

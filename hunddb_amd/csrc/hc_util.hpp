@@ -51,6 +51,7 @@ enum Knob : int {
   kKnobSegSortMin,     // HC_SEG_SORT_MIN: records from which an unsorted batch is sorted for the stream (2^14; 0 never)
   kKnobSegSyncSpins,   // HC_SEG_SYNC_SPINS: test hook, the sort's residency-check bound in polls (2^17)
   kKnobSegSortUc,      // HC_SEG_SORT_UC: test hook, units per coarse bucket of the sort at most (0: 32768)
+  kKnobSegLgChunk,     // HC_SEG_LG_CHUNK: tuning, log2 of the stream's units per chunk slot (3: 128 KiB; 0-12)
   kKnobCount
 };
 struct KnobDef {
@@ -66,6 +67,7 @@ inline constexpr KnobDef kKnobDefs[kKnobCount] = {
     {"HC_FORCE_GPU", 0},       {"HC_INJECT_FAIL", 0},
     {"HC_SEG_GRP_MIN", 1 << 18}, {"HC_SEG_MIN_BLOCKS", 4096},
     {"HC_SEG_SORT_MIN", 1 << 14}, {"HC_SEG_SYNC_SPINS", 1 << 17}, {"HC_SEG_SORT_UC", 0},
+    {"HC_SEG_LG_CHUNK", 3},
 };
 // HC_INJECT_FAIL sites, as knob values (site | 16 for :nomem)
 enum : int64_t { kInjectAddCrcs = 1, kInjectReadFromDisk = 2, kInjectWalReplay = 3, kInjectNomem = 16 };

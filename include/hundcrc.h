@@ -357,7 +357,7 @@ int hc_debug_seg_prof(uint64_t *out16);
  * race): HC_DEVICE, HC_SEG_MIN_MSGS, HC_COPY_THREADS, HC_WAL_MIN_RANGE,
  * HC_ADD_CRCS_GPU_MIN_BLOCKS, HC_READ_GPU_MIN_BLOCKS, HC_WAL_GPU_MIN_BLOCKS,
  * HC_FORCE_GPU, HC_INJECT_FAIL, HC_SEG_GRP_MIN, HC_SEG_MIN_BLOCKS, HC_SEG_SORT_MIN,
- * HC_SEG_SYNC_SPINS, HC_SEG_SORT_UC.  hc_debug_set changes one of them afterwards
+ * HC_SEG_SYNC_SPINS, HC_SEG_SORT_UC, HC_SEG_LG_CHUNK.  hc_debug_set changes one of them afterwards
  * (tests and tools); value NULL restores the compiled default.  HC_OK, or
  * HC_E_ARG for an unknown name.
  * HC_INJECT_FAIL (test hook) accepts "add_crcs", "read_from_disk" or
