@@ -2278,16 +2278,6 @@ struct SegRed {
   uint32_t w[kFastWaves], w2[kFastWaves];
   unsigned long long q[kFastWaves];
 };
-__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, SegRed &r) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-  if ((threadIdx.x & 63u) == 0) r.w[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-  for (uint32_t k = 0; k < (blockDim.x >> 6); k++) t += r.w[k];
-  __syncthreads();
-  return t;
-}
 __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, SegRed &r) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
@@ -2862,14 +2852,49 @@ __global__ __launch_bounds__(1024) void k_seg_combine(const uint8_t *base, const
             const uint32_t sa = (uint32_t)xa[p] & 3u;
             const uint64_t Bq = (xa[p] - 4u * nw) & ~3ull;
             uint32_t D[kSegSmallGap / 4 + 1];
+            if (nwmax <= 5) {
+              // gaps of <= 20 B (WAL headers: 17): the dwords from <= 3 aligned
+              // 16-B loads, C0 = the chunk holding the first dword with gap bytes,
+              // a chunk loaded only when it holds a dword the loop below reads
+              // (six dword loads a record took 98.6 us of combine at 2M records,
+              // these 82.8: the gap reads are bound by their instruction count,
+              // profiles/r6/r6u/)
+              const uint64_t i0 = gp > Bq ? (gp - Bq) >> 2 : 0;  // first dword with gap bytes
+              const uint64_t a0w = Bq + 4u * i0, C0 = a0w & ~15ull;
+              const uint32_t ilast = sa ? nw : nw - 1;             // last dword read
+              const uint64_t alast = Bq + 4u * ilast;
+              uint32_t Q[12];
   #pragma unroll
-            for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
-              D[i] = 0;
-              if (i > nwmax) continue;
-              const uint64_t ai = Bq + 4u * i;
-              if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
-                D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
-                if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
+              for (int k = 0; k < 3; k++) {
+                const uint64_t ck = C0 + 16u * k;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (nw && ck <= alast) v = *reinterpret_cast<const uint4 *>(geo.a0 + ck);
+                Q[4 * k] = v.x; Q[4 * k + 1] = v.y; Q[4 * k + 2] = v.z; Q[4 * k + 3] = v.w;
+              }
+  #pragma unroll
+              for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
+                D[i] = 0;
+                if (i > 5) continue;
+                const uint64_t ai = Bq + 4u * i;
+                if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
+                  const uint32_t qi = (uint32_t)(((int64_t)ai - (int64_t)C0) >> 2);
+                  uint32_t v = 0;
+  #pragma unroll
+                  for (uint32_t t = 0; t < 12; t++) v = qi == t ? Q[t] : v;
+                  D[i] = v;
+                  if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
+                }
+              }
+            } else {
+  #pragma unroll
+              for (uint32_t i = 0; i <= kSegSmallGap / 4; i++) {
+                D[i] = 0;
+                if (i > nwmax) continue;
+                const uint64_t ai = Bq + 4u * i;
+                if (i <= nw && ai + 4u > gp && (i < nw || sa)) {
+                  D[i] = *reinterpret_cast<const uint32_t *>(geo.a0 + ai);
+                  if (ai < gp) D[i] &= ~0u << (8u * (uint32_t)(gp - ai));
+                }
               }
             }
             uint32_t r = 0;
