@@ -63,6 +63,28 @@ def test_seg_log_uniform_records(cuda, hc, oracle, seg_all, start):
     assert "k_seg_stream" in hc.last_launch()["kernel"]
 
 
+@pytest.mark.parametrize("lg", ["0", "1", "5", "7", "12"])
+def test_seg_chunk_slots(cuda, hc, oracle, seg_all, knobs, lg):
+    """HC_SEG_LG_CHUNK: the stream deals its 16 KiB units to the workgroups in
+    round-robin slots of 2^lg units (default 3, round 6; 0: one unit a slot; 12
+    is cut down until every workgroup has 4 slots).  Packed, 17-B gapped and
+    permuted (sorted view) batches stay bit-exact at other slot sizes."""
+    torch = cuda
+    knobs.setenv("HC_SEG_LG_CHUNK", lg)
+    rng = np.random.default_rng(int(lg) + 91)
+    n = 60_000
+    lens = (64.0 * np.exp(rng.random(n) * np.log(1024.0))).astype(np.uint64)
+    off = packed(lens, 3)
+    goff = gapped(lens, np.full(n, 17, dtype=np.uint64), 7)
+    total = int(goff[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    buf = torch.from_numpy(host).cuda()
+    check(torch, hc, oracle, host, buf, off, lens, "packed")
+    check(torch, hc, oracle, host, buf, goff, lens, "gapped")
+    p = rng.permutation(n)
+    check(torch, hc, oracle, host, buf, off[p], lens[p], "sorted_packed")
+
+
 def test_seg_boundaries_and_shapes(cuda, hc, oracle, seg_all):
     """Records ending exactly on row / group / unit boundaries, empty records,
     records of 64 B .. 1 MiB (spanning many units), one record, two records."""
