@@ -88,8 +88,8 @@ WORKLOADS = {
     # the plan finds them unsorted, so the stream refuses them
     "records_shuffled": (2_000_000, "records_shuffled", "weak"),
     # uniform blocks k_crc_grp refuses (config.go:241 allows any BlockSize >= 1024): 1M x 4092 B
-    # (k_crc_any: the route it wins, hc_api.cpp seg_blocks_preferred) and 0.5M x 8188 B (their
-    # messages block[4:] on the stream's small-gap mode, launch_seg_blocks; round 5)
+    # and 0.5M x 8188 B, their messages block[4:] on the stream's small-gap mode
+    # (launch_seg_blocks; round 5; 4-B aligned 2-8 KiB blocks stayed on k_crc_any until round 6)
     "blocks4092": (1_000_000, 4092, "weak"),
     "blocks8188": (500_000, 8188, "weak"),
 }

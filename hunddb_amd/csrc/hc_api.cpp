@@ -236,19 +236,14 @@ uint32_t *seg_cached_ws(DeviceState &d, hipStream_t s, uint64_t need, std::uniqu
 // (launch_seg_blocks); k_crc_any ran them at 57-62 % (round 4).
 uint64_t seg_min_blocks() { return (uint64_t)std::max<int64_t>(1, knob(kKnobSegMinBlocks)); }
 // The stream against k_crc_any over 4 GiB of uniform blocks, same buffers,
-// alternating routes (tools/seg_blocks_sweep.py, profiles/r5/r5m/sweep.jsonl,
-// TB/s): 1020 B 2.5 / 2.8, 2044 3.7 / 4.1, 4092 5.46 / 5.43, 6000 6.15 / 6.01,
-// 8188 5.76 / 6.20, 12000 5.69 / 6.28, 16380 5.18 / 6.34, 65532 6.40 / 6.48;
-// at an address that is not 4-B aligned 4092 5.02 / 5.42, 4096 5.19 / 5.45,
-// 8192 5.00 / 6.05.  k_crc_any keeps 4-B aligned blocks of 2-8 KiB.
-// A uniform whole-message batch (HC_F_MESSAGES, messages of ulen at base +
-// j * stride) is the same stream work as blocks of ulen + 4 bytes at base - 4.
-bool seg_blocks_preferred(const uint8_t *base, uint64_t stride, uint32_t ulen, bool msg = false) {
-  const uintptr_t b = reinterpret_cast<uintptr_t>(base) - (msg ? 4u : 0u);
-  const uint64_t l = (uint64_t)ulen + (msg ? 4u : 0u);
-  const bool aligned4 = ((b | stride) & 3u) == 0;
-  return !(aligned4 && l > 2048 && l < 8000);
-}
+// alternating routes (tools/seg_blocks_sweep.py, TB/s, k_crc_any / stream).
+// Round 5 (profiles/r5/r5m/, the stream's 2 MiB chunk slots): 2044 B 3.7 / 4.1,
+// 4092 5.46 / 5.43, 6000 6.15 / 6.01 -- k_crc_any kept 4-B aligned blocks of
+// 2-8 KiB.  Round 6 (profiles/r6/r6z/, 128 KiB slots): 1020 B 2.45-2.60 /
+// 2.86-2.94, 2044 3.47-4.11 / 4.18-4.30, 4092 5.36-5.40 / 5.52-5.54, 6000
+// 6.18 / 6.18-6.19, 8188 5.80 / 6.27, 16380 5.18 / 6.39-6.41, 65532 6.37 /
+// 6.48-6.49; not 4-B aligned 4092 5.08 / 5.57, 8192 5.02-5.05 / 6.21-6.24:
+// every length goes to the stream.
 
 // The span bound of a batch at `base` (the allocation holding it), as k_seg_*'s unit count; 0 if unknown.
 uint64_t seg_units_for(const uint8_t *base) {
@@ -307,9 +302,7 @@ int dispatch(int dev, const uint8_t *base, const uint64_t *off, const uint32_t *
       e = launch_fast(b, fast_grid, s);
       info.fast_blocks = n;
     } else if (seg_ok && ulen >= 4 && stride >= ulen && n >= seg_min_blocks() && n < 0x7FFFFFFFull &&
-               (!(flags & kFlagMessages) || crc_out) &&
-               seg_blocks_preferred(base, stride, ulen, (flags & kFlagMessages) != 0) &&
-               seg_blocks(d, b, s, fast_grid, e)) {
+               (!(flags & kFlagMessages) || crc_out) && seg_blocks(d, b, s, fast_grid, e)) {
       info.kernel = "k_seg_plan+k_seg_stream+k_seg_combine";
       info.fast_blocks = n;
       t_seg_dev = dev;

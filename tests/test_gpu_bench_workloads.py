@@ -31,7 +31,7 @@ CASES = {
     # gated k_crc_grp launch moves the bytes (name that kernel)
     "records4k_shuffled": (300_000, "k_crc_grp", 300_000 * (4096 + 4)),
     "records_shuffled": (4096, None, None),                   # unsorted records: the stream refuses them
-    "blocks4092": (4096, "k_crc_any", 4096 * 4092),           # 4-B aligned 4092-B blocks stay on k_crc_any
+    "blocks4092": (4096, "k_seg_stream", 4096 * 4092),        # the message stream (round 6; k_crc_any before)
     "blocks8188": (4096, None, 4096 * 8188),                  # the message stream (launch_seg_blocks)
 }
 

@@ -21,11 +21,6 @@ def seg_blocks(knobs):
     knobs.setenv("HC_SEG_MIN_BLOCKS", "1")  # every size below is offered to the stream
 
 
-def preferred(ptr, stride, ulen):
-    """hc_api.cpp seg_blocks_preferred: k_crc_any keeps 4-B aligned 2-8 KiB blocks"""
-    return not ((ptr | stride) & 3 == 0 and 2048 < ulen < 8000)
-
-
 def u32(t):
     return t.cpu().numpy().view(np.uint32)
 
@@ -44,7 +39,7 @@ def run(torch, hc, buf, n, stride, ulen, flags=0, verify=False):
 
 CASES = [  # (ulen, stride - ulen, start, path; None: as the plan's restatement says)
     (4092, 0, 0, "gapped"),       # config.go:241's non-4 KiB BlockSize, back to back: 4-B gaps (the stored
-    (4092, 0, 3, "gapped"),       # words); aligned, they stay on k_crc_any (seg_blocks_preferred)
+    (4092, 0, 3, "gapped"),       # words); aligned too since round 6 (k_crc_any kept them before)
     (4096, 0, 1, "gapped"),       # 4 KiB blocks at an odd address (k_crc_grp needs 16-B alignment)
     (1000, 0, 0, "gapped"),
     (5000, 24, 2, "gapped"),      # 28-B gaps
@@ -74,8 +69,6 @@ def test_uniform_blocks_on_the_stream(seg_blocks, cuda, hc, oracle, ulen, extra,
     moff = np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(4)
     want_path = expected_path(view.data_ptr(), moff, np.full(n, ulen - 4, np.uint64)) or "fallback"
     assert path is None or path == want_path
-    if not preferred(view.data_ptr(), stride, ulen):
-        want_path = "fallback"  # not offered to the stream
     assert hc.seg_path() == want_path
 
 
@@ -133,7 +126,7 @@ MSG_CASES = [  # (ulen, stride - ulen, start): uniform HC_F_MESSAGES batches k_c
     (1000, 3, 1),    # odd address, 3-B gaps
     (4096, 0, 1),    # 4 KiB messages at an odd address
     (8190, 2, 2),    # 8 KiB-ish, 2-B gaps
-    (4000, 96, 0),   # 4-B aligned 4004-B equivalent blocks: kept on k_crc_any (seg_blocks_preferred)
+    (4000, 96, 0),   # 4-B aligned 4004-B equivalent blocks (k_crc_any's until round 6)
     (5, 11, 3),      # tiny messages
 ]
 
@@ -158,7 +151,7 @@ def test_uniform_messages_route(cuda, hc, oracle, ulen, extra, start):
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (bad[:8], got[bad[:8]], want[bad[:8]])
     ptr = view.data_ptr()
-    if not preferred(ptr - 4, stride, ulen + 4) or ulen < 4:
+    if ulen < 4:
         assert hc.last_launch()["kernel"] == "k_crc_any"
     else:
         assert hc.last_launch()["kernel"].startswith("k_seg_plan")
