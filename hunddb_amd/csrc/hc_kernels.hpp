@@ -119,7 +119,10 @@ hipError_t launch_merkle_levels(uint8_t *levels16, uint64_t n, hipStream_t s);
 uint64_t seg_max_units(uint64_t span_bound);
 uint64_t seg_workspace_bytes(uint64_t n, uint64_t max_units, bool sort = false);
 constexpr uint64_t kSegGrpFallbackMin = 1ull << 18;  // grp_min's default (HC_SEG_GRP_MIN)
-constexpr uint64_t kSegSortMin = 1ull << 14;         // sort_min's default (HC_SEG_SORT_MIN)
+// sort_min's default (HC_SEG_SORT_MIN): the sorted view's fixed cost (its grid barriers,
+// ~170 us) against k_crc_any's work on permuted config-5 records broke even near 2^18
+// records (0.594 vs 0.585 ms; 16k: 0.257 vs 0.085, 1M: 1.71 vs 2.02; profiles/r6/r6bb/)
+constexpr uint64_t kSegSortMin = 1ull << 18;
 // taken (optional, device word): 1 packed, 2 gapped, 3 k_crc_grp fallback,
 // 4 small gaps, 0 k_crc_any fallback; | 8 when the stream ran on the sorted view.
 // sync_spins bounds the sort's first grid barrier, the check that the grid is

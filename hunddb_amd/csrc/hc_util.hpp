@@ -48,7 +48,7 @@ enum Knob : int {
   kKnobInject,         // HC_INJECT_FAIL=<site>[:nomem]: test mode, a named GPU batch fails (0 = none)
   kKnobSegGrpMin,      // HC_SEG_GRP_MIN: records from which a refused batch may take k_crc_grp (2^18)
   kKnobSegMinBlocks,   // HC_SEG_MIN_BLOCKS: uniform device block batches k_crc_grp refuses go to k_seg_* (4096)
-  kKnobSegSortMin,     // HC_SEG_SORT_MIN: records from which an unsorted batch is sorted for the stream (2^14; 0 never)
+  kKnobSegSortMin,     // HC_SEG_SORT_MIN: records from which an unsorted batch is sorted for the stream (2^18; 0 never)
   kKnobSegSyncSpins,   // HC_SEG_SYNC_SPINS: test hook, the sort's residency-check bound in polls (2^17)
   kKnobSegSortUc,      // HC_SEG_SORT_UC: test hook, units per coarse bucket of the sort at most (0: 32768)
   kKnobSegLgChunk,     // HC_SEG_LG_CHUNK: tuning, log2 of the stream's units per chunk slot (3: 128 KiB; 0-12)
@@ -66,7 +66,7 @@ inline constexpr KnobDef kKnobDefs[kKnobCount] = {
     {"HC_WAL_GPU_MIN_BLOCKS", (int64_t)kWalGpuMinBlocks},
     {"HC_FORCE_GPU", 0},       {"HC_INJECT_FAIL", 0},
     {"HC_SEG_GRP_MIN", 1 << 18}, {"HC_SEG_MIN_BLOCKS", 4096},
-    {"HC_SEG_SORT_MIN", 1 << 14}, {"HC_SEG_SYNC_SPINS", 1 << 17}, {"HC_SEG_SORT_UC", 0},
+    {"HC_SEG_SORT_MIN", 1 << 18}, {"HC_SEG_SYNC_SPINS", 1 << 17}, {"HC_SEG_SORT_UC", 0},
     {"HC_SEG_LG_CHUNK", 3},
 };
 // HC_INJECT_FAIL sites, as knob values (site | 16 for :nomem)

@@ -74,9 +74,9 @@ def test_gapped_messages_all_window_sizes(cuda, hc, oracle, n):
     out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
     hc.dev_crc32_blocks(buf, out, off=doff, lens=dlen, nblocks=n, flags=hc.HC_F_MESSAGES)
     torch.cuda.synchronize()
-    # one record is packed: the stream takes it; from HC_SEG_SORT_MIN records the
-    # permuted batch is sorted and the stream takes the sorted view (round 6)
-    if n >= 1 << 14:
+    # one record is packed: the stream takes it; from HC_SEG_SORT_MIN records (2^18)
+    # the permuted batch is sorted and the stream takes the sorted view (round 6)
+    if n >= 1 << 18:
         from test_gpu_seg_sort import sorted_path
         assert hc.seg_path() == sorted_path(buf.data_ptr(), off, lens)
     else:

@@ -71,6 +71,7 @@ def test_seg_chunk_slots(cuda, hc, oracle, seg_all, knobs, lg):
     permuted (sorted view) batches stay bit-exact at other slot sizes."""
     torch = cuda
     knobs.setenv("HC_SEG_LG_CHUNK", lg)
+    knobs.setenv("HC_SEG_SORT_MIN", "16384")  # the permuted case below is sorted
     rng = np.random.default_rng(int(lg) + 91)
     n = 60_000
     lens = (64.0 * np.exp(rng.random(n) * np.log(1024.0))).astype(np.uint64)

@@ -1,5 +1,6 @@
 """The sorted view (round 6): a whole-message
-batch listed out of order, from HC_SEG_SORT_MIN records (2^14), is sorted by
+batch listed out of order, from HC_SEG_SORT_MIN records (2^18; 2^14 in these
+tests, through the knob, so that the small cases stay cheap), is sorted by
 record start inside k_seg_stream (grid barriers), planned again and streamed in
 that order; k_seg_combine writes every word through the permutation.  Every
 word against the oracle's GetCRC per record (crc_util.go:15-17), and the path
@@ -13,7 +14,13 @@ from test_gpu_seg import expected_path, gapped, packed, u32
 
 pytestmark = pytest.mark.gpu
 
-SORT_MIN = 1 << 14
+SORT_MIN = 1 << 14      # these tests' threshold (HC_SEG_SORT_MIN, set below)
+DEFAULT_SORT_MIN = 1 << 18  # the library's (hc_kernels.hpp kSegSortMin)
+
+
+@pytest.fixture(autouse=True)
+def _sort_from_16k(knobs):
+    knobs.setenv("HC_SEG_SORT_MIN", str(SORT_MIN))
 
 
 def run(torch, hc, buf, off, lens):
@@ -140,6 +147,23 @@ def test_below_threshold_and_disabled(cuda, hc, oracle, buf_host, knobs):
     check(cuda, hc, oracle, host, buf, off[p], lens[p], "sorted_packed")
     knobs.setenv("HC_SEG_SORT_MIN", "0")
     check(cuda, hc, oracle, host, buf, off[p], lens[p], "fallback")
+
+
+def test_default_threshold(cuda, hc, oracle, buf_host, knobs):
+    """At the library's own threshold (2^18 records: where the sorted view's fixed
+    cost meets k_crc_any's, profiles/r6/r6bb/) a permuted batch one record short
+    of it stays on k_crc_any; one at it is sorted."""
+    host, buf = buf_host
+    knobs.delenv("HC_SEG_SORT_MIN", raising=False)
+    rng = np.random.default_rng(44)
+    n = DEFAULT_SORT_MIN
+    lens = loguniform(rng, n, span=64.0)
+    off = packed(lens, 1)
+    assert int(off[-1] + lens[-1]) <= host.size
+    p = rng.permutation(n)
+    check(cuda, hc, oracle, host, buf, off[p], lens[p], "sorted_packed")
+    q = p[p != n - 1]  # the same records less the last: one short of the threshold
+    check(cuda, hc, oracle, host, buf, off[q], lens[q], "fallback")
 
 
 def test_residency_check_abort_falls_back(cuda, hc, oracle, buf_host, knobs):
